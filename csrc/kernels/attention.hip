@@ -1,0 +1,350 @@
+// K1 / K2: paged attention for gfx950 on MFMA (v_mfma_f32_16x16x32_bf16).
+//
+// Formulation ("swapped" S^T = K * Q^T, guide §5.5 T12 / §3 acc-as-operand):
+//   * a wave owns 16 query COLUMNS (decode: the G query heads sharing one KV
+//     head; prefill: 16 consecutive query tokens of one head);
+//   * per 32-token unit it computes two 16x16 S^T tiles with K as the A operand
+//     loaded straight from the token-major K cache (16 B per lane), so each lane
+//     ends up with 4 tokens x 1 query column per tile;
+//   * the softmax is column-wise: lane-local over 8 values + 2 xor-shuffles;
+//   * the S^T accumulators ARE the B operand of the P*V MFMA (O^T = V^T P^T):
+//     element j of lane-group g <-> token 4g+j (tile 0) / 16+4g+j-4 (tile 1),
+//     and the dim-major V^T cache gives the matching A operand as two 8-B loads
+//     (4 consecutive tokens each) per 16-row d-tile -- no LDS transpose at all.
+// Decode splits a sequence's context into P partitions (grid.z) so that small
+// batches still fill 256 CUs; a reduce kernel merges (m, l, O) partials.
+#include "eia_common.h"
+
+#define NEG_INF (-INFINITY)
+
+template <int D>
+struct WaveAcc {
+  f32x4 o[D / 16];   // O^T tiles: lane holds rows d = 16*dt + 4*g + i, column c
+  float m;           // running max (log2 domain) of this lane's column
+  float l;           // lane-partial running sum
+};
+
+template <int D>
+EIA_DEV void wave_acc_init(WaveAcc<D>& a) {
+#pragma unroll
+  for (int dt = 0; dt < D / 16; ++dt) a.o[dt] = (f32x4){0.f, 0.f, 0.f, 0.f};
+  a.m = NEG_INF;
+  a.l = 0.f;
+}
+
+// Process tokens [tb, tb+32) of one sequence for one wave.
+//   qf      : Q^T B-operand fragments (pre-loaded)
+//   q_abs   : absolute position of this lane's query column (INT_MAX: no causal mask)
+//   kv_lo   : first token this lane's column may attend to (sliding window / chunk)
+template <int D>
+EIA_DEV void attn_unit(WaveAcc<D>& acc, const bf16x8 (&qf)[D / 32],
+                       const bf16_t* __restrict__ kc, const bf16_t* __restrict__ vc,
+                       const int* __restrict__ bt, int tb, int L, int kvh, int Hkv, int bs,
+                       float scale_log2, int q_abs, int kv_lo) {
+  const int lane = threadIdx.x & 63;
+  const int c = lane & 15, g = lane >> 4;
+  const bool has1 = (tb + 16) < L;
+  const long head_stride_k = (long)bs * D;
+  const int blk0 = bt[tb / bs];
+  const int blk1 = has1 ? bt[(tb + 16) / bs] : blk0;
+  const int offt0 = tb % bs;
+  const int offt1 = has1 ? (tb + 16) % bs : offt0;
+
+  f32x4 s0 = {0.f, 0.f, 0.f, 0.f}, s1 = {0.f, 0.f, 0.f, 0.f};
+  {
+    const bf16_t* kp0 = kc + ((long)blk0 * Hkv + kvh) * head_stride_k + (long)(offt0 + c) * D + 8 * g;
+    const bf16_t* kp1 = kc + ((long)blk1 * Hkv + kvh) * head_stride_k + (long)(offt1 + c) * D + 8 * g;
+    bf16x8 ka[D / 32], kb[D / 32];
+#pragma unroll
+    for (int s = 0; s < D / 32; ++s) ka[s] = *reinterpret_cast<const bf16x8*>(kp0 + 32 * s);
+    if (has1) {
+#pragma unroll
+      for (int s = 0; s < D / 32; ++s) kb[s] = *reinterpret_cast<const bf16x8*>(kp1 + 32 * s);
+    }
+#pragma unroll
+    for (int s = 0; s < D / 32; ++s) s0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ka[s], qf[s], s0, 0, 0, 0);
+    if (has1) {
+#pragma unroll
+      for (int s = 0; s < D / 32; ++s) s1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kb[s], qf[s], s1, 0, 0, 0);
+    }
+  }
+  // issue the V loads early (independent of the softmax)
+  const bf16_t* vp0 = vc + ((long)blk0 * Hkv + kvh) * (long)D * bs + offt0 + 4 * g;
+  const bf16_t* vp1 = vc + ((long)blk1 * Hkv + kvh) * (long)D * bs + offt1 + 4 * g;
+  bf16x4 vlo[D / 16], vhi[D / 16];
+#pragma unroll
+  for (int dt = 0; dt < D / 16; ++dt) {
+    const long d = 16 * dt + c;
+    vlo[dt] = *reinterpret_cast<const bf16x4*>(vp0 + d * bs);
+    vhi[dt] = *reinterpret_cast<const bf16x4*>(vp1 + d * bs);
+  }
+
+  float v[8];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int t0 = tb + 4 * g + i, t1 = tb + 16 + 4 * g + i;
+    const bool ok0 = (t0 < L) && (t0 <= q_abs) && (t0 >= kv_lo);
+    const bool ok1 = (t1 < L) && (t1 <= q_abs) && (t1 >= kv_lo);
+    v[i] = ok0 ? s0[i] * scale_log2 : NEG_INF;
+    v[4 + i] = ok1 ? s1[i] * scale_log2 : NEG_INF;
+  }
+  float mloc = v[0];
+#pragma unroll
+  for (int i = 1; i < 8; ++i) mloc = fmaxf(mloc, v[i]);
+  mloc = fmaxf(mloc, __shfl_xor(mloc, 16, 64));
+  mloc = fmaxf(mloc, __shfl_xor(mloc, 32, 64));
+  const float mnew = fmaxf(acc.m, mloc);
+  const float muse = (mnew == NEG_INF) ? 0.f : mnew;
+  const float alpha = exp2f(acc.m - muse);
+  bf16x8 pb;
+  float psum = 0.f;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const float p = exp2f(v[i] - muse);
+    const bf16_t pbf = f2bf(p);
+    pb[i] = pbf;
+    psum += bf2f(pbf);     // normalise with exactly the weights fed to the MFMA
+  }
+  acc.l = acc.l * alpha + psum;
+  acc.m = mnew;
+  if (!__all(alpha == 1.f)) {
+#pragma unroll
+    for (int dt = 0; dt < D / 16; ++dt) acc.o[dt] *= alpha;
+  }
+#pragma unroll
+  for (int dt = 0; dt < D / 16; ++dt) {
+    bf16x8 a;
+    a[0] = vlo[dt][0]; a[1] = vlo[dt][1]; a[2] = vlo[dt][2]; a[3] = vlo[dt][3];
+    a[4] = vhi[dt][0]; a[5] = vhi[dt][1]; a[6] = vhi[dt][2]; a[7] = vhi[dt][3];
+    acc.o[dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, pb, acc.o[dt], 0, 0, 0);
+  }
+}
+
+// ---------------------------------------------------------------------------------- decode
+
+template <int D>
+__global__ void __launch_bounds__(256)
+paged_decode_kernel(const bf16_t* __restrict__ q, long q_stride,
+                    const bf16_t* __restrict__ kc, const bf16_t* __restrict__ vc,
+                    const int* __restrict__ block_tables, int bt_stride,
+                    const int* __restrict__ seq_lens,
+                    bf16_t* __restrict__ out, long out_stride,
+                    float* __restrict__ part_o, float* __restrict__ part_ml,
+                    float scale_log2, int Hq, int Hkv, int bs, int P, int NQG) {
+  __shared__ float sm[4][16];
+  __shared__ float sl[4][16];
+  __shared__ float so[4][D][17];
+
+  const int b = blockIdx.x;
+  const int kvh = blockIdx.y / NQG, qg = blockIdx.y % NQG;
+  const int p = blockIdx.z;
+  const int G = Hq / Hkv;
+  const int hq0 = kvh * G + qg * 16;
+  const int nq = min(16, G - qg * 16);
+  const int L = seq_lens[b];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int c = lane & 15, g = lane >> 4;
+
+  bf16x8 qf[D / 32];
+  {
+    const bool cval = c < nq;
+    const bf16_t* qp = q + (long)b * q_stride + (long)(hq0 + (cval ? c : 0)) * D + 8 * g;
+#pragma unroll
+    for (int s = 0; s < D / 32; ++s) {
+      bf16x8 t = *reinterpret_cast<const bf16x8*>(qp + 32 * s);
+      if (!cval) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) t[j] = f2bf(0.f);
+      }
+      qf[s] = t;
+    }
+  }
+  WaveAcc<D> acc;
+  wave_acc_init(acc);
+  const int U = (L + 31) / 32;
+  const int ub = (int)(((long)p * U) / P), ue = (int)(((long)(p + 1) * U) / P);
+  const int* bt = block_tables + (long)b * bt_stride;
+  for (int u = ub + w; u < ue; u += 4)
+    attn_unit<D>(acc, qf, kc, vc, bt, 32 * u, L, kvh, Hkv, bs, scale_log2, 0x7fffffff, 0);
+
+  float lt = acc.l;
+  lt += __shfl_xor(lt, 16, 64);
+  lt += __shfl_xor(lt, 32, 64);
+  if (g == 0) { sm[w][c] = acc.m; sl[w][c] = lt; }
+#pragma unroll
+  for (int dt = 0; dt < D / 16; ++dt)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) so[w][16 * dt + 4 * g + i][c] = acc.o[dt][i];
+  __syncthreads();
+
+  for (int idx = threadIdx.x; idx < 16 * D; idx += blockDim.x) {
+    const int cq = idx / D, d = idx % D;
+    if (cq >= nq) continue;
+    float M = NEG_INF;
+#pragma unroll
+    for (int ww = 0; ww < 4; ++ww) M = fmaxf(M, sm[ww][cq]);
+    float Ls = 0.f, O = 0.f;
+    if (M != NEG_INF) {
+#pragma unroll
+      for (int ww = 0; ww < 4; ++ww) {
+        const float f = exp2f(sm[ww][cq] - M);
+        Ls += sl[ww][cq] * f;
+        O += so[ww][d][cq] * f;
+      }
+    }
+    const int hq = hq0 + cq;
+    if (P == 1) {
+      out[(long)b * out_stride + (long)hq * D + d] = f2bf(Ls > 0.f ? O / Ls : 0.f);
+    } else {
+      const long pi = ((long)b * Hq + hq) * P + p;
+      part_o[pi * D + d] = O;
+      if (d == 0) { part_ml[2 * pi] = M; part_ml[2 * pi + 1] = Ls; }
+    }
+  }
+}
+
+template <int D>
+__global__ void __launch_bounds__(256)
+paged_decode_reduce_kernel(const float* __restrict__ part_o, const float* __restrict__ part_ml,
+                           bf16_t* __restrict__ out, long out_stride, int Hq, int P) {
+  const int b = blockIdx.x, h = blockIdx.y;
+  const long base = ((long)b * Hq + h) * P;
+  float M = NEG_INF;
+  for (int p = 0; p < P; ++p) M = fmaxf(M, part_ml[2 * (base + p)]);
+  for (int d = threadIdx.x; d < D; d += blockDim.x) {
+    float Ls = 0.f, O = 0.f;
+    if (M != NEG_INF) {
+      for (int p = 0; p < P; ++p) {
+        const float f = exp2f(part_ml[2 * (base + p)] - M);
+        Ls += part_ml[2 * (base + p) + 1] * f;
+        O += part_o[(base + p) * D + d] * f;
+      }
+    }
+    out[(long)b * out_stride + (long)h * D + d] = f2bf(Ls > 0.f ? O / Ls : 0.f);
+  }
+}
+
+// ---------------------------------------------------------------------------------- prefill
+
+// work[2*i] = sequence index, work[2*i+1] = first query (multiple of 16*(4/HPW)).
+template <int D>
+__global__ void __launch_bounds__(256)
+paged_prefill_kernel(const bf16_t* __restrict__ q, long q_stride,
+                     bf16_t* __restrict__ out, long out_stride,
+                     const bf16_t* __restrict__ kc, const bf16_t* __restrict__ vc,
+                     const int* __restrict__ block_tables, int bt_stride,
+                     const int* __restrict__ seq_lens, const int* __restrict__ cu_q,
+                     const int* __restrict__ work, float scale_log2, int Hq, int Hkv, int bs,
+                     int HPW, int causal, int sliding_window, int chunk_size) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int c = lane & 15, g = lane >> 4;
+  const int hw = w % HPW, qsub = w / HPW;
+  const int s = work[2 * blockIdx.x];
+  const int qstart = work[2 * blockIdx.x + 1] + 16 * qsub;
+  const int hq = blockIdx.y * HPW + hw;
+  const int G = Hq / Hkv;
+  const int kvh = hq / G;
+  const int q0 = cu_q[s];
+  const int qlen = cu_q[s + 1] - q0;
+  if (qstart >= qlen) return;              // wave-uniform; kernel has no barriers
+  const int L = seq_lens[s];
+  const int ctx = L - qlen;
+  const int qi = qstart + c;
+  const bool cval = qi < qlen;
+  const long tokrow = q0 + (cval ? qi : qstart);
+
+  bf16x8 qf[D / 32];
+  {
+    const bf16_t* qp = q + tokrow * q_stride + (long)hq * D + 8 * g;
+#pragma unroll
+    for (int ss = 0; ss < D / 32; ++ss) qf[ss] = *reinterpret_cast<const bf16x8*>(qp + 32 * ss);
+  }
+  const int qa = ctx + (cval ? qi : qstart);
+  const int q_abs = causal ? qa : 0x7fffffff;
+  int kv_lo = 0;
+  if (sliding_window > 0) kv_lo = max(kv_lo, qa - sliding_window + 1);
+  if (chunk_size > 0) kv_lo = max(kv_lo, (qa / chunk_size) * chunk_size);
+  // wave-wide token range
+  const int qa_first = ctx + qstart;
+  int lo_w = 0;
+  if (sliding_window > 0) lo_w = max(lo_w, qa_first - sliding_window + 1);
+  if (chunk_size > 0) lo_w = max(lo_w, (qa_first / chunk_size) * chunk_size);
+  lo_w &= ~31;
+  const int hi_w = causal ? min(L, ctx + min(qstart + 16, qlen)) : L;
+
+  WaveAcc<D> acc;
+  wave_acc_init(acc);
+  const int* bt = block_tables + (long)s * bt_stride;
+  for (int tb = lo_w; tb < hi_w; tb += 32)
+    attn_unit<D>(acc, qf, kc, vc, bt, tb, L, kvh, Hkv, bs, scale_log2, q_abs, kv_lo);
+
+  float lt = acc.l;
+  lt += __shfl_xor(lt, 16, 64);
+  lt += __shfl_xor(lt, 32, 64);
+  if (!cval) return;
+  const float inv = lt > 0.f ? 1.f / lt : 0.f;
+  bf16_t* op = out + tokrow * out_stride + (long)hq * D + 4 * g;
+#pragma unroll
+  for (int dt = 0; dt < D / 16; ++dt) {
+    bf16x4 o4;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) o4[i] = f2bf(acc.o[dt][i] * inv);
+    *reinterpret_cast<bf16x4*>(op + 16 * dt) = o4;
+  }
+}
+
+// ---------------------------------------------------------------------------------- launchers
+
+EIA_API int eia_paged_decode(const void* q, long q_stride, const void* k_cache, const void* v_cache,
+                             const int* block_tables, int bt_stride, const int* seq_lens,
+                             void* out, long out_stride, float* part_o, float* part_ml,
+                             float scale, int B, int Hq, int Hkv, int D, int bs, int P,
+                             hipStream_t st) {
+  if (B < 0 || Hkv <= 0 || Hq % Hkv != 0 || bs % 16 != 0 || P < 1) return EIA_BAD_SHAPE;
+  if (P > 1 && (part_o == nullptr || part_ml == nullptr)) return EIA_BAD_SHAPE;
+  if (B == 0) return EIA_OK;
+  const int G = Hq / Hkv;
+  const int NQG = (G + 15) / 16;
+  const float sl2 = scale * 1.4426950408889634f;
+  dim3 grid(B, Hkv * NQG, P), block(256);
+#define DEC(DD)                                                                             \
+  hipLaunchKernelGGL((paged_decode_kernel<DD>), grid, block, 0, st, (const bf16_t*)q, q_stride, \
+                     (const bf16_t*)k_cache, (const bf16_t*)v_cache, block_tables, bt_stride, \
+                     seq_lens, (bf16_t*)out, out_stride, part_o, part_ml, sl2, Hq, Hkv, bs, P, NQG); \
+  if (P > 1)                                                                                \
+    hipLaunchKernelGGL((paged_decode_reduce_kernel<DD>), dim3(B, Hq), dim3(DD < 256 ? DD : 256), 0, st, \
+                       part_o, part_ml, (bf16_t*)out, out_stride, Hq, P);
+  switch (D) {
+    case 64: DEC(64) break;
+    case 128: DEC(128) break;
+    case 256: DEC(256) break;
+    default: return EIA_UNSUPPORTED;
+  }
+#undef DEC
+  EIA_LAUNCH_CHECK();
+}
+
+EIA_API int eia_paged_prefill(const void* q, long q_stride, void* out, long out_stride,
+                              const void* k_cache, const void* v_cache, const int* block_tables,
+                              int bt_stride, const int* seq_lens, const int* cu_q, const int* work,
+                              int n_work, float scale, int Hq, int Hkv, int D, int bs, int HPW,
+                              int causal, int sliding_window, int chunk_size, hipStream_t st) {
+  if (Hkv <= 0 || Hq % Hkv != 0 || bs % 16 != 0) return EIA_BAD_SHAPE;
+  if (!(HPW == 1 || HPW == 2 || HPW == 4) || (Hq / Hkv) % HPW != 0) return EIA_BAD_SHAPE;
+  if (n_work == 0) return EIA_OK;
+  const float sl2 = scale * 1.4426950408889634f;
+  dim3 grid(n_work, Hq / HPW), block(256);
+#define PRE(DD)                                                                              \
+  hipLaunchKernelGGL((paged_prefill_kernel<DD>), grid, block, 0, st, (const bf16_t*)q, q_stride, \
+                     (bf16_t*)out, out_stride, (const bf16_t*)k_cache, (const bf16_t*)v_cache, \
+                     block_tables, bt_stride, seq_lens, cu_q, work, sl2, Hq, Hkv, bs, HPW, causal, \
+                     sliding_window, chunk_size);
+  switch (D) {
+    case 64: PRE(64) break;
+    case 128: PRE(128) break;
+    case 256: PRE(256) break;
+    default: return EIA_UNSUPPORTED;
+  }
+#undef PRE
+  EIA_LAUNCH_CHECK();
+}

@@ -1,0 +1,192 @@
+// K8: fused token sampler.  One 1024-thread workgroup per row of fp32 logits.
+//   temperature <= 0           -> greedy argmax (first max index, like torch.argmax)
+//   otherwise                  -> Gumbel-max over the admissible set
+//     admissible = { i : logit_i >= tau },  tau = max(tau_topk, tau_topp, tau_minp)
+//   top-k / top-p thresholds are EXACT: radix select over the order-preserving
+//   uint32 key of each logit, 4 x 8-bit digits, histograms in LDS
+//   (counts for top-k, probability mass for top-p; top-p is evaluated inside the
+//   top-k set, i.e. vLLM's "top-k then top-p" order).  min-p is closed form:
+//   p_i / p_max >= min_p  <=>  logit_i >= max + T*ln(min_p).
+// RNG: counter-based splitmix64(seed, token) -> one uniform per (row, token), so a
+// request's sample depends only on its (seed, step) pair, never on batch layout.
+#include "eia_common.h"
+
+#define SAMPLE_THREADS 1024
+
+EIA_DEV uint32_t f2key(float f) {
+  const uint32_t u = __float_as_uint(f);
+  return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+}
+EIA_DEV float key2f(uint32_t k) {
+  const uint32_t u = (k & 0x80000000u) ? (k & 0x7fffffffu) : ~k;
+  return __uint_as_float(u);
+}
+
+EIA_DEV uint64_t splitmix64(uint64_t x) {
+  x += 0x9E3779B97F4A7C15ull;
+  x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ull;
+  x = (x ^ (x >> 27)) * 0x94D049BB133111EBull;
+  return x ^ (x >> 31);
+}
+
+// uniform in (0, 1)
+EIA_DEV float rng_uniform(uint64_t seed, uint32_t i) {
+  const uint64_t h = splitmix64(seed ^ (0xD1B54A32D192ED03ull * (uint64_t)(i + 1)));
+  return ((float)(h >> 40) + 0.5f) * (1.0f / 16777216.0f);
+}
+
+struct ArgMax { float v; int i; };
+
+EIA_DEV ArgMax argmax_combine(ArgMax a, ArgMax b) {
+  if (b.v > a.v || (b.v == a.v && b.i < a.i)) return b;
+  return a;
+}
+
+EIA_DEV ArgMax block_argmax(ArgMax x, float* sv, int* si) {
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    ArgMax y{__shfl_xor(x.v, o, 64), __shfl_xor(x.i, o, 64)};
+    x = argmax_combine(x, y);
+  }
+  __syncthreads();
+  if (lane == 0) { sv[wid] = x.v; si[wid] = x.i; }
+  __syncthreads();
+  ArgMax r{sv[0], si[0]};
+  for (int w = 1; w < (int)(blockDim.x >> 6); ++w) r = argmax_combine(r, ArgMax{sv[w], si[w]});
+  return r;
+}
+
+// Radix select. mode 0: k-th largest by count (target = k).  mode 1: by mass
+// exp((l - m) * invT) (target = mass).  Only keys >= floor_key take part.
+template <int MODE>
+EIA_DEV uint32_t radix_select(const float* __restrict__ row, int V, float target, uint32_t floor_key,
+                              float m, float invT, float* hist, uint32_t* sel) {
+  uint32_t prefix = 0, pmask = 0;
+  float remaining = target;
+  for (int r = 0; r < 4; ++r) {
+    const int shift = 24 - 8 * r;
+    for (int b = threadIdx.x; b < 256; b += blockDim.x) hist[b] = 0.f;
+    __syncthreads();
+    for (int i = threadIdx.x; i < V; i += blockDim.x) {
+      const float l = row[i];
+      const uint32_t k = f2key(l);
+      if (k < floor_key || (k & pmask) != prefix) continue;
+      const int d = (k >> shift) & 0xFF;
+      const float w = (MODE == 0) ? 1.f : __expf((l - m) * invT);
+      atomicAdd(&hist[d], w);
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      float cum = 0.f;
+      int chosen = 0;
+      for (int b = 255; b >= 0; --b) {
+        if (cum + hist[b] >= remaining) { chosen = b; break; }
+        cum += hist[b];
+      }
+      sel[0] = (uint32_t)chosen;
+      reinterpret_cast<float*>(sel)[1] = cum;
+    }
+    __syncthreads();
+    const uint32_t chosen = sel[0];
+    remaining -= reinterpret_cast<float*>(sel)[1];
+    prefix |= chosen << shift;
+    pmask |= 0xFFu << shift;
+    __syncthreads();
+  }
+  return prefix;
+}
+
+__global__ void __launch_bounds__(SAMPLE_THREADS)
+sample_kernel(const float* __restrict__ logits, long stride, int V,
+              const float* __restrict__ temperature, const int* __restrict__ top_k,
+              const float* __restrict__ top_p, const float* __restrict__ min_p,
+              const uint64_t* __restrict__ seeds, int* __restrict__ out_tokens) {
+  __shared__ float sv[SAMPLE_THREADS / 64];
+  __shared__ int si[SAMPLE_THREADS / 64];
+  __shared__ float hist[256];
+  __shared__ uint32_t sel[2];
+  __shared__ float red[SAMPLE_THREADS / 64];
+  const int b = blockIdx.x;
+  const float* row = logits + (long)b * stride;
+
+  ArgMax am{-INFINITY, 0x7fffffff};
+  for (int i = threadIdx.x; i < V; i += blockDim.x) am = argmax_combine(am, ArgMax{row[i], i});
+  am = block_argmax(am, sv, si);
+  const float T = temperature[b];
+  if (!(T > 0.f) || am.v == -INFINITY) {
+    if (threadIdx.x == 0) out_tokens[b] = am.i == 0x7fffffff ? 0 : am.i;
+    return;
+  }
+  const float m = am.v;
+  const float invT = 1.f / T;
+  uint32_t tau = 0;   // key floor
+  const int k = top_k[b];
+  if (k > 0 && k < V) tau = radix_select<0>(row, V, (float)k, 0u, m, invT, hist, sel);
+  const float p = top_p[b];
+  if (p < 1.f) {
+    float z = 0.f;
+    for (int i = threadIdx.x; i < V; i += blockDim.x) {
+      const float l = row[i];
+      if (f2key(l) >= tau) z += __expf((l - m) * invT);
+    }
+    z = block_sum(z, red);
+    const uint32_t tp = radix_select<1>(row, V, p * z, tau, m, invT, hist, sel);
+    tau = tau > tp ? tau : tp;
+  }
+  const float mp = min_p[b];
+  if (mp > 0.f) {
+    const uint32_t km = f2key(m + T * __logf(mp));
+    tau = tau > km ? tau : km;
+  }
+  const uint64_t seed = seeds[b];
+  ArgMax best{-INFINITY, 0x7fffffff};
+  for (int i = threadIdx.x; i < V; i += blockDim.x) {
+    const float l = row[i];
+    if (f2key(l) < tau) continue;
+    const float u = rng_uniform(seed, (uint32_t)i);
+    const float gval = l / T - logf(-logf(u));
+    best = argmax_combine(best, ArgMax{gval, i});
+  }
+  best = block_argmax(best, sv, si);
+  if (threadIdx.x == 0) out_tokens[b] = best.i == 0x7fffffff ? am.i : best.i;
+}
+
+EIA_API int eia_sample(const float* logits, long stride, int B, int V, const float* temperature,
+                       const int* top_k, const float* top_p, const float* min_p,
+                       const uint64_t* seeds, int* out_tokens, hipStream_t st) {
+  if (B < 0 || V <= 0) return EIA_BAD_SHAPE;
+  if (B == 0) return EIA_OK;
+  hipLaunchKernelGGL(sample_kernel, dim3(B), dim3(SAMPLE_THREADS), 0, st, logits, stride, V,
+                     temperature, top_k, top_p, min_p, seeds, out_tokens);
+  EIA_LAUNCH_CHECK();
+}
+
+// Sparse penalties: for each (row, token, count) triple in the list apply
+//   repetition (HF: divide positive / multiply negative), frequency, presence.
+// prompt tokens get count 0 and flag 1 (repetition only).
+__global__ void apply_penalties_kernel(float* __restrict__ logits, long stride,
+                                       const int* __restrict__ rows, const int* __restrict__ toks,
+                                       const int* __restrict__ counts, int n,
+                                       const float* __restrict__ rep, const float* __restrict__ freq,
+                                       const float* __restrict__ pres) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const int r = rows[i];
+  float* lp = logits + (long)r * stride + toks[i];
+  float l = *lp;
+  const float rp = rep[r];
+  if (rp != 1.f) l = l > 0.f ? l / rp : l * rp;
+  const int cnt = counts[i];
+  if (cnt > 0) l -= freq[r] * (float)cnt + pres[r];
+  *lp = l;
+}
+
+EIA_API int eia_apply_penalties(float* logits, long stride, const int* rows, const int* toks,
+                                const int* counts, int n, const float* rep, const float* freq,
+                                const float* pres, hipStream_t st) {
+  if (n <= 0) return EIA_OK;
+  hipLaunchKernelGGL(apply_penalties_kernel, dim3((n + 255) / 256), dim3(256), 0, st, logits,
+                     stride, rows, toks, counts, n, rep, freq, pres);
+  EIA_LAUNCH_CHECK();
+}

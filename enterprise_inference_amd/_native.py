@@ -1,0 +1,143 @@
+"""Loader for the in-tree native libraries.
+
+* ``_lib/libeia_kernels.so`` -- gfx950 HIP kernels with a C ABI, bound here with
+  ctypes (argtypes declared once, so a call costs ~1 µs and is capture-safe:
+  launches go to the caller's current HIP stream).
+* ``_lib/_eia_runtime*.so`` -- pybind11 host runtime (block manager, batch
+  builder, shm ring).
+
+Policy: on a machine with a GPU the HIP kernels are REQUIRED -- a missing or
+broken library raises instead of silently falling back to PyTorch ops.
+"""
+
+from __future__ import annotations
+
+import ctypes
+import importlib
+import importlib.util
+import os
+import sys
+import threading
+from typing import Optional
+
+import torch  # noqa: F401  (must be imported first: it owns the HIP runtime)
+
+_LIB_DIR = os.path.join(os.path.dirname(os.path.abspath(__file__)), "_lib")
+_KERNELS_SO = os.path.join(_LIB_DIR, "libeia_kernels.so")
+_lock = threading.Lock()
+_kernels: Optional[ctypes.CDLL] = None
+_runtime = None
+
+P = ctypes.c_void_p
+I = ctypes.c_int
+L = ctypes.c_long
+F = ctypes.c_float
+IP = ctypes.c_void_p  # int* (device)
+S = ctypes.c_void_p   # hipStream_t
+
+_SIGNATURES = {
+    "eia_rms_norm": [P, P, P, P, F, I, I, L, L, S],
+    "eia_layer_norm": [P, P, P, P, P, F, I, I, S],
+    "eia_rope_qkv_cache": [P, L, IP, P, IP, P, P, P, P, P, P, F, I, I, I, I, I, I, S],
+    "eia_paged_decode": [P, L, P, P, IP, I, IP, P, L, P, P, F, I, I, I, I, I, I, S],
+    "eia_paged_prefill": [P, L, P, L, P, P, IP, I, IP, IP, IP, I, F, I, I, I, I, I, I, I, I, S],
+    "eia_act_and_mul": [P, P, I, I, L, L, I, S],
+    "eia_act": [P, P, L, I, S],
+    "eia_sample": [P, L, I, I, P, P, P, P, P, P, S],
+    "eia_apply_penalties": [P, L, P, P, P, I, P, P, P, S],
+    "eia_moe_topk_softmax": [P, I, I, I, I, P, P, I, S],
+    "eia_moe_align": [P, I, I, I, I, P, P, P, P, S],
+    "eia_grouped_gemm": [P, P, P, P, P, P, I, I, I, I, I, I, I, S],
+    "eia_moe_combine": [P, P, P, P, I, I, I, S],
+    "eia_gemm": [P, P, P, P, I, I, I, I, I, S],
+    "eia_ar_oneshot": [P, P, P, P, I, I, I, L, I, S],
+    "eia_ar_twoshot": [P, P, P, P, I, I, I, L, I, S],
+}
+
+
+def kernels_path() -> str:
+    return _KERNELS_SO
+
+
+def gpu_available() -> bool:
+    return torch.cuda.is_available()
+
+
+def _build_kernels() -> None:
+    root = os.path.dirname(os.path.dirname(_LIB_DIR))
+    spec = importlib.util.spec_from_file_location("eia_build", os.path.join(root, "csrc", "build.py"))
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    mod.build_kernels()
+
+
+def _build_runtime() -> None:
+    root = os.path.dirname(os.path.dirname(_LIB_DIR))
+    spec = importlib.util.spec_from_file_location("eia_build", os.path.join(root, "csrc", "build.py"))
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    mod.build_runtime()
+
+
+def kernels() -> ctypes.CDLL:
+    """Return the HIP kernel library (building it in-tree if it is missing)."""
+    global _kernels
+    if _kernels is not None:
+        return _kernels
+    with _lock:
+        if _kernels is not None:
+            return _kernels
+        if not os.path.exists(_KERNELS_SO):
+            _build_kernels()
+        lib = ctypes.CDLL(_KERNELS_SO, mode=ctypes.RTLD_GLOBAL)
+        for name, argtypes in _SIGNATURES.items():
+            fn = getattr(lib, name, None)
+            if fn is None:
+                continue
+            fn.argtypes = argtypes
+            fn.restype = ctypes.c_int
+        _kernels = lib
+        return lib
+
+
+def runtime():
+    """Return the pybind11 host runtime module (auto-built with g++ if missing)."""
+    global _runtime
+    if _runtime is not None:
+        return _runtime
+    with _lock:
+        if _runtime is not None:
+            return _runtime
+        if _LIB_DIR not in sys.path:
+            sys.path.insert(0, _LIB_DIR)
+        try:
+            _runtime = importlib.import_module("_eia_runtime")
+        except ImportError:
+            _build_runtime()
+            importlib.invalidate_caches()
+            _runtime = importlib.import_module("_eia_runtime")
+        return _runtime
+
+
+def check(status: int, name: str) -> None:
+    if status != 0:
+        raise RuntimeError(f"{name} failed with status {status}")
+
+
+def stream_ptr(device: Optional[torch.device] = None) -> int:
+    return torch.cuda.current_stream(device).cuda_stream
+
+
+def loaded_native_libraries() -> list[str]:
+    """Paths of in-tree native libraries mapped into this process (for smoke checks)."""
+    out = []
+    try:
+        with open("/proc/self/maps") as f:
+            for line in f:
+                if _LIB_DIR in line:
+                    p = line.split()[-1]
+                    if p not in out:
+                        out.append(p)
+    except OSError:
+        pass
+    return out

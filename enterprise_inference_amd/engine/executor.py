@@ -1,0 +1,154 @@
+"""Executors: how a scheduled step reaches the GPU(s).
+
+* ``UniprocExecutor``  -- one ModelRunner in this process (TP=1, or the CPU path).
+* ``TPExecutor``       -- tensor parallel, one process per GPU (the reference's
+  ``--distributed_executor_backend mp``, core/helm-charts/vllm/xeon-values.yaml:78-79).
+  The driver (TP rank 0) owns the scheduler and block manager; per step it
+  publishes (plan, staging bytes) through the native shared-memory ring
+  (csrc/runtime/shm_ring.cpp) and every rank replays the same plan; the
+  collectives inside the model (RCCL / custom xGMI all-reduce) keep them in
+  lockstep.  Workers are spawned here, or are already running under torchrun.
+"""
+
+from __future__ import annotations
+
+import logging
+import multiprocessing as mp
+import os
+import pickle
+import socket
+from typing import Optional
+
+import torch
+import torch.distributed as dist
+
+from .. import _native
+from ..config import EngineConfig
+from ..parallel import state as pstate
+from .model_runner import ModelRunner, StepOutput
+
+logger = logging.getLogger(__name__)
+
+
+def _free_port() -> int:
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _agree_num_blocks(nb: int) -> int:
+    if pstate.tp_size() == 1:
+        return nb
+    t = torch.tensor([nb], dtype=torch.int64)
+    dist.all_reduce(t, op=dist.ReduceOp.MIN, group=pstate.tp_cpu_group())
+    return int(t.item())
+
+
+def setup_runner(cfg: EngineConfig) -> ModelRunner:
+    runner = ModelRunner(cfg)
+    if cfg.parallel.tensor_parallel_size > 1 and runner.is_gpu and \
+            not cfg.parallel.disable_custom_all_reduce:
+        from ..parallel.custom_allreduce import init_custom_allreduce
+        init_custom_allreduce(cfg.parallel.custom_allreduce_max_bytes)
+    nb = runner.determine_num_blocks()
+    nb = _agree_num_blocks(nb)
+    runner.allocate_kv_cache(nb)
+    runner.capture_graphs()
+    return runner
+
+
+class UniprocExecutor:
+    def __init__(self, cfg: EngineConfig, runner: Optional[ModelRunner] = None):
+        self.runner = runner or setup_runner(cfg)
+        self.num_blocks = self.runner.num_blocks
+
+    def execute(self, bm, sched) -> StepOutput:
+        return self.runner.execute(bm, sched)
+
+    def shutdown(self) -> None:
+        pass
+
+
+def worker_loop(runner: ModelRunner, ring_name: str) -> None:
+    """Non-driver TP rank: replay every plan the driver publishes until None arrives."""
+    ring = _native.runtime().ShmRing(ring_name, False)
+    while True:
+        msg = ring.get(-1.0)
+        if msg is None:
+            break
+        obj = pickle.loads(msg)
+        if obj is None:
+            break
+        plan, payload = obj
+        runner.load_payload(plan, payload)
+        with torch.no_grad():
+            runner.run(plan)
+
+
+def _spawned_worker(cfg: EngineConfig, rank: int, world: int, port: int, ring_name: str) -> None:
+    os.environ.update(RANK=str(rank), WORLD_SIZE=str(world), LOCAL_RANK=str(rank),
+                      MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    if torch.cuda.is_available():
+        torch.cuda.set_device(rank)
+    pstate.init_distributed(cfg.parallel.tensor_parallel_size,
+                            enable_expert_parallel=cfg.parallel.enable_expert_parallel)
+    runner = setup_runner(cfg)
+    worker_loop(runner, ring_name)
+    pstate.destroy_distributed()
+
+
+class TPExecutor:
+    """Driver side of tensor parallelism."""
+
+    def __init__(self, cfg: EngineConfig, spawn: bool = True):
+        tp = cfg.parallel.tensor_parallel_size
+        self.procs = []
+        self.ring_name = f"/eia_ring_{os.getpid()}_{id(self) & 0xffff}"
+        rt = _native.runtime()
+        self.ring = rt.ShmRing(self.ring_name, True, tp - 1, 8, 16 << 20)
+        if spawn and not dist.is_initialized():
+            port = _free_port()
+            ctx = mp.get_context("spawn")
+            for r in range(1, tp):
+                p = ctx.Process(target=_spawned_worker, args=(cfg, r, tp, port, self.ring_name),
+                                daemon=True)
+                p.start()
+                self.procs.append(p)
+            os.environ.update(RANK="0", WORLD_SIZE=str(tp), LOCAL_RANK="0",
+                              MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+            if torch.cuda.is_available():
+                torch.cuda.set_device(0)
+            pstate.init_distributed(tp, enable_expert_parallel=cfg.parallel.enable_expert_parallel)
+        self.runner = setup_runner(cfg)
+        self.num_blocks = self.runner.num_blocks
+
+    def execute(self, bm, sched) -> StepOutput:
+        r = self.runner
+        sample_items = sched.decodes + [p for p in sched.prefills if p.samples]
+        plan = r.prepare(bm, sched)
+        self.ring.put(pickle.dumps((plan, r.plan_payload(plan)), protocol=5), -1.0)
+        with torch.no_grad():
+            logits = r.run(plan)
+            if not sample_items:
+                return StepOutput([], None)
+            return r.sample(logits, sample_items)
+
+    def shutdown(self) -> None:
+        try:
+            self.ring.put(pickle.dumps(None), 5.0)
+        except Exception:   # noqa: BLE001
+            pass
+        for p in self.procs:
+            p.join(timeout=30)
+            if p.is_alive():
+                p.terminate()
+        self.procs = []
+
+
+def make_executor(cfg: EngineConfig):
+    if cfg.parallel.tensor_parallel_size > 1:
+        if dist.is_initialized():
+            # launched under torchrun: this process is TP rank 0 of its group
+            return TPExecutor(cfg, spawn=False)
+        return TPExecutor(cfg, spawn=True)
+    return UniprocExecutor(cfg)

@@ -1,0 +1,303 @@
+"""Synchronous LLM engine: requests in, incremental RequestOutputs out.
+
+One ``step()`` = schedule -> execute on the GPU(s) -> append tokens -> stop
+checks -> detokenise.  The OpenAI server drives it from a background thread
+(engine/async_engine.py); ``generate()`` is the offline helper used by tests,
+``bench.py`` and the ``LLM`` class.
+"""
+
+from __future__ import annotations
+
+import dataclasses
+import logging
+import random
+import time
+from typing import Dict, Iterable, List, Optional, Sequence as Seq, Union
+
+from ..config import EngineConfig
+from ..tokenizer import get_tokenizer
+from .detokenizer import Detokenizer
+from .sampling_params import SamplingParams
+from .scheduler import Scheduler, SchedulerOutput
+from .sequence import FINISH_REASON, SeqStatus, Sequence
+
+logger = logging.getLogger(__name__)
+
+
+@dataclasses.dataclass
+class CompletionOutput:
+    index: int
+    text: str
+    token_ids: List[int]
+    cumulative_logprob: Optional[float]
+    logprobs: Optional[List[Dict[int, float]]]
+    finish_reason: Optional[str] = None
+    stop_reason: Union[int, str, None] = None
+    new_text: str = ""
+    new_token_ids: List[int] = dataclasses.field(default_factory=list)
+    new_logprobs: Optional[List[Dict[int, float]]] = None
+
+    def finished(self) -> bool:
+        return self.finish_reason is not None
+
+
+@dataclasses.dataclass
+class RequestMetrics:
+    arrival_time: float
+    first_scheduled_time: Optional[float] = None
+    first_token_time: Optional[float] = None
+    last_token_time: Optional[float] = None
+    finished_time: Optional[float] = None
+
+    @property
+    def ttft(self) -> Optional[float]:
+        return None if self.first_token_time is None else self.first_token_time - self.arrival_time
+
+
+@dataclasses.dataclass
+class RequestOutput:
+    request_id: str
+    prompt: Optional[str]
+    prompt_token_ids: List[int]
+    outputs: List[CompletionOutput]
+    finished: bool
+    metrics: RequestMetrics
+    num_cached_tokens: int = 0
+    prompt_logprobs: Optional[list] = None
+
+
+class _Request:
+    __slots__ = ("request_id", "prompt", "prompt_token_ids", "params", "seqs", "arrival_time",
+                 "n", "finished_emitted")
+
+    def __init__(self, request_id, prompt, prompt_token_ids, params, seqs, arrival_time):
+        self.request_id = request_id
+        self.prompt = prompt
+        self.prompt_token_ids = prompt_token_ids
+        self.params = params
+        self.seqs = seqs
+        self.arrival_time = arrival_time
+        self.n = params.n
+        self.finished_emitted = False
+
+
+@dataclasses.dataclass
+class EngineStats:
+    num_prompt_tokens: int = 0          # prompt tokens computed (excl. prefix-cache hits)
+    num_generation_tokens: int = 0
+    num_steps: int = 0
+    num_preemptions: int = 0
+    step_time_s: float = 0.0
+
+
+class LLMEngine:
+    def __init__(self, cfg: EngineConfig, tokenizer=None, executor=None):
+        self.cfg = cfg
+        if executor is None:
+            from .executor import make_executor
+            executor = make_executor(cfg)
+        self.executor = executor
+        self.num_blocks = executor.num_blocks
+        self.scheduler = Scheduler(cfg.scheduler, cfg.cache, self.num_blocks)
+        m = cfg.model
+        self.tokenizer = tokenizer or get_tokenizer(cfg.tokenizer or cfg.model_path, m.vocab_size,
+                                                    m.eos_token_id, m.bos_token_id,
+                                                    cfg.trust_remote_code)
+        eos = m.eos_token_id
+        eos_ids = set(eos if isinstance(eos, list) else ([eos] if eos is not None else []))
+        tok_eos = getattr(self.tokenizer, "eos_token_id", None)
+        if tok_eos is not None:
+            eos_ids.add(tok_eos)
+        self.eos_ids = {e for e in eos_ids if e is not None and e < m.vocab_size}
+        self.detok = Detokenizer(self.tokenizer)
+        self.requests: Dict[str, _Request] = {}
+        self.stats = EngineStats()
+        self.finished_log: List[RequestOutput] = []      # consumed by the metrics exporter
+        self.served_model_name = cfg.served_model_name or m.name or "model"
+        self._step_listeners = []
+
+    # ------------------------------------------------------------------ requests
+    def add_request(self, request_id: str, prompt: Optional[str] = None,
+                    params: Optional[SamplingParams] = None,
+                    prompt_token_ids: Optional[List[int]] = None,
+                    arrival_time: Optional[float] = None, priority: int = 0) -> None:
+        if request_id in self.requests:
+            raise ValueError(f"duplicate request id {request_id}")
+        params = params or SamplingParams()
+        if prompt_token_ids is None:
+            if prompt is None:
+                raise ValueError("prompt or prompt_token_ids required")
+            prompt_token_ids = self.tokenizer.encode(prompt)
+        if not prompt_token_ids:
+            raise ValueError("empty prompt")
+        maxlen = self.cfg.scheduler.max_model_len
+        if len(prompt_token_ids) >= maxlen:
+            raise ValueError(f"prompt has {len(prompt_token_ids)} tokens; max_model_len is {maxlen}")
+        vocab = self.cfg.model.vocab_size
+        if max(prompt_token_ids) >= vocab or min(prompt_token_ids) < 0:
+            raise ValueError("prompt token id out of vocabulary range")
+        if params.max_tokens is None:
+            params = params.clone(max_tokens=maxlen - len(prompt_token_ids))
+        params.eos_ids = sorted(self.eos_ids)
+        if params.best_of > params.n and params.logprobs is None:
+            params = params.clone(logprobs=0)
+            params.eos_ids = sorted(self.eos_ids)
+        arrival = arrival_time if arrival_time is not None else time.time()
+        seqs = []
+        for i in range(params.best_of):
+            seed = (params.seed + i) if params.seed is not None else random.getrandbits(63)
+            s = Sequence(request_id, prompt_token_ids, params, index=i, arrival_time=arrival,
+                         seed=seed, priority=priority)
+            if params.guided_choice or params.guided_regex or params.guided_json is not None:
+                from .guided import make_guided_state
+                s.guided_state = make_guided_state(params, self.tokenizer, vocab)
+            seqs.append(s)
+            self.scheduler.add(s)
+        self.requests[request_id] = _Request(request_id, prompt, list(prompt_token_ids), params,
+                                             seqs, arrival)
+
+    def abort_request(self, request_id: Union[str, Iterable[str]]) -> None:
+        ids = [request_id] if isinstance(request_id, str) else list(request_id)
+        for rid in ids:
+            self.scheduler.abort_request(rid)
+            self.requests.pop(rid, None)
+
+    def has_unfinished_requests(self) -> bool:
+        return self.scheduler.num_unfinished() > 0
+
+    def num_unfinished_requests(self) -> int:
+        return len(self.requests)
+
+    # ------------------------------------------------------------------ step
+    def step(self) -> List[RequestOutput]:
+        t0 = time.time()
+        sched = self.scheduler.schedule()
+        touched: Dict[str, _Request] = {}
+        for s in self.scheduler.finished_since_last:
+            r = self.requests.get(s.request_id)
+            if r:
+                touched[r.request_id] = r
+        self.scheduler.finished_since_last.clear()
+        if sched.empty:
+            return self._emit(touched, {})
+        res = self.executor.execute(self.scheduler.bm, sched)
+        self.scheduler.update_after_step(sched)
+        now = time.time()
+        self.stats.num_steps += 1
+        self.stats.num_preemptions = self.scheduler.num_preemptions
+        self.stats.num_prompt_tokens += sum(it.num_tokens for it in sched.prefills) + sum(
+            it.num_tokens for it in sched.decodes if it.seq.is_prefill)
+        deltas: Dict[int, tuple] = {}
+        sample_items = sched.decodes + [p for p in sched.prefills if p.samples]
+        for r, it in enumerate(sample_items):
+            seq = it.seq
+            if seq.finished:
+                continue
+            tok = res.tokens[r]
+            lp = res.logprobs[r] if res.logprobs is not None else None
+            self._append_token(seq, tok, lp, now)
+            before = len(seq.output_text)
+            new_text = self.detok.step(seq)
+            self._check_stop(seq, tok, new_text)
+            new_text = seq.output_text[before:]
+            deltas[seq.seq_id] = (new_text, [tok], [lp] if lp is not None else None)
+            touched[seq.request_id] = self.requests[seq.request_id]
+            self.stats.num_generation_tokens += 1
+        self.stats.step_time_s += time.time() - t0
+        return self._emit(touched, deltas)
+
+    def _append_token(self, seq: Sequence, tok: int, lp, now: float) -> None:
+        seq.output_token_ids.append(tok)
+        if lp is not None:
+            seq.output_logprobs.append(lp)
+            seq.cumulative_logprob += lp.get(tok, 0.0)
+        if seq.first_token_time is None:
+            seq.first_token_time = now
+        seq.last_token_time = now
+
+    def _check_stop(self, seq: Sequence, tok: int, new_text: str) -> None:
+        p = seq.params
+        n_out = len(seq.output_token_ids)
+        status = None
+        if n_out >= p.min_tokens:
+            if not p.ignore_eos and tok in self.eos_ids:
+                status = SeqStatus.FINISHED_STOPPED
+            elif tok in p.stop_token_ids:
+                status = SeqStatus.FINISHED_STOPPED
+                seq.stop_reason = tok
+            else:
+                hit = self.detok.check_stop_strings(seq, new_text)
+                if hit is not None:
+                    status = SeqStatus.FINISHED_STOPPED
+                    seq.stop_reason = hit[0]
+        if status is None and (n_out >= p.max_tokens or seq.num_tokens >= self.cfg.scheduler.max_model_len):
+            status = SeqStatus.FINISHED_LENGTH
+        if status is None and seq.guided_state is not None:
+            seq.guided_state.advance(tok)
+            if seq.guided_state.is_done():
+                status = SeqStatus.FINISHED_STOPPED
+        if status is not None:
+            self.scheduler.finish(seq, status)
+
+    def _emit(self, touched: Dict[str, _Request], deltas: Dict[int, tuple]) -> List[RequestOutput]:
+        outs = []
+        for rid, r in touched.items():
+            finished = all(s.finished for s in r.seqs)
+            seqs = r.seqs
+            if finished and r.params.best_of > r.params.n:
+                seqs = sorted(seqs, key=lambda s: s.cumulative_logprob, reverse=True)[:r.params.n]
+            elif r.params.best_of > r.params.n:
+                continue     # best_of is only returned at the end
+            comps = []
+            for i, s in enumerate(seqs):
+                d = deltas.get(s.seq_id, ("", [], None))
+                comps.append(CompletionOutput(
+                    index=i if r.params.best_of > r.params.n else s.index,
+                    text=s.output_text, token_ids=list(s.output_token_ids),
+                    cumulative_logprob=s.cumulative_logprob if r.params.logprobs is not None else None,
+                    logprobs=s.output_logprobs if r.params.logprobs is not None else None,
+                    finish_reason=FINISH_REASON.get(s.status), stop_reason=s.stop_reason,
+                    new_text=d[0], new_token_ids=d[1], new_logprobs=d[2]))
+            s0 = r.seqs[0]
+            metrics = RequestMetrics(r.arrival_time, s0.first_scheduled_time,
+                                     min((s.first_token_time for s in r.seqs if s.first_token_time),
+                                         default=None),
+                                     max((s.last_token_time for s in r.seqs if s.last_token_time),
+                                         default=None),
+                                     max((s.finish_time for s in r.seqs if s.finish_time), default=None)
+                                     if finished else None)
+            ro = RequestOutput(rid, r.prompt, r.prompt_token_ids, comps, finished, metrics,
+                               s0.num_cached_tokens)
+            outs.append(ro)
+            if finished:
+                self.requests.pop(rid, None)
+                self.finished_log.append(ro)
+                if len(self.finished_log) > 10000:
+                    del self.finished_log[:5000]
+        return outs
+
+    # ------------------------------------------------------------------ helpers
+    def generate(self, prompts: Optional[Seq[str]] = None, params=None,
+                 prompt_token_ids: Optional[Seq[List[int]]] = None) -> List[RequestOutput]:
+        n = len(prompts) if prompts is not None else len(prompt_token_ids)
+        plist = params if isinstance(params, list) else [params or SamplingParams()] * n
+        ids = []
+        for i in range(n):
+            rid = f"gen-{time.time_ns()}-{i}"
+            self.add_request(rid, prompts[i] if prompts is not None else None, plist[i],
+                             prompt_token_ids[i] if prompt_token_ids is not None else None)
+            ids.append(rid)
+        done: Dict[str, RequestOutput] = {}
+        while len(done) < n:
+            for o in self.step():
+                if o.finished:
+                    done[o.request_id] = o
+        return [done[i] for i in ids]
+
+    def kv_cache_usage(self) -> float:
+        return self.scheduler.kv_usage()
+
+    def shutdown(self) -> None:
+        ex = getattr(self.executor, "shutdown", None)
+        if ex:
+            ex()

@@ -1,0 +1,443 @@
+"""Per-GPU model runner: input staging, paged KV cache, HIP graphs, sampling.
+
+Step anatomy (decode-only steps replay a HIP graph captured per batch bucket,
+mirroring the reference's HPU-graph bucketing ``VLLM_DECODE_BS_BUCKET_STEP``,
+core/helm-charts/vllm/gaudi-values.yaml:51-64):
+  host: native batch builder writes ids/positions/slots/block tables into a
+        pinned int32 staging buffer  ->  1-2 async H2D copies
+  GPU : embed -> L x (norm, QKV, RoPE+KV, attention, O, norm, MLP) -> norm -> LM head
+  GPU : sampler kernel (K8) on the rows that emit a token
+"""
+
+from __future__ import annotations
+
+import logging
+import math
+import time
+from typing import Dict, List, Optional, Tuple
+
+import numpy as np
+import torch
+
+from .. import _native
+from ..config import EngineConfig
+from ..models.loader import build_model
+from ..ops import attention as attn_ops
+from ..ops import sampling as sampling_ops
+from ..parallel import state as pstate
+from .block_manager import BlockManager
+from .scheduler import ScheduledSeq, SchedulerOutput
+
+logger = logging.getLogger(__name__)
+
+
+def graph_buckets(max_bs: int, step: int) -> List[int]:
+    b = [x for x in (1, 2, 4, 8) if x <= max_bs]
+    x = max(step, 16)
+    while x < max_bs:
+        b.append(x)
+        x += step
+    if not b or b[-1] != max_bs:
+        b.append(max_bs)
+    return sorted(set(b))
+
+
+class StepOutput:
+    __slots__ = ("tokens", "logprobs", "prompt_logprobs")
+
+    def __init__(self, tokens, logprobs=None):
+        self.tokens = tokens            # list[int] for the sampling rows, in batch order
+        self.logprobs = logprobs        # optional list[dict[int, float]]
+        self.prompt_logprobs = None
+
+
+class ModelRunner:
+    def __init__(self, cfg: EngineConfig, device: Optional[torch.device] = None):
+        self.cfg = cfg
+        if device is None:
+            device = torch.device("cuda", torch.cuda.current_device()) \
+                if (cfg.device == "cuda" and torch.cuda.is_available()) else torch.device("cpu")
+        self.device = device
+        self.is_gpu = device.type == "cuda"
+        if self.is_gpu:
+            _native.kernels()         # fail loudly now if the HIP library is unusable
+        torch.manual_seed(cfg.seed)
+        t0 = time.time()
+        self.model = build_model(cfg, device)
+        self.load_time = time.time() - t0
+        m = cfg.model
+        self.num_layers = m.num_hidden_layers
+        self.head_dim = m.head_dim
+        self.num_kv_heads = self.model.kv_heads_per_rank()
+        self.block_size = cfg.cache.block_size
+        self.max_num_seqs = cfg.scheduler.max_num_seqs
+        self.max_tokens = cfg.scheduler.max_num_batched_tokens
+        self.maxb = cfg.max_blocks_per_seq
+        self.kv_caches: List[Tuple[torch.Tensor, torch.Tensor]] = []
+        self.num_blocks = 0
+        self.graphs: Dict[int, torch.cuda.CUDAGraph] = {}
+        self.graph_pool = None
+        self.vocab = m.vocab_size
+        self.num_heads = m.num_attention_heads // pstate.tp_size()
+        self._alloc_staging()
+
+    # ------------------------------------------------------------------ buffers
+    def _alloc_staging(self) -> None:
+        T, S, mb = self.max_tokens, self.max_num_seqs, self.maxb
+        qb = attn_ops.prefill_query_block(self.num_heads, self.num_kv_heads)
+        self.max_work = T // qb + S + 1
+        pin = self.is_gpu
+        # graph (decode) region, fixed offsets
+        self.g_hdr = torch.zeros(4 * S, dtype=torch.int32, pin_memory=pin)      # ids|pos|slot|len
+        self.g_bt = torch.zeros(S * mb, dtype=torch.int32, pin_memory=pin)
+        # eager region: packed per step
+        self.e_size = 3 * T + 2 * S * mb + 3 * S + 1 + 2 * self.max_work + S + 64
+        self.e_buf = torch.zeros(self.e_size, dtype=torch.int32, pin_memory=pin)
+        self.s_f32 = torch.zeros(3 * S, dtype=torch.float32, pin_memory=pin)    # temp|top_p|min_p
+        self.s_i32 = torch.zeros(S, dtype=torch.int32, pin_memory=pin)          # top_k
+        self.s_i64 = torch.zeros(S, dtype=torch.int64, pin_memory=pin)          # seeds
+        dev = self.device
+        self.d_g_hdr = torch.zeros(4 * S, dtype=torch.int32, device=dev)
+        self.d_g_bt = torch.zeros(S * mb, dtype=torch.int32, device=dev)
+        self.d_e_buf = torch.zeros(self.e_size, dtype=torch.int32, device=dev)
+        self.d_s_f32 = torch.zeros(3 * S, dtype=torch.float32, device=dev)
+        self.d_s_i32 = torch.zeros(S, dtype=torch.int32, device=dev)
+        self.d_s_i64 = torch.zeros(S, dtype=torch.int64, device=dev)
+        pmax = 16
+        self.part_o = torch.empty(S * self.num_heads * pmax * self.head_dim, dtype=torch.float32,
+                                  device=dev) if self.is_gpu else None
+        self.part_ml = torch.empty(S * self.num_heads * pmax * 2, dtype=torch.float32,
+                                   device=dev) if self.is_gpu else None
+
+    # ------------------------------------------------------------------ KV cache
+    def kv_block_bytes(self) -> int:
+        e = torch.tensor([], dtype=self.cfg.cache.cache_dtype).element_size()
+        return self.num_layers * 2 * self.num_kv_heads * self.block_size * self.head_dim * e
+
+    def determine_num_blocks(self) -> int:
+        cc = self.cfg.cache
+        if cc.num_gpu_blocks:
+            return int(cc.num_gpu_blocks)
+        per = self.kv_block_bytes()
+        if not self.is_gpu:
+            return max(16, int(cc.cpu_kvcache_space_gb * (1 << 30) // per))
+        # profile peak activation memory with a max-size prefill
+        torch.cuda.synchronize()
+        torch.cuda.reset_peak_memory_stats()
+        self._profile_run()
+        torch.cuda.synchronize()
+        peak = torch.cuda.max_memory_allocated()
+        free, total = torch.cuda.mem_get_info()
+        used_now = torch.cuda.memory_allocated()
+        reserve = 2 << 30                                     # graphs + logits + slack
+        budget = total * cc.gpu_memory_utilization - peak - reserve
+        budget = min(budget, free - (1 << 30) - (peak - used_now))
+        nb = int(budget // per)
+        if nb <= 0:
+            raise RuntimeError("not enough GPU memory for the KV cache; lower max_num_batched_tokens"
+                               " or raise gpu_memory_utilization")
+        return nb
+
+    def _profile_run(self) -> None:
+        n = self.max_tokens
+        ids = torch.zeros(n, dtype=torch.int32, device=self.device)
+        pos = torch.arange(n, dtype=torch.int32, device=self.device) % self.cfg.scheduler.max_model_len
+        slots = torch.full((n,), -1, dtype=torch.int32, device=self.device)
+        # scratch 1-block caches suffice (slots < 0: no writes)
+        k = torch.zeros(1, self.num_kv_heads, self.block_size, self.head_dim, dtype=self.cfg.dtype,
+                        device=self.device)
+        v = torch.zeros(1, self.num_kv_heads, self.head_dim, self.block_size, dtype=self.cfg.dtype,
+                        device=self.device)
+        # one sequence per max_model_len chunk, all zero-length context -> attention reads block 0
+        qlen = min(n, self.cfg.scheduler.max_model_len)
+        nseq = math.ceil(n / qlen)
+        qls = [min(qlen, n - i * qlen) for i in range(nseq)]
+        cu = torch.tensor([0] + list(np.cumsum(qls)), dtype=torch.int32, device=self.device)
+        lens = torch.tensor(qls, dtype=torch.int32, device=self.device)
+        bt = torch.zeros(nseq, max(1, self.maxb), dtype=torch.int32, device=self.device)
+        qb = attn_ops.prefill_query_block(self.num_heads, self.num_kv_heads)
+        work = attn_ops.build_prefill_work(qls, qb)
+        md = attn_ops.AttentionMetadata(
+            num_decode=0, num_prefill_tokens=n, slot_mapping=slots, positions=pos,
+            prefill_block_tables=bt, prefill_seq_lens=torch.ones_like(lens),
+            prefill_cu_q=cu, prefill_work=torch.tensor(work, dtype=torch.int32, device=self.device),
+            prefill_n_work=len(work) // 2, causal=False)
+        with torch.no_grad():
+            h = self.model(ids, md, [(k, v)] * self.num_layers)
+            idx = torch.arange(min(n, self.max_num_seqs), device=self.device)
+            self.model.compute_logits(h[idx])
+        del h
+
+    def allocate_kv_cache(self, num_blocks: Optional[int] = None) -> int:
+        nb = num_blocks or self.determine_num_blocks()
+        self.num_blocks = nb
+        Hkv, bs, D = self.num_kv_heads, self.block_size, self.head_dim
+        per_layer = nb * Hkv * bs * D
+        # zero-filled: never-written slots must stay finite (masked P=0 times V)
+        buf = torch.zeros(self.num_layers, 2, per_layer, dtype=self.cfg.cache.cache_dtype,
+                          device=self.device)
+        self.kv_buf = buf
+        self.kv_caches = [(buf[l, 0].view(nb, Hkv, bs, D), buf[l, 1].view(nb, Hkv, D, bs))
+                          for l in range(self.num_layers)]
+        logger.info("KV cache: %d blocks x %d tokens (%.1f GiB)", nb, bs,
+                    buf.numel() * buf.element_size() / 2**30)
+        return nb
+
+    # ------------------------------------------------------------------ inputs
+    def _decode_partitions(self, B: int, max_len: int) -> int:
+        if not self.is_gpu:
+            return 1
+        return attn_ops.decode_partitions(B, self.num_kv_heads, self.num_heads, max_len)
+
+    def _prepare_graph(self, bm: BlockManager, decodes: List[ScheduledSeq], Bp: int) -> dict:
+        S = self.max_num_seqs
+        hdr = self.g_hdr.numpy()
+        n = len(decodes)
+        hdr[0:n] = np.fromiter((d.seq.token_at(d.start) for d in decodes), dtype=np.int32, count=n)
+        seq_ids = np.fromiter((d.seq.seq_id for d in decodes), dtype=np.int64, count=n)
+        starts = np.fromiter((d.start for d in decodes), dtype=np.int32, count=n)
+        base = self.g_hdr.data_ptr()
+        bm.native.build(seq_ids, starts, np.ones(n, dtype=np.int32), base + 4 * S, base + 8 * S,
+                        self.g_bt.data_ptr(), self.maxb, base + 12 * S, S)
+        if Bp > n:
+            hdr[n:Bp] = 0
+            hdr[S + n:S + Bp] = 0
+            hdr[2 * S + n:2 * S + Bp] = -1
+            hdr[3 * S + n:3 * S + Bp] = 0
+        return {"kind": "graph", "Bp": Bp, "nd": n}
+
+    def _upload_graph(self, Bp: int) -> None:
+        self.d_g_hdr.copy_(self.g_hdr, non_blocking=True)
+        self.d_g_bt[:Bp * self.maxb].copy_(self.g_bt[:Bp * self.maxb], non_blocking=True)
+
+    def _graph_metadata(self, Bp: int, P: int) -> Tuple[torch.Tensor, attn_ops.AttentionMetadata]:
+        S = self.max_num_seqs
+        d = self.d_g_hdr
+        md = attn_ops.AttentionMetadata(
+            num_decode=Bp, num_prefill_tokens=0, slot_mapping=d[2 * S:2 * S + Bp],
+            positions=d[S:S + Bp], decode_block_tables=self.d_g_bt[:Bp * self.maxb].view(Bp, self.maxb),
+            decode_seq_lens=d[3 * S:3 * S + Bp], decode_partitions=P, decode_part_o=self.part_o,
+            decode_part_ml=self.part_ml)
+        return d[:Bp], md
+
+    def _prepare_eager(self, bm: BlockManager, out: SchedulerOutput) -> dict:
+        """Pack the step's metadata into the eager staging buffer; returns the plan."""
+        buf = self.e_buf.numpy()
+        base = self.e_buf.data_ptr()
+        items = out.decodes + out.prefills
+        T = out.num_batched_tokens
+        nd, npf = len(out.decodes), len(out.prefills)
+        o = {}
+        off = 0
+
+        def take(name, n):
+            nonlocal off
+            o[name] = off
+            off += n
+
+        take("ids", T)
+        take("pos", T)
+        take("slot", T)
+        p = o["ids"]
+        for it in items:
+            s = it.seq
+            if it.num_tokens == 1:
+                buf[p] = s.token_at(it.start)
+            else:
+                buf[p:p + it.num_tokens] = s.all_token_ids[it.start:it.start + it.num_tokens]
+            p += it.num_tokens
+        mb_d = max([bm.native.num_seq_blocks(d.seq.seq_id) for d in out.decodes], default=1)
+        mb_p = max([bm.native.num_seq_blocks(d.seq.seq_id) for d in out.prefills], default=1)
+        take("dbt", nd * mb_d)
+        take("dlen", nd)
+        take("pbt", npf * mb_p)
+        take("plen", npf)
+        take("cu", npf + 1)
+        if nd:
+            bm.native.build(np.fromiter((d.seq.seq_id for d in out.decodes), np.int64, nd),
+                            np.fromiter((d.start for d in out.decodes), np.int32, nd),
+                            np.ones(nd, np.int32), base + 4 * o["pos"], base + 4 * o["slot"],
+                            base + 4 * o["dbt"], mb_d, base + 4 * o["dlen"], T)
+        qlens = [it.num_tokens for it in out.prefills]
+        if npf:
+            bm.native.build(np.fromiter((d.seq.seq_id for d in out.prefills), np.int64, npf),
+                            np.fromiter((d.start for d in out.prefills), np.int32, npf),
+                            np.asarray(qlens, np.int32), base + 4 * (o["pos"] + nd),
+                            base + 4 * (o["slot"] + nd), base + 4 * o["pbt"], mb_p,
+                            base + 4 * o["plen"], T - nd)
+            buf[o["cu"]] = 0
+            buf[o["cu"] + 1:o["cu"] + 1 + npf] = np.cumsum(qlens)
+        qb = attn_ops.prefill_query_block(self.num_heads, self.num_kv_heads)
+        work = attn_ops.build_prefill_work(qlens, qb)
+        take("work", len(work))
+        if work:
+            buf[o["work"]:o["work"] + len(work)] = work
+        sample_rows = list(range(nd))
+        acc = nd
+        for it in out.prefills:
+            acc += it.num_tokens
+            if it.samples:
+                sample_rows.append(acc - 1)
+        take("lidx", len(sample_rows))
+        if sample_rows:
+            buf[o["lidx"]:o["lidx"] + len(sample_rows)] = sample_rows
+        max_len = max([it.start + it.num_tokens for it in out.decodes], default=1)
+        P = self._decode_partitions(nd, max_len) if nd else 1
+        return {"kind": "eager", "T": T, "nd": nd, "npf": npf, "mb_d": mb_d, "mb_p": mb_p,
+                "o": o, "n_work": len(work) // 2, "n_lidx": len(sample_rows), "P": P, "off": off}
+
+    def _eager_inputs(self, plan: dict):
+        d = self.d_e_buf
+        o, T, nd, npf = plan["o"], plan["T"], plan["nd"], plan["npf"]
+        mb_d, mb_p, nw = plan["mb_d"], plan["mb_p"], plan["n_work"]
+        md = attn_ops.AttentionMetadata(
+            num_decode=nd, num_prefill_tokens=T - nd, slot_mapping=d[o["slot"]:o["slot"] + T],
+            positions=d[o["pos"]:o["pos"] + T],
+            decode_block_tables=d[o["dbt"]:o["dbt"] + nd * mb_d].view(nd, mb_d) if nd else None,
+            decode_seq_lens=d[o["dlen"]:o["dlen"] + nd] if nd else None,
+            decode_partitions=plan["P"], decode_part_o=self.part_o, decode_part_ml=self.part_ml,
+            prefill_block_tables=d[o["pbt"]:o["pbt"] + npf * mb_p].view(npf, mb_p) if npf else None,
+            prefill_seq_lens=d[o["plen"]:o["plen"] + npf] if npf else None,
+            prefill_cu_q=d[o["cu"]:o["cu"] + npf + 1] if npf else None,
+            prefill_work=d[o["work"]:o["work"] + 2 * nw] if npf else None,
+            prefill_n_work=nw)
+        lidx = d[o["lidx"]:o["lidx"] + plan["n_lidx"]].long()
+        return d[o["ids"]:o["ids"] + T], md, lidx
+
+    def prepare(self, bm: BlockManager, out: SchedulerOutput) -> dict:
+        """Host side of a step (driver only): fill the pinned staging buffers."""
+        nd = len(out.decodes)
+        if not out.prefills and self.graphs and nd <= max(self.graphs):
+            Bp = min(b for b in self.graphs if b >= nd)
+            return self._prepare_graph(bm, out.decodes, Bp)
+        return self._prepare_eager(bm, out)
+
+    def plan_payload(self, plan: dict) -> bytes:
+        """Staging bytes a TP worker needs to replay `plan` (sent over the shm ring)."""
+        if plan["kind"] == "graph":
+            Bp = plan["Bp"]
+            return self.g_hdr.numpy().tobytes() + self.g_bt.numpy()[:Bp * self.maxb].tobytes()
+        return self.e_buf.numpy()[:plan["off"]].tobytes()
+
+    def load_payload(self, plan: dict, payload: bytes) -> None:
+        a = np.frombuffer(payload, dtype=np.int32)
+        if plan["kind"] == "graph":
+            S = self.max_num_seqs
+            self.g_hdr.numpy()[:] = a[:4 * S]
+            self.g_bt.numpy()[:len(a) - 4 * S] = a[4 * S:]
+        else:
+            self.e_buf.numpy()[:len(a)] = a
+
+    def run(self, plan: dict) -> Optional[torch.Tensor]:
+        """Device side of a step (every TP rank): returns logits of the sampling rows."""
+        if plan["kind"] == "graph":
+            Bp = plan["Bp"]
+            self._upload_graph(Bp)
+            self.graphs[Bp].replay()
+            return self.graph_logits[Bp][:plan["nd"]]
+        off = plan["off"]
+        self.d_e_buf[:off].copy_(self.e_buf[:off], non_blocking=True)
+        ids, md, lidx = self._eager_inputs(plan)
+        h = self.model(ids, md, self.kv_caches)
+        if plan["n_lidx"] == 0:
+            return None
+        return self.model.compute_logits(h.index_select(0, lidx))
+
+    # ------------------------------------------------------------------ sampling
+    def _sampling_tensors(self, items: List[ScheduledSeq]):
+        n = len(items)
+        f = self.s_f32.numpy()
+        S = self.max_num_seqs
+        k = self.s_i32.numpy()
+        sd = self.s_i64.numpy()
+        for i, it in enumerate(items):
+            p = it.seq.params
+            f[i] = 0.0 if p.greedy else p.temperature
+            f[S + i] = p.top_p
+            f[2 * S + i] = p.min_p
+            k[i] = p.top_k if p.top_k > 0 else 0
+            sd[i] = sampling_ops.row_seed(it.seq.seed, len(it.seq.output_token_ids))
+        if self.is_gpu:
+            self.d_s_f32.copy_(self.s_f32, non_blocking=True)
+            self.d_s_i32[:n].copy_(self.s_i32[:n], non_blocking=True)
+            self.d_s_i64[:n].copy_(self.s_i64[:n], non_blocking=True)
+            F_, K_, SD = self.d_s_f32, self.d_s_i32, self.d_s_i64
+        else:
+            F_, K_, SD = self.s_f32, self.s_i32, self.s_i64
+        return F_[:n], K_[:n], F_[S:S + n], F_[2 * S:2 * S + n], SD[:n]
+
+    def sample(self, logits: torch.Tensor, items: List[ScheduledSeq]) -> StepOutput:
+        from .logits_process import apply_logits_processors
+
+        logits = apply_logits_processors(logits, items)
+        temp, top_k, top_p, min_p, seeds = self._sampling_tensors(items)
+        toks = sampling_ops.sample(logits, temp, top_k, top_p, min_p, seeds)
+        lp = None
+        want = [it.seq.params.logprobs for it in items]
+        if any(w is not None for w in want):
+            logp = torch.log_softmax(logits, dim=-1)
+            n = max(w or 0 for w in want)
+            top_v, top_i = (logp.topk(n, dim=-1) if n > 0 else (None, None))
+            chosen = logp.gather(1, toks.long()[:, None])[:, 0]
+            chosen, tv, ti = chosen.tolist(), (top_v.tolist() if n else None), (
+                top_i.tolist() if n else None)
+            tl = toks.tolist()
+            lp = []
+            for r, w in enumerate(want):
+                if w is None:
+                    lp.append(None)
+                    continue
+                d = {tl[r]: chosen[r]}
+                if w:
+                    for j in range(w):
+                        d.setdefault(ti[r][j], tv[r][j])
+                lp.append(d)
+            return StepOutput(tl, lp)
+        return StepOutput(toks.tolist(), None)
+
+    # ------------------------------------------------------------------ execute
+    @torch.no_grad()
+    def execute(self, bm: BlockManager, out: SchedulerOutput) -> StepOutput:
+        sample_items = out.decodes + [p for p in out.prefills if p.samples]
+        plan = self.prepare(bm, out)
+        logits = self.run(plan)
+        if not sample_items:
+            return StepOutput([], None)
+        return self.sample(logits, sample_items)
+
+    # ------------------------------------------------------------------ graphs
+    @torch.no_grad()
+    def capture_graphs(self, buckets: Optional[List[int]] = None) -> float:
+        if not self.is_gpu or self.cfg.enforce_eager:
+            return 0.0
+        t0 = time.time()
+        buckets = buckets or graph_buckets(self.max_num_seqs, self.cfg.scheduler.decode_bs_bucket_step)
+        self.graph_logits: Dict[int, torch.Tensor] = {}
+        self.graph_pool = torch.cuda.graph_pool_handle()
+        # dummy decode inputs: len 1, slot -1 (no cache write), block 0
+        S = self.max_num_seqs
+        hdr = torch.zeros(4 * S, dtype=torch.int32)
+        hdr[2 * S:3 * S] = -1
+        hdr[3 * S:] = 1
+        self.d_g_hdr.copy_(hdr)
+        self.d_g_bt.zero_()
+        stream = torch.cuda.Stream()
+        stream.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(stream):
+            for Bp in sorted(buckets, reverse=True):
+                P = self._decode_partitions(Bp, self.cfg.scheduler.max_model_len)
+                ids, md = self._graph_metadata(Bp, P)
+                for _ in range(2):       # warm-up (hipBLASLt heuristics, allocator)
+                    h = self.model(ids, md, self.kv_caches)
+                    self.model.compute_logits(h)
+                g = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(g, pool=self.graph_pool, stream=stream):
+                    h = self.model(ids, md, self.kv_caches)
+                    logits = self.model.compute_logits(h)
+                self.graphs[Bp] = g
+                self.graph_logits[Bp] = logits
+        torch.cuda.current_stream().wait_stream(stream)
+        torch.cuda.synchronize()
+        dt = time.time() - t0
+        logger.info("captured %d decode graphs in %.1fs", len(self.graphs), dt)
+        return dt

@@ -1,0 +1,273 @@
+"""Tensor-parallel building blocks (SURVEY §2.11 "TP" row).
+
+Weights are stored [out, in] (torch Linear convention) so ``F.linear`` goes to
+hipBLASLt for the plain GEMMs (K6).  Every parameter carries a ``weight_loader``
+that takes the FULL checkpoint tensor and keeps this rank's shard, so the same
+loader serves TP=1..8 and the TP-vs-TP1 equivalence tests.
+"""
+
+from __future__ import annotations
+
+from typing import List, Optional, Sequence
+
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+from ..parallel import comm, state
+
+
+def _param(shape, dtype, device) -> nn.Parameter:
+    return nn.Parameter(torch.empty(shape, dtype=dtype, device=device), requires_grad=False)
+
+
+def _shard(t: torch.Tensor, dim: int, rank: int, size: int) -> torch.Tensor:
+    n = t.shape[dim]
+    if n % size != 0:
+        raise ValueError(f"dim {dim} of size {n} not divisible by tp={size}")
+    return t.narrow(dim, rank * (n // size), n // size)
+
+
+def default_loader(param: nn.Parameter, loaded: torch.Tensor) -> None:
+    if param.shape != loaded.shape:
+        raise ValueError(f"shape mismatch {tuple(param.shape)} vs {tuple(loaded.shape)}")
+    param.data.copy_(loaded)
+
+
+class ColumnParallelLinear(nn.Module):
+    """y = x W^T (+b), W split along the output dim; optional gather of y."""
+
+    def __init__(self, in_features: int, out_features: int, bias: bool = False,
+                 gather_output: bool = False, dtype=torch.bfloat16, device=None):
+        super().__init__()
+        tp = state.tp_size()
+        self.in_features, self.out_features = in_features, out_features
+        self.out_local = out_features // tp
+        self.gather_output = gather_output
+        self.weight = _param((self.out_local, in_features), dtype, device)
+        self.weight.weight_loader = self._load
+        self.bias = _param((self.out_local,), dtype, device) if bias else None
+        if self.bias is not None:
+            self.bias.weight_loader = self._load
+
+    def _load(self, param, loaded, shard_id=None):
+        param.data.copy_(_shard(loaded, 0, state.tp_rank(), state.tp_size()))
+
+    def forward(self, x):
+        y = F.linear(x, self.weight, self.bias)
+        if self.gather_output:
+            y = comm.all_gather(y, -1)
+        return y
+
+
+class MergedColumnParallelLinear(ColumnParallelLinear):
+    """Several column-parallel outputs fused into one GEMM (e.g. gate_up_proj)."""
+
+    def __init__(self, in_features: int, out_sizes: Sequence[int], bias: bool = False,
+                 dtype=torch.bfloat16, device=None):
+        super().__init__(in_features, sum(out_sizes), bias, False, dtype, device)
+        self.out_sizes = list(out_sizes)
+
+    def _load(self, param, loaded, shard_id=None):
+        tp, r = state.tp_size(), state.tp_rank()
+        if shard_id is None:   # fused checkpoint tensor: split per part first
+            parts = torch.split(loaded, self.out_sizes, dim=0)
+            param.data.copy_(torch.cat([_shard(p, 0, r, tp) for p in parts], 0))
+            return
+        off = sum(self.out_sizes[:shard_id]) // tp
+        n = self.out_sizes[shard_id] // tp
+        param.data.narrow(0, off, n).copy_(_shard(loaded, 0, r, tp))
+
+
+class QKVParallelLinear(ColumnParallelLinear):
+    """Fused q/k/v projection; heads split across ranks (kv heads replicated if < tp)."""
+
+    def __init__(self, hidden: int, head_dim: int, num_heads: int, num_kv_heads: int,
+                 bias: bool = False, dtype=torch.bfloat16, device=None):
+        tp = state.tp_size()
+        if num_heads % tp != 0:
+            raise ValueError("num_heads must be divisible by tensor_parallel_size")
+        self.head_dim = head_dim
+        self.num_heads = num_heads // tp
+        self.kv_replicas = max(1, tp // num_kv_heads)
+        self.num_kv_heads = max(1, num_kv_heads // tp)
+        self.total_kv_heads = num_kv_heads
+        out_local = (self.num_heads + 2 * self.num_kv_heads) * head_dim
+        nn.Module.__init__(self)
+        self.in_features = hidden
+        self.out_local = out_local
+        self.gather_output = False
+        self.weight = _param((out_local, hidden), dtype, device)
+        self.weight.weight_loader = self._load
+        self.bias = _param((out_local,), dtype, device) if bias else None
+        if self.bias is not None:
+            self.bias.weight_loader = self._load
+
+    def _kv_head_range(self):
+        r = state.tp_rank()
+        first = (r // self.kv_replicas) * self.num_kv_heads
+        return first, self.num_kv_heads
+
+    def _load(self, param, loaded, shard_id=None):
+        d = self.head_dim
+        r = state.tp_rank()
+        qn, kvn = self.num_heads * d, self.num_kv_heads * d
+        if shard_id is None:  # fused [q; k; v] checkpoint tensor
+            tq = self.num_heads * state.tp_size() * d
+            tkv = self.total_kv_heads * d
+            q, k, v = torch.split(loaded, [tq, tkv, tkv], dim=0)
+            for sid, t in (("q", q), ("k", k), ("v", v)):
+                self._load(param, t, sid)
+            return
+        if shard_id == "q":
+            param.data.narrow(0, 0, qn).copy_(loaded.narrow(0, r * qn, qn))
+        else:
+            first, n = self._kv_head_range()
+            src = loaded.narrow(0, first * d, n * d)
+            off = qn if shard_id == "k" else qn + kvn
+            param.data.narrow(0, off, kvn).copy_(src)
+
+
+class RowParallelLinear(nn.Module):
+    """y = x W^T (+b), W split along the input dim; all-reduce of the partial sums."""
+
+    def __init__(self, in_features: int, out_features: int, bias: bool = False,
+                 reduce_results: bool = True, dtype=torch.bfloat16, device=None):
+        super().__init__()
+        tp = state.tp_size()
+        self.in_local = in_features // tp
+        self.out_features = out_features
+        self.reduce_results = reduce_results
+        self.weight = _param((out_features, self.in_local), dtype, device)
+        self.weight.weight_loader = self._load
+        self.bias = _param((out_features,), dtype, device) if bias else None
+        if self.bias is not None:
+            self.bias.weight_loader = default_loader
+
+    def _load(self, param, loaded, shard_id=None):
+        param.data.copy_(_shard(loaded, 1, state.tp_rank(), state.tp_size()))
+
+    def forward(self, x):
+        y = F.linear(x, self.weight)
+        if self.reduce_results:
+            y = comm.all_reduce(y)
+        if self.bias is not None:
+            y = y + self.bias
+        return y
+
+
+class ReplicatedLinear(nn.Module):
+    def __init__(self, in_features, out_features, bias=False, dtype=torch.bfloat16, device=None):
+        super().__init__()
+        self.weight = _param((out_features, in_features), dtype, device)
+        self.weight.weight_loader = default_loader
+        self.bias = _param((out_features,), dtype, device) if bias else None
+        if self.bias is not None:
+            self.bias.weight_loader = default_loader
+
+    def forward(self, x):
+        return F.linear(x, self.weight, self.bias)
+
+
+class VocabParallelEmbedding(nn.Module):
+    """Embedding with the vocab split across ranks (K10 + C3)."""
+
+    def __init__(self, vocab: int, dim: int, dtype=torch.bfloat16, device=None):
+        super().__init__()
+        tp = state.tp_size()
+        self.vocab = vocab
+        self.vocab_padded = ((vocab + 64 * tp - 1) // (64 * tp)) * 64 * tp
+        self.per_rank = self.vocab_padded // tp
+        self.start = state.tp_rank() * self.per_rank
+        self.weight = _param((self.per_rank, dim), dtype, device)
+        self.weight.weight_loader = self._load
+
+    def _load(self, param, loaded, shard_id=None):
+        n = max(0, min(self.per_rank, loaded.shape[0] - self.start))
+        param.data.zero_()
+        if n > 0:
+            param.data[:n].copy_(loaded[self.start:self.start + n])
+
+    def forward(self, ids: torch.Tensor) -> torch.Tensor:
+        if state.tp_size() == 1:
+            return F.embedding(ids, self.weight)
+        local = ids - self.start
+        mask = (local < 0) | (local >= self.per_rank)
+        out = F.embedding(local.masked_fill(mask, 0), self.weight)
+        out = out.masked_fill(mask[:, None], 0)
+        return comm.all_reduce(out)
+
+
+class ParallelLMHead(nn.Module):
+    """Vocab-parallel LM head; logits gathered across ranks (C4)."""
+
+    def __init__(self, vocab: int, dim: int, dtype=torch.bfloat16, device=None,
+                 tied: Optional[VocabParallelEmbedding] = None):
+        super().__init__()
+        tp = state.tp_size()
+        self.vocab = vocab
+        self.vocab_padded = ((vocab + 64 * tp - 1) // (64 * tp)) * 64 * tp
+        self.per_rank = self.vocab_padded // tp
+        self.start = state.tp_rank() * self.per_rank
+        if tied is not None:
+            self.weight = tied.weight
+        else:
+            self.weight = _param((self.per_rank, dim), dtype, device)
+            self.weight.weight_loader = VocabParallelEmbedding._load.__get__(self)
+
+    def forward(self, h: torch.Tensor) -> torch.Tensor:
+        logits = F.linear(h, self.weight)
+        if state.tp_size() > 1:
+            logits = comm.all_gather(logits, -1)
+        return logits[..., :self.vocab]
+
+
+class RMSNorm(nn.Module):
+    def __init__(self, dim: int, eps: float, dtype=torch.bfloat16, device=None):
+        super().__init__()
+        self.eps = eps
+        self.weight = _param((dim,), dtype, device)
+        self.weight.weight_loader = default_loader
+
+    def forward(self, x, residual=None):
+        from ..ops import norm
+        if residual is None:
+            return norm.rms_norm(x, self.weight, self.eps)
+        return norm.fused_add_rms_norm(x, residual, self.weight, self.eps)
+
+
+class LayerNorm(nn.Module):
+    def __init__(self, dim: int, eps: float, bias: bool = True, dtype=torch.bfloat16, device=None):
+        super().__init__()
+        self.eps = eps
+        self.weight = _param((dim,), dtype, device)
+        self.weight.weight_loader = default_loader
+        self.bias = _param((dim,), dtype, device) if bias else None
+        if self.bias is not None:
+            self.bias.weight_loader = default_loader
+
+    def forward(self, x, residual=None):
+        from ..ops import norm
+        return norm.layer_norm(x, self.weight, self.bias, self.eps, residual)
+
+
+def init_random_(module: nn.Module, seed: int = 0, std: float = 0.02) -> None:
+    """Deterministic random init of every parameter (north star: random weights).
+
+    Norm weights -> 1, biases -> 0, matrices ~ N(0, std). Generated on the
+    parameter's device (fast for 70B on GPU), seeded per-parameter.
+    """
+    for i, (name, p) in enumerate(module.named_parameters()):
+        g = torch.Generator(device=p.device)
+        g.manual_seed(seed * 1000003 + i)
+        if p.dim() == 1:
+            if "norm" in name or name.endswith("ln.weight") or "layernorm" in name.lower():
+                p.data.fill_(1.0)
+            else:
+                p.data.zero_()
+        else:
+            p.data.normal_(0.0, std, generator=g)
+
+
+def all_weight_loaders(module: nn.Module) -> List[str]:
+    return [n for n, p in module.named_parameters() if not hasattr(p, "weight_loader")]

@@ -1,0 +1,148 @@
+"""Paged attention ops (K1 decode, K2 varlen prefill) -> csrc/kernels/attention.hip.
+
+A step's token batch is laid out as [decode tokens (1 per sequence) | prefill
+tokens (varlen chunks)].  Both parts read K/V from the paged cache (the K4
+kernel has already written this step's K/V), so chunked prefill and prefix
+caching need no special path.
+"""
+
+from __future__ import annotations
+
+import dataclasses
+import math
+from typing import List, Optional, Sequence
+
+import torch
+
+from . import reference as ref
+from ._dispatch import check, lib, ptr, require, stream, use_hip
+
+
+def heads_per_workgroup(num_heads: int, num_kv_heads: int) -> int:
+    g = num_heads // num_kv_heads
+    return 4 if g % 4 == 0 else 2 if g % 2 == 0 else 1
+
+
+def prefill_query_block(num_heads: int, num_kv_heads: int) -> int:
+    """Queries covered by one prefill workgroup (4 waves x 16 columns / heads-per-WG)."""
+    return 16 * (4 // heads_per_workgroup(num_heads, num_kv_heads))
+
+
+def build_prefill_work(q_lens: Sequence[int], qblock: int) -> List[int]:
+    work: List[int] = []
+    for s, n in enumerate(q_lens):
+        for q0 in range(0, n, qblock):
+            work += [s, q0]
+    return work
+
+
+def decode_partitions(batch: int, num_kv_heads: int, num_heads: int, max_len: int,
+                      target_wgs: int = 1024, max_parts: int = 16) -> int:
+    g = num_heads // num_kv_heads
+    wgs = max(1, batch * num_kv_heads * ((g + 15) // 16))
+    p = max(1, math.ceil(target_wgs / wgs))
+    p = min(p, max_parts, max(1, math.ceil(max_len / 256)))
+    return p
+
+
+@dataclasses.dataclass
+class AttentionMetadata:
+    num_decode: int
+    num_prefill_tokens: int
+    slot_mapping: torch.Tensor                 # [T] int32
+    positions: torch.Tensor                    # [T] int32
+    # decode part (rows may be padded with seq_len 0 for HIP-graph buckets)
+    decode_block_tables: Optional[torch.Tensor] = None   # [Bd, maxb] int32
+    decode_seq_lens: Optional[torch.Tensor] = None       # [Bd] int32
+    decode_partitions: int = 1
+    decode_part_o: Optional[torch.Tensor] = None
+    decode_part_ml: Optional[torch.Tensor] = None
+    # prefill part
+    prefill_block_tables: Optional[torch.Tensor] = None  # [Sp, maxb] int32
+    prefill_seq_lens: Optional[torch.Tensor] = None      # [Sp] int32 (context + new)
+    prefill_cu_q: Optional[torch.Tensor] = None          # [Sp+1] int32
+    prefill_work: Optional[torch.Tensor] = None          # [n_work*2] int32
+    prefill_n_work: int = 0
+    causal: bool = True
+
+    @property
+    def num_tokens(self) -> int:
+        return self.num_decode + self.num_prefill_tokens
+
+
+def paged_decode(q: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tensor,
+                 block_tables: torch.Tensor, seq_lens: torch.Tensor, scale: float,
+                 partitions: int = 1, part_o: Optional[torch.Tensor] = None,
+                 part_ml: Optional[torch.Tensor] = None,
+                 out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """q [B, Hq, D] -> out [B, Hq, D]."""
+    if not (use_hip(q, k_cache) and q.dtype == torch.bfloat16):
+        r = ref.paged_attention_decode(q, k_cache, v_cache, block_tables, seq_lens, scale)
+        if out is not None:
+            out.copy_(r)
+            return out
+        return r
+    B, Hq, D = q.shape
+    Hkv, bs = k_cache.shape[1], k_cache.shape[2]
+    require(q.stride(2) == 1 and q.stride(1) == D, "paged_decode: q layout [B,Hq,D]")
+    require(block_tables.dtype == torch.int32 and seq_lens.dtype == torch.int32, "int32 metadata")
+    require(block_tables.shape[0] >= B and seq_lens.shape[0] >= B, "metadata rows < batch")
+    require(block_tables.stride(1) == 1, "block_tables rows must be contiguous")
+    o = torch.empty_like(q) if out is None else out
+    if partitions > 1:
+        need = B * Hq * partitions
+        require(part_o is not None and part_o.numel() >= need * D and part_ml.numel() >= need * 2,
+                "decode workspace too small")
+    check(lib().eia_paged_decode(
+        ptr(q), q.stride(0), ptr(k_cache), ptr(v_cache), ptr(block_tables), block_tables.stride(0),
+        ptr(seq_lens), ptr(o), o.stride(0), ptr(part_o) if partitions > 1 else None,
+        ptr(part_ml) if partitions > 1 else None, float(scale), B, Hq, Hkv, D, bs, partitions,
+        stream(q)), "paged_decode")
+    return o
+
+
+def paged_prefill(q: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tensor,
+                  block_tables: torch.Tensor, seq_lens: torch.Tensor, cu_q: torch.Tensor,
+                  work: Optional[torch.Tensor], n_work: int, scale: float, causal: bool = True,
+                  sliding_window: Optional[int] = None, chunk_size: Optional[int] = None,
+                  out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """q [T, Hq, D] (varlen, cu_q) -> out [T, Hq, D]."""
+    if not (use_hip(q, k_cache) and q.dtype == torch.bfloat16):
+        r = ref.paged_attention_prefill(q, k_cache, v_cache, block_tables, cu_q, seq_lens, scale,
+                                        causal, sliding_window, chunk_size)
+        if out is not None:
+            out.copy_(r)
+            return out
+        return r
+    T, Hq, D = q.shape
+    Hkv, bs = k_cache.shape[1], k_cache.shape[2]
+    require(q.stride(2) == 1 and q.stride(1) == D, "paged_prefill: q layout [T,Hq,D]")
+    for t in (block_tables, seq_lens, cu_q, work):
+        require(t is not None and t.dtype == torch.int32 and t.is_cuda, "int32 device metadata")
+    require(block_tables.stride(1) == 1, "block_tables rows must be contiguous")
+    o = torch.empty_like(q) if out is None else out
+    hpw = heads_per_workgroup(Hq, Hkv)
+    check(lib().eia_paged_prefill(
+        ptr(q), q.stride(0), ptr(o), o.stride(0), ptr(k_cache), ptr(v_cache), ptr(block_tables),
+        block_tables.stride(0), ptr(seq_lens), ptr(cu_q), ptr(work), n_work, float(scale), Hq, Hkv,
+        D, bs, hpw, 1 if causal else 0, sliding_window or 0, chunk_size or 0, stream(q)),
+        "paged_prefill")
+    return o
+
+
+def attention(q: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tensor,
+              md: AttentionMetadata, scale: float, sliding_window: Optional[int] = None,
+              chunk_size: Optional[int] = None) -> torch.Tensor:
+    """Dispatch the step's decode and prefill parts. q [T, Hq, D]."""
+    nd = md.num_decode
+    if md.num_prefill_tokens == 0:
+        return paged_decode(q[:nd], k_cache, v_cache, md.decode_block_tables, md.decode_seq_lens,
+                            scale, md.decode_partitions, md.decode_part_o, md.decode_part_ml)
+    out = torch.empty_like(q)
+    if nd:
+        paged_decode(q[:nd], k_cache, v_cache, md.decode_block_tables, md.decode_seq_lens, scale,
+                     md.decode_partitions, md.decode_part_o, md.decode_part_ml, out=out[:nd])
+    paged_prefill(q[nd:], k_cache, v_cache, md.prefill_block_tables, md.prefill_seq_lens,
+                  md.prefill_cu_q, md.prefill_work, md.prefill_n_work, scale, md.causal,
+                  sliding_window, chunk_size, out=out[nd:])
+    return out

@@ -1,0 +1,51 @@
+"""Fused RoPE + paged-KV write (K4 + K3) -> csrc/kernels/rope_cache.hip."""
+
+from __future__ import annotations
+
+from typing import Optional
+
+import torch
+
+from . import reference as ref
+from ._dispatch import check, lib, ptr, require, stream, use_hip
+
+
+class RotaryCache:
+    """Per-model cos/sin table [max_pos, head_dim] fp32 (cos | sin halves)."""
+
+    def __init__(self, head_dim: int, max_pos: int, theta: float, scaling: Optional[dict],
+                 device: torch.device, is_neox: bool = True):
+        self.head_dim = head_dim
+        self.is_neox = is_neox
+        self.cos_sin = ref.rope_cos_sin_cache(max_pos, head_dim, theta, scaling).to(device)
+
+
+def rope_qkv_cache(qkv: torch.Tensor, positions: Optional[torch.Tensor],
+                   rotary: Optional[RotaryCache], slot_mapping: torch.Tensor,
+                   k_cache: torch.Tensor, v_cache: torch.Tensor, num_heads: int,
+                   num_kv_heads: int, head_dim: int, bias: Optional[torch.Tensor] = None,
+                   q_norm_w: Optional[torch.Tensor] = None, k_norm_w: Optional[torch.Tensor] = None,
+                   norm_eps: float = 1e-6) -> torch.Tensor:
+    """qkv [T, (Hq+2Hkv)*D] -> q [T, Hq, D]; k/v scattered into the paged cache."""
+    cos_sin = None if rotary is None else rotary.cos_sin
+    if not (use_hip(qkv, k_cache) and qkv.dtype == torch.bfloat16):
+        if rotary is not None and not rotary.is_neox:
+            raise NotImplementedError("GPT-J style RoPE only on the HIP path")
+        return ref.rope_qkv_cache(qkv, positions, cos_sin, slot_mapping, k_cache, v_cache,
+                                  num_heads, num_kv_heads, head_dim, bias, q_norm_w, k_norm_w,
+                                  norm_eps)
+    T = qkv.shape[0]
+    require(qkv.stride(-1) == 1 and qkv.shape[1] == (num_heads + 2 * num_kv_heads) * head_dim,
+            "rope_qkv_cache: qkv shape")
+    require(slot_mapping.dtype == torch.int32 and slot_mapping.numel() >= T, "slot_mapping int32[T]")
+    if positions is not None:
+        require(positions.dtype == torch.int32, "positions must be int32")
+    require(k_cache.shape[1] == num_kv_heads and k_cache.shape[3] == head_dim, "k_cache layout")
+    require(v_cache.shape[2] == head_dim, "v_cache layout")
+    q = torch.empty((T, num_heads, head_dim), dtype=qkv.dtype, device=qkv.device)
+    check(lib().eia_rope_qkv_cache(
+        ptr(qkv), qkv.stride(0), ptr(positions), ptr(cos_sin), ptr(slot_mapping), ptr(k_cache),
+        ptr(v_cache), ptr(q), ptr(bias), ptr(q_norm_w), ptr(k_norm_w), float(norm_eps), T,
+        num_heads, num_kv_heads, head_dim, k_cache.shape[2],
+        1 if (rotary is None or rotary.is_neox) else 0, stream(qkv)), "rope_qkv_cache")
+    return q

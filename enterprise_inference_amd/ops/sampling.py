@@ -1,0 +1,115 @@
+"""Token sampling (K8) -> csrc/kernels/sampling.hip.
+
+The CPU reference implements the SAME counter-based RNG (splitmix64 over
+(seed, token id)) so a seeded request samples identically on both paths.
+"""
+
+from __future__ import annotations
+
+from typing import Optional
+
+import torch
+
+from . import reference as ref
+from ._dispatch import check, lib, ptr, require, stream, use_hip
+
+_M64 = (1 << 64) - 1
+
+
+def _s64(x: int) -> int:
+    x &= _M64
+    return x - (1 << 64) if x >= (1 << 63) else x
+
+
+_C0 = _s64(0x9E3779B97F4A7C15)
+_C1 = _s64(0xBF58476D1CE4E5B9)
+_C2 = _s64(0x94D049BB133111EB)
+_CI = _s64(0xD1B54A32D192ED03)
+
+
+def _lsr(x: torch.Tensor, k: int) -> torch.Tensor:
+    return (x >> k) & ((1 << (64 - k)) - 1)
+
+
+def splitmix64_t(x: torch.Tensor) -> torch.Tensor:
+    x = x + _C0
+    x = (x ^ _lsr(x, 30)) * _C1
+    x = (x ^ _lsr(x, 27)) * _C2
+    return x ^ _lsr(x, 31)
+
+
+def splitmix64_int(x: int) -> int:
+    x = (x + 0x9E3779B97F4A7C15) & _M64
+    x = ((x ^ (x >> 30)) * 0xBF58476D1CE4E5B9) & _M64
+    x = ((x ^ (x >> 27)) * 0x94D049BB133111EB) & _M64
+    return x ^ (x >> 31)
+
+
+def row_seed(request_seed: int, step: int) -> int:
+    """Per (request, output index) seed, as a signed int64 for torch."""
+    return _s64(splitmix64_int((request_seed & _M64) ^ (step * 0x2545F4914F6CDD1D & _M64)))
+
+
+def uniform_t(seeds: torch.Tensor, V: int) -> torch.Tensor:
+    """[B, V] float32 uniforms in (0,1), bit-identical to rng_uniform() in the kernel."""
+    idx = torch.arange(1, V + 1, dtype=torch.int64, device=seeds.device)
+    h = splitmix64_t(seeds.to(torch.int64)[:, None] ^ (idx[None, :] * _CI))
+    return (_lsr(h, 40).to(torch.float32) + 0.5) * (1.0 / 16777216.0)
+
+
+def sample_reference(logits: torch.Tensor, temperature: torch.Tensor, top_k: torch.Tensor,
+                     top_p: torch.Tensor, min_p: torch.Tensor, seeds: torch.Tensor) -> torch.Tensor:
+    logits = logits.float()
+    greedy = logits.argmax(-1).to(torch.int32)
+    t = temperature.float()
+    if not bool((t > 0).any()):
+        return greedy
+    tt = torch.where(t > 0, t, torch.ones_like(t))
+    masked = ref.top_k_top_p_min_p_mask(logits / tt[:, None], top_k, top_p.float(), min_p.float())
+    u = uniform_t(seeds, logits.shape[-1])
+    g = masked - torch.log(-torch.log(u))
+    sampled = g.argmax(-1).to(torch.int32)
+    return torch.where(t > 0, sampled, greedy)
+
+
+def sample(logits: torch.Tensor, temperature: torch.Tensor, top_k: torch.Tensor,
+           top_p: torch.Tensor, min_p: torch.Tensor, seeds: torch.Tensor,
+           out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """logits fp32 [B, V]; per-row params on the same device. Returns int32 [B]."""
+    if not use_hip(logits):
+        r = sample_reference(logits, temperature, top_k, top_p, min_p, seeds)
+        if out is not None:
+            out.copy_(r)
+            return out
+        return r
+    require(logits.dtype == torch.float32 and logits.stride(-1) == 1, "sample: fp32 logits")
+    B, V = logits.shape
+    for t, dt in ((temperature, torch.float32), (top_k, torch.int32), (top_p, torch.float32),
+                  (min_p, torch.float32), (seeds, torch.int64)):
+        require(t.dtype == dt and t.is_cuda and t.numel() >= B, f"sample: param {dt}")
+    o = torch.empty(B, dtype=torch.int32, device=logits.device) if out is None else out
+    check(lib().eia_sample(ptr(logits), logits.stride(0), B, V, ptr(temperature), ptr(top_k),
+                           ptr(top_p), ptr(min_p), ptr(seeds), ptr(o), stream(logits)), "sample")
+    return o
+
+
+def apply_penalties(logits: torch.Tensor, rows: torch.Tensor, toks: torch.Tensor,
+                    counts: torch.Tensor, rep: torch.Tensor, freq: torch.Tensor,
+                    pres: torch.Tensor) -> torch.Tensor:
+    """In-place sparse penalties; (row, tok) pairs must be unique."""
+    n = rows.numel()
+    if n == 0:
+        return logits
+    if not use_hip(logits):
+        r, t = rows.long(), toks.long()
+        l = logits[r, t]
+        rp = rep[r]
+        l = torch.where(l > 0, l / rp, l * rp)
+        c = counts.float()
+        l = torch.where(c > 0, l - freq[r] * c - pres[r], l)
+        logits[r, t] = l
+        return logits
+    check(lib().eia_apply_penalties(ptr(logits), logits.stride(0), ptr(rows), ptr(toks),
+                                    ptr(counts), n, ptr(rep), ptr(freq), ptr(pres),
+                                    stream(logits)), "apply_penalties")
+    return logits
