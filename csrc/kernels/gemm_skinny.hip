@@ -1,0 +1,359 @@
+// K6 / K7: weight-streaming "skinny" GEMM for decode-sized M (M <= 128).
+//
+//   Y[M, N] = X[M, K] . W[N, K]^T      (torch Linear layout, bf16 in, fp32 accumulate)
+//
+// Decode GEMMs are HBM-bound on the weight stream (Llama-3.1-8B at batch 65:
+// 16 GB of weights per step, ~1 TFLOP).  The profile of hipBLASLt on these
+// shapes (profiles/rocprof_r1_baseline.md) showed 2-3.8 TB/s; the design here
+// targets the ~6 TB/s HBM ceiling:
+//
+//  * W is the MFMA A operand (rows = n), X the B operand (columns = m), with
+//    v_mfma_f32_16x16x32_bf16.  Within a 128-deep K "super-step" lane (r, g)
+//    of a wave reads W[n0 + r][kb + 32g .. kb + 32g + 32) -- 64 contiguous bytes
+//    per row as four 16-B loads -- and MFMA step s consumes elements 8s..8s+7
+//    of that run.  Any k permutation is legal as long as X uses the same one,
+//    so W is streamed in its native layout with full-row coalescing and no
+//    re-layout (prefill keeps using the same tensor through hipBLASLt).
+//  * X (tiny, L2-resident) is staged per 256-deep K chunk into LDS (register
+//    staging, padded rows) and shared by the workgroup's waves; W for chunk
+//    c+1 is in flight (registers) while chunk c is multiplied, so every wave
+//    keeps 16 KiB of weight loads outstanding.
+//  * Each wave owns two 16-row tiles (NT = 2); a 128-thread workgroup covers
+//    64 rows.  Small-N shapes are split over K across workgroups (grid.y) so
+//    the grid covers all 256 CUs (per-CU HBM rate is the limit, not MFMA);
+//    split partials are fp32 slabs [SK][M][N] reduced by the consumer
+//    (splitk_reduce / splitk_add_rmsnorm below, fused with bias / residual).
+//  * Mode SWIGLU (K7): tile 0 of a wave is gate rows [n0, n0+16) and tile 1 the
+//    matching up rows [I + n0, ...) of the merged gate_up weight, so the
+//    epilogue writes silu(g) * u directly ([M, I]); the 2I-wide intermediate
+//    never reaches HBM.
+#include "eia_common.h"
+
+namespace {
+
+constexpr int KC = 256;             // K chunk per pipeline stage
+constexpr int XPAD = 8;             // LDS row padding (elements)
+constexpr int XLD = KC + XPAD;      // LDS row stride (elements)
+
+enum Mode : int { MODE_BF16 = 0, MODE_F32_SPLIT = 1, MODE_SWIGLU = 2 };
+
+EIA_DEV float silu(float x) { return x / (1.f + __expf(-x)); }
+
+// Once-read weight stream: non-temporal loads (guide: MI355X_MICROARCH "nt-weights").
+EIA_DEV bf16x8 ld_nt(const bf16_t* p) {
+#ifdef EIA_GEMM_NT
+  return __builtin_bit_cast(bf16x8, __builtin_nontemporal_load(reinterpret_cast<const s16x8*>(p)));
+#else
+  return *reinterpret_cast<const bf16x8*>(p);
+#endif
+}
+
+// MT: 16-column tiles of X (M <= 16*MT); NT: 16-row W tiles per wave; WAVES per workgroup.
+template <int MT, int NT, int WAVES>
+__global__ void __launch_bounds__(WAVES * 64)
+gemm_skinny_kernel(const bf16_t* __restrict__ X, long ldx, const bf16_t* __restrict__ W, long ldw,
+                   const bf16_t* __restrict__ bias, void* __restrict__ out, long ldo, int M, int N,
+                   int krange, int mode, int inter) {
+  extern __shared__ __align__(16) bf16_t xs[];   // [2][MT*16][XLD]
+  const int lane = threadIdx.x & 63;
+  const int wave = threadIdx.x >> 6;
+  const int r = lane & 15, g = lane >> 4;
+  const int k0 = blockIdx.y * krange;
+  const int nchunks = krange / KC;
+  const int last = nchunks - 1;
+
+  // rows of W owned by this wave's tiles
+  const bf16_t* wp[NT];
+  int nbase;
+  if (NT == 2 && mode == MODE_SWIGLU) {
+    nbase = blockIdx.x * (WAVES * 16) + wave * 16;      // output column block
+    wp[0] = W + (long)(nbase + r) * ldw + k0 + 32 * g;
+    wp[NT - 1] = W + (long)(inter + nbase + r) * ldw + k0 + 32 * g;
+  } else {
+    nbase = blockIdx.x * (WAVES * NT * 16) + wave * (NT * 16);
+#pragma unroll
+    for (int t = 0; t < NT; ++t) wp[t] = W + (long)(nbase + 16 * t + r) * ldw + k0 + 32 * g;
+  }
+
+  constexpr int XV = MT * 16 * (KC / 8);                // 16-B vectors per X chunk
+  constexpr int XPT = XV / (WAVES * 64);                // per thread
+  static_assert(XV % (WAVES * 64) == 0, "X chunk split");
+
+  auto load_x = [&](int c, bf16x8 (&xr)[XPT]) {
+#pragma unroll
+    for (int j = 0; j < XPT; ++j) {
+      const int v = threadIdx.x + j * WAVES * 64;
+      const int row = v / (KC / 8), col = (v % (KC / 8)) * 8;
+      const int xrow = row < M ? row : M - 1;          // clamp: padded columns are never stored
+      xr[j] = *reinterpret_cast<const bf16x8*>(X + (long)xrow * ldx + k0 + c * KC + col);
+    }
+  };
+  auto store_x = [&](int buf, const bf16x8 (&xr)[XPT]) {
+#pragma unroll
+    for (int j = 0; j < XPT; ++j) {
+      const int v = threadIdx.x + j * WAVES * 64;
+      const int row = v / (KC / 8), col = (v % (KC / 8)) * 8;
+      *reinterpret_cast<bf16x8*>(xs + (buf * MT * 16 + row) * XLD + col) = xr[j];
+    }
+  };
+  // W fragments of one chunk: [tile][superstep*4 + s]; lane (r, g) covers
+  // k = 128*superstep + 32g + 8s + j of the chunk
+  auto load_w = [&](int c, bf16x8 (&w)[NT][8]) {
+#pragma unroll
+    for (int t = 0; t < NT; ++t)
+#pragma unroll
+      for (int ss = 0; ss < 2; ++ss)
+#pragma unroll
+        for (int s = 0; s < 4; ++s) w[t][ss * 4 + s] = ld_nt(wp[t] + c * KC + 128 * ss + 8 * s);
+  };
+
+  f32x4 acc[NT][MT];
+#pragma unroll
+  for (int t = 0; t < NT; ++t)
+#pragma unroll
+    for (int m = 0; m < MT; ++m) acc[t][m] = (f32x4){0.f, 0.f, 0.f, 0.f};
+
+  auto compute = [&](int buf, const bf16x8 (&w)[NT][8]) {
+    const bf16_t* xb = xs + (buf * MT * 16 + r) * XLD + 32 * g;
+#pragma unroll
+    for (int st = 0; st < 8; ++st) {
+      bf16x8 xf[MT];
+#pragma unroll
+      for (int m = 0; m < MT; ++m)
+        xf[m] = *reinterpret_cast<const bf16x8*>(xb + m * 16 * XLD + 128 * (st >> 2) + 8 * (st & 3));
+#pragma unroll
+      for (int m = 0; m < MT; ++m)
+#pragma unroll
+        for (int t = 0; t < NT; ++t)
+          acc[t][m] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w[t][st], xf[m], acc[t][m], 0, 0, 0);
+    }
+  };
+
+  // Pipeline: two named W register sets (no copies: guide rule 20); each phase
+  // issues X(c+1) then W(c+1) -- pinned ahead of the MFMAs with sched_barrier,
+  // since hipcc otherwise sinks the X loads behind the compute and waits vmcnt(0)
+  // on them -- so the in-order vmcnt wait for X before its ds_write leaves the
+  // weight prefetch in flight.  Loads are unconditional (chunk index clamped)
+  // and the loop body has no early exit, so the vmcnt accounting stays exact.
+  bf16x8 wa[NT][8], wb[NT][8];
+  {
+    bf16x8 xr[XPT];
+    load_x(0, xr);
+    load_w(0, wa);
+    store_x(0, xr);
+  }
+  __syncthreads();
+#define EIA_PHASE(C, WCUR, WNEXT)                 \
+  {                                               \
+    bf16x8 xr[XPT];                               \
+    load_x(min((C) + 1, last), xr);               \
+    load_w(min((C) + 1, last), WNEXT);            \
+    __builtin_amdgcn_sched_barrier(0);            \
+    compute((C) & 1, WCUR);                       \
+    __builtin_amdgcn_sched_barrier(0);            \
+    store_x(((C) + 1) & 1, xr);                   \
+    __syncthreads();                              \
+  }
+  int c = 0;
+  for (; c + 2 <= nchunks; c += 2) {
+    EIA_PHASE(c, wa, wb);
+    EIA_PHASE(c + 1, wb, wa);
+  }
+  if (c < nchunks) EIA_PHASE(c, wa, wb);
+#undef EIA_PHASE
+
+  // epilogue: lane (r, g) holds rows n = tile_base + 4g + i, column m = 16*mt + r
+  if (NT == 2 && mode == MODE_SWIGLU) {
+    bf16_t* o = reinterpret_cast<bf16_t*>(out);
+    const int n = nbase + 4 * g;
+#pragma unroll
+    for (int m = 0; m < MT; ++m) {
+      const int row = m * 16 + r;
+      if (row < M) {
+        bf16x4 v;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) v[i] = f2bf(silu(acc[0][m][i]) * acc[NT - 1][m][i]);
+        *reinterpret_cast<bf16x4*>(o + (long)row * ldo + n) = v;
+      }
+    }
+    return;
+  }
+#pragma unroll
+  for (int t = 0; t < NT; ++t) {
+    const int n = nbase + 16 * t + 4 * g;
+    if (mode == MODE_F32_SPLIT) {
+      float* o = reinterpret_cast<float*>(out) + (long)blockIdx.y * M * N;
+#pragma unroll
+      for (int m = 0; m < MT; ++m) {
+        const int row = m * 16 + r;
+        if (row < M) *reinterpret_cast<f32x4*>(o + (long)row * N + n) = acc[t][m];
+      }
+    } else {
+      bf16_t* o = reinterpret_cast<bf16_t*>(out);
+      float b[4] = {0.f, 0.f, 0.f, 0.f};
+      if (bias != nullptr) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) b[i] = bf2f(bias[n + i]);
+      }
+#pragma unroll
+      for (int m = 0; m < MT; ++m) {
+        const int row = m * 16 + r;
+        if (row < M) {
+          bf16x4 v;
+#pragma unroll
+          for (int i = 0; i < 4; ++i) v[i] = f2bf(acc[t][m][i] + b[i]);
+          *reinterpret_cast<bf16x4*>(o + (long)row * ldo + n) = v;
+        }
+      }
+    }
+  }
+}
+
+// Sum SK fp32 slabs [SK][M][N] (+bias) -> bf16 out[M][ldo].  One thread per 4 columns.
+__global__ void __launch_bounds__(256)
+splitk_reduce_kernel(const float* __restrict__ part, int sk, int M, int N,
+                     const bf16_t* __restrict__ bias, bf16_t* __restrict__ out, long ldo) {
+  const long idx = ((long)blockIdx.x * blockDim.x + threadIdx.x) * 4;
+  const long total = (long)M * N;
+  if (idx >= total) return;
+  const int row = idx / N, col = idx % N;
+  f32x4 s = *reinterpret_cast<const f32x4*>(part + idx);
+  for (int k = 1; k < sk; ++k) s += *reinterpret_cast<const f32x4*>(part + (long)k * total + idx);
+  bf16x4 v;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) v[i] = f2bf(s[i] + (bias ? bf2f(bias[col + i]) : 0.f));
+  *reinterpret_cast<bf16x4*>(out + (long)row * ldo + col) = v;
+}
+
+// residual[M][H] += sum_k part[k] ; out = rmsnorm(residual) * w   (one workgroup per row)
+template <int VPT>
+__global__ void __launch_bounds__(256)
+splitk_add_rmsnorm_kernel(const float* __restrict__ part, int sk, int M, int H,
+                          bf16_t* __restrict__ residual, const bf16_t* __restrict__ w, float eps,
+                          bf16_t* __restrict__ out, long ldo) {
+  __shared__ float scratch[4];
+  const int row = blockIdx.x;
+  const long total = (long)M * H;
+  float v[VPT][4];
+  float ss = 0.f;
+#pragma unroll
+  for (int i = 0; i < VPT; ++i) {
+    const int c = (threadIdx.x + i * 256) * 4;
+    if (c < H) {
+      const long off = (long)row * H + c;
+      f32x4 a = *reinterpret_cast<const f32x4*>(part + off);
+      for (int k = 1; k < sk; ++k) a += *reinterpret_cast<const f32x4*>(part + k * total + off);
+      bf16x4 rr = *reinterpret_cast<const bf16x4*>(residual + off);
+      bf16x4 nr;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        nr[j] = f2bf(a[j] + bf2f(rr[j]));
+        v[i][j] = bf2f(nr[j]);
+        ss += v[i][j] * v[i][j];
+      }
+      *reinterpret_cast<bf16x4*>(residual + off) = nr;
+    }
+  }
+  const float tot = block_sum(ss, scratch);
+  const float inv = rsqrtf(tot / (float)H + eps);
+#pragma unroll
+  for (int i = 0; i < VPT; ++i) {
+    const int c = (threadIdx.x + i * 256) * 4;
+    if (c < H) {
+      bf16x4 ww = *reinterpret_cast<const bf16x4*>(w + c);
+      bf16x4 o;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) o[j] = f2bf(v[i][j] * inv * bf2f(ww[j]));
+      *reinterpret_cast<bf16x4*>(out + (long)row * ldo + c) = o;
+    }
+  }
+}
+
+template <int MT, int NT, int WAVES>
+int launch_cfg(const bf16_t* X, long ldx, const bf16_t* W, long ldw, const bf16_t* bias, void* out,
+               long ldo, int M, int N, int K, int sk, int mode, hipStream_t st) {
+  const size_t lds = 2ull * MT * 16 * XLD * sizeof(bf16_t);
+  static bool attr_set = false;   // > 64 KiB of dynamic LDS must be opted into
+  if (!attr_set) {
+    hipFuncSetAttribute(reinterpret_cast<const void*>(gemm_skinny_kernel<MT, NT, WAVES>),
+                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    attr_set = true;
+  }
+  dim3 grid(mode == MODE_SWIGLU ? (N / 2) / (WAVES * 16) : N / (WAVES * NT * 16), sk);
+  hipLaunchKernelGGL((gemm_skinny_kernel<MT, NT, WAVES>), grid, dim3(WAVES * 64), lds, st, X, ldx,
+                     W, ldw, bias, out, ldo, M, N, K / sk, mode, N / 2);
+  return (int)hipGetLastError();
+}
+
+template <int MT>
+int launch_mt(int cfg, const bf16_t* X, long ldx, const bf16_t* W, long ldw, const bf16_t* bias,
+              void* out, long ldo, int M, int N, int K, int sk, int mode, hipStream_t st) {
+  switch (cfg) {   // cfg = (NT - 1) | ((WAVES / 2 - 1) << 1)
+    case 0: return launch_cfg<MT, 1, 2>(X, ldx, W, ldw, bias, out, ldo, M, N, K, sk, mode, st);
+    case 1: return launch_cfg<MT, 2, 2>(X, ldx, W, ldw, bias, out, ldo, M, N, K, sk, mode, st);
+    case 2: return launch_cfg<MT, 1, 4>(X, ldx, W, ldw, bias, out, ldo, M, N, K, sk, mode, st);
+    default: return launch_cfg<MT, 2, 4>(X, ldx, W, ldw, bias, out, ldo, M, N, K, sk, mode, st);
+  }
+}
+
+}  // namespace
+
+// mode 0: out bf16 [M][ldo] (+bias), sk must be 1
+// mode 1: out fp32 partial slabs [sk][M][N] (reduce with eia_splitk_reduce / _add_rmsnorm)
+// mode 2: SwiGLU: W = merged [gate; up] (N = 2I rows), out bf16 [M][ldo] = silu(gate) * up
+// cfg: bit0 -> two 16-row W tiles per wave (else one), bit1 -> 4 waves per workgroup (else 2)
+EIA_API int eia_gemm_skinny(const void* X, long ldx, const void* W, long ldw, const void* bias,
+                            void* out, long ldo, int M, int N, int K, int sk, int mode, int cfg,
+                            hipStream_t st) {
+  const int nt = (cfg & 1) ? 2 : 1, waves = (cfg & 2) ? 4 : 2;
+  if (M < 1 || M > 128 || sk < 1 || K % (sk * KC) != 0 || cfg < 0 || cfg > 3) return EIA_BAD_SHAPE;
+  if (mode == MODE_SWIGLU) {
+    if (nt != 2 || sk != 1 || N % 2 != 0 || (N / 2) % (waves * 16) != 0) return EIA_BAD_SHAPE;
+  } else if (N % (waves * nt * 16) != 0) {
+    return EIA_BAD_SHAPE;
+  }
+  if (mode == MODE_BF16 && sk != 1) return EIA_BAD_SHAPE;
+  if ((ldx % 8) || (ldw % 8) || (ldo % 4)) return EIA_BAD_SHAPE;
+  const bf16_t* x = static_cast<const bf16_t*>(X);
+  const bf16_t* w = static_cast<const bf16_t*>(W);
+  const bf16_t* b = static_cast<const bf16_t*>(bias);
+  const int mt = (M + 15) / 16;
+#define EIA_MT(V) return launch_mt<V>(cfg, x, ldx, w, ldw, b, out, ldo, M, N, K, sk, mode, st)
+  switch (mt) {
+    case 1: EIA_MT(1);
+    case 2: EIA_MT(2);
+    case 3: EIA_MT(3);
+    case 4: EIA_MT(4);
+    case 5: EIA_MT(5);
+    case 6: EIA_MT(6);
+    case 7: EIA_MT(7);
+    default: EIA_MT(8);
+  }
+#undef EIA_MT
+}
+
+EIA_API int eia_splitk_reduce(const float* part, int sk, int M, int N, const void* bias, void* out,
+                              long ldo, hipStream_t st) {
+  if (N % 4 != 0) return EIA_BAD_SHAPE;
+  const long n4 = (long)M * N / 4;
+  hipLaunchKernelGGL(splitk_reduce_kernel, dim3((n4 + 255) / 256), dim3(256), 0, st, part, sk, M, N,
+                     static_cast<const bf16_t*>(bias), static_cast<bf16_t*>(out), ldo);
+  EIA_LAUNCH_CHECK();
+}
+
+EIA_API int eia_splitk_add_rmsnorm(const float* part, int sk, int M, int H, void* residual,
+                                   const void* w, float eps, void* out, long ldo, hipStream_t st) {
+  if (H % 4 != 0 || H > 4 * 256 * 16) return EIA_BAD_SHAPE;
+  const int vpt = (H / 4 + 255) / 256;
+  bf16_t* res = static_cast<bf16_t*>(residual);
+  const bf16_t* ww = static_cast<const bf16_t*>(w);
+  bf16_t* o = static_cast<bf16_t*>(out);
+#define EIA_SKN(V)                                                                              \
+  hipLaunchKernelGGL(splitk_add_rmsnorm_kernel<V>, dim3(M), dim3(256), 0, st, part, sk, M, H, res, \
+                     ww, eps, o, ldo)
+  if (vpt <= 4) EIA_SKN(4);
+  else if (vpt <= 8) EIA_SKN(8);
+  else EIA_SKN(16);
+#undef EIA_SKN
+  EIA_LAUNCH_CHECK();
+}

@@ -49,7 +49,9 @@ _SIGNATURES = {
     "eia_moe_align": [P, I, I, I, I, P, P, P, P, S],
     "eia_grouped_gemm": [P, P, P, P, P, P, I, I, I, I, I, I, I, S],
     "eia_moe_combine": [P, P, P, P, I, I, I, S],
-    "eia_gemm": [P, P, P, P, I, I, I, I, I, S],
+    "eia_gemm_skinny": [P, L, P, L, P, P, L, I, I, I, I, I, I, S],
+    "eia_splitk_reduce": [P, I, I, I, P, P, L, S],
+    "eia_splitk_add_rmsnorm": [P, I, I, I, P, P, F, P, L, S],
     "eia_ar_oneshot": [P, P, P, P, I, I, I, L, I, S],
     "eia_ar_twoshot": [P, P, P, P, I, I, I, L, I, S],
 }

@@ -1,0 +1,169 @@
+"""Asyncio front-end over the synchronous ``LLMEngine``.
+
+The engine step loop runs on one background thread (the GPU is driven from a
+single host thread; TP workers are separate processes fed by the executor).
+Request add / abort calls from the HTTP event loop are queued and applied at
+the top of each iteration, and every ``RequestOutput`` is handed back to the
+request's asyncio queue with ``call_soon_threadsafe``.
+
+Failure handling:
+  * ``healthy`` is False until warmup finished and after the loop dies, so
+    ``/health`` turns 503/500 and the kubelet restarts the pod (the reference's
+    readiness probe, core/helm-charts/vllm/values.yaml:135-141);
+  * a step-time watchdog trips when one iteration exceeds
+    ``VLLM_ENGINE_ITERATION_TIMEOUT_S`` (core/helm-charts/vllm/xeon-values.yaml:66);
+  * ``EIA_FAULT_INJECT`` (test-only) = ``delay_step:<sec>`` | ``crash_after:<steps>``.
+"""
+
+from __future__ import annotations
+
+import asyncio
+import logging
+import os
+import queue
+import threading
+import time
+from typing import AsyncIterator, Dict, Optional
+
+from .llm_engine import LLMEngine, RequestOutput
+from .sampling_params import SamplingParams
+
+logger = logging.getLogger(__name__)
+
+
+class EngineDeadError(RuntimeError):
+    pass
+
+
+class AsyncLLMEngine:
+    def __init__(self, engine: LLMEngine, metrics=None, log_requests: bool = True):
+        self.engine = engine
+        self.metrics = metrics
+        self.log_requests = log_requests
+        self._cmds: "queue.Queue" = queue.Queue()
+        self._streams: Dict[str, asyncio.Queue] = {}
+        self._loops: Dict[str, asyncio.AbstractEventLoop] = {}
+        self._wake = threading.Event()
+        self._stop = False
+        self.dead: Optional[BaseException] = None
+        self.ready = False
+        self.last_step_start: Optional[float] = None
+        self.timeout_s = float(os.environ.get("VLLM_ENGINE_ITERATION_TIMEOUT_S",
+                                              engine.cfg.engine_iteration_timeout_s))
+        self._fault = os.environ.get("EIA_FAULT_INJECT", "")
+        self._thread = threading.Thread(target=self._run, name="eia-engine", daemon=True)
+        self._thread.start()
+        self.ready = True
+        if metrics is not None:
+            metrics.set_healthy(True)
+
+    # ------------------------------------------------------------------ state
+    @property
+    def healthy(self) -> bool:
+        if self.dead is not None or not self.ready:
+            return False
+        t = self.last_step_start
+        return t is None or (time.time() - t) < self.timeout_s
+
+    def check_health(self) -> None:
+        if self.dead is not None:
+            raise EngineDeadError(f"engine loop died: {self.dead!r}")
+        if not self.healthy:
+            raise EngineDeadError("engine step exceeded VLLM_ENGINE_ITERATION_TIMEOUT_S")
+
+    # ------------------------------------------------------------------ API
+    async def generate(self, request_id: str, prompt: Optional[str], params: SamplingParams,
+                       prompt_token_ids=None, priority: int = 0) -> AsyncIterator[RequestOutput]:
+        self.check_health()
+        q: asyncio.Queue = asyncio.Queue()
+        loop = asyncio.get_running_loop()
+        self._streams[request_id] = q
+        self._loops[request_id] = loop
+        self._cmds.put(("add", request_id, prompt, params, prompt_token_ids, time.time(), priority))
+        self._wake.set()
+        try:
+            while True:
+                item = await q.get()
+                if isinstance(item, BaseException):
+                    raise item
+                yield item
+                if item.finished:
+                    return
+        except (asyncio.CancelledError, GeneratorExit):
+            self.abort(request_id)   # client disconnected
+            raise
+        finally:
+            self._streams.pop(request_id, None)
+            self._loops.pop(request_id, None)
+
+    def abort(self, request_id: str) -> None:
+        self._cmds.put(("abort", request_id))
+        self._wake.set()
+
+    def shutdown(self) -> None:
+        self._stop = True
+        self._wake.set()
+        self._thread.join(timeout=30)
+        self.engine.shutdown()
+
+    # ------------------------------------------------------------------ loop
+    def _deliver(self, rid: str, item) -> None:
+        q, loop = self._streams.get(rid), self._loops.get(rid)
+        if q is not None and loop is not None:
+            loop.call_soon_threadsafe(q.put_nowait, item)
+
+    def _drain_cmds(self) -> None:
+        while True:
+            try:
+                cmd = self._cmds.get_nowait()
+            except queue.Empty:
+                return
+            if cmd[0] == "add":
+                _, rid, prompt, params, ids, arrival, prio = cmd
+                try:
+                    self.engine.add_request(rid, prompt, params, ids, arrival_time=arrival,
+                                            priority=prio)
+                    if self.log_requests:
+                        logger.info("request %s added", rid)
+                except Exception as e:   # noqa: BLE001 - validation errors go to the client
+                    self._deliver(rid, e)
+            else:
+                self.engine.abort_request(cmd[1])
+
+    def _run(self) -> None:
+        steps = 0
+        crash_after = delay = None
+        if self._fault.startswith("crash_after:"):
+            crash_after = int(self._fault.split(":")[1])
+        elif self._fault.startswith("delay_step:"):
+            delay = float(self._fault.split(":")[1])
+        try:
+            while not self._stop:
+                self._drain_cmds()
+                if not self.engine.has_unfinished_requests():
+                    self._wake.wait(0.05)
+                    self._wake.clear()
+                    continue
+                t0 = time.time()
+                self.last_step_start = t0
+                if delay:
+                    time.sleep(delay)
+                outs = self.engine.step()
+                self.last_step_start = None
+                steps += 1
+                if crash_after is not None and steps >= crash_after:
+                    raise RuntimeError("EIA_FAULT_INJECT crash")
+                if self.metrics is not None:
+                    self.metrics.observe_step(self.engine, time.time() - t0)
+                for o in outs:
+                    if o.finished and self.metrics is not None:
+                        self.metrics.observe_finished(o)
+                    self._deliver(o.request_id, o)
+        except BaseException as e:   # noqa: BLE001
+            logger.exception("engine loop died")
+            self.dead = e
+            if self.metrics is not None:
+                self.metrics.set_healthy(False)
+            err = EngineDeadError(f"engine loop died: {e!r}")
+            for rid in list(self._streams):
+                self._deliver(rid, err)

@@ -1,0 +1,178 @@
+"""Guided decoding: ``guided_choice`` / ``guided_regex`` / ``guided_json`` request fields
+(docs/api-spec.yaml:479 onward; vLLM extras the reference exposes through its
+OpenAI surface) and chat ``response_format``.
+
+Each sequence carries a ``GuidedState`` that yields the allowed next-token ids
+(K13: applied as a -inf mask before the sampler kernel, engine/logits_process.py):
+
+* choice -> token trie over the tokenised choices (exact, O(#choices));
+* regex  -> incremental partial-match of ``text + token_text`` with the
+  ``regex`` module (``partial=True``); candidate tokens are pre-filtered by their
+  first character class to keep the per-step scan cheap;
+* json   -> a JSON-schema subset compiled to a regex (objects with typed
+  properties, enums, arrays, nested objects; ``{}`` = any flat JSON object).
+"""
+
+from __future__ import annotations
+
+import json
+from typing import Dict, List, Optional
+
+try:
+    import regex as _re
+except ImportError:  # pragma: no cover - regex ships in the image
+    _re = None
+
+_WS = r"[ \t\n]*"
+_STR = r'"(?:[^"\\\x00-\x1f]|\\["\\/bfnrt]|\\u[0-9a-fA-F]{4})*"'
+_NUM = r"-?(?:0|[1-9][0-9]*)(?:\.[0-9]+)?(?:[eE][+-]?[0-9]+)?"
+_INT = r"-?(?:0|[1-9][0-9]*)"
+_BOOL = r"(?:true|false)"
+_NULL = r"null"
+_SCALAR = f"(?:{_STR}|{_NUM}|{_BOOL}|{_NULL})"
+
+
+def schema_to_regex(schema, depth: int = 0) -> str:
+    """Compile a JSON-schema subset into a regex matching its JSON serialisations."""
+    if schema is None or schema == {} or schema is True:
+        if depth > 2:
+            return _SCALAR
+        val = f"(?:{_SCALAR}|{schema_to_regex({'type': 'array'}, depth + 1)})"
+        pair = f"{_STR}{_WS}:{_WS}{val}"
+        return r"\{" + _WS + f"(?:{pair}(?:{_WS},{_WS}{pair})*)?" + _WS + r"\}"
+    if isinstance(schema, str):
+        schema = json.loads(schema)
+    if "enum" in schema:
+        return "(?:" + "|".join(_re.escape(json.dumps(v)) for v in schema["enum"]) + ")"
+    if "const" in schema:
+        return _re.escape(json.dumps(schema["const"]))
+    for key in ("anyOf", "oneOf"):
+        if key in schema:
+            return "(?:" + "|".join(schema_to_regex(s, depth + 1) for s in schema[key]) + ")"
+    t = schema.get("type")
+    if isinstance(t, list):
+        return "(?:" + "|".join(schema_to_regex({**schema, "type": x}, depth) for x in t) + ")"
+    if t == "string":
+        if "pattern" in schema:
+            return '"' + schema["pattern"].lstrip("^").rstrip("$") + '"'
+        return _STR
+    if t == "number":
+        return _NUM
+    if t == "integer":
+        return _INT
+    if t == "boolean":
+        return _BOOL
+    if t == "null":
+        return _NULL
+    if t == "array":
+        item = schema_to_regex(schema.get("items", {"type": "string"}), depth + 1) \
+            if depth < 4 else _SCALAR
+        return r"\[" + _WS + f"(?:{item}(?:{_WS},{_WS}{item})*)?" + _WS + r"\]"
+    if t == "object" or "properties" in schema:
+        props: Dict = schema.get("properties", {})
+        if not props:
+            return schema_to_regex({}, depth + 1)
+        required = set(schema.get("required", list(props)))
+        parts = []
+        for i, (name, sub) in enumerate(props.items()):
+            kv = _re.escape(json.dumps(name)) + _WS + ":" + _WS + schema_to_regex(sub, depth + 1)
+            sep = "" if i == 0 else f"{_WS},{_WS}"
+            parts.append(f"{sep}{kv}" if name in required else f"(?:{sep}{kv})?")
+        return r"\{" + _WS + "".join(parts) + _WS + r"\}"
+    return _SCALAR
+
+
+class GuidedState:
+    def allowed_tokens(self) -> Optional[List[int]]:
+        raise NotImplementedError
+
+    def advance(self, token: int) -> None:
+        raise NotImplementedError
+
+    def is_done(self) -> bool:
+        return False
+
+
+class ChoiceState(GuidedState):
+    def __init__(self, choices: List[str], tokenizer, eos_ids: List[int]):
+        self.seqs = [tokenizer.encode(c, add_special_tokens=False) for c in choices]
+        self.pos = 0
+        self.alive = list(range(len(self.seqs)))
+        self.eos = list(eos_ids)
+        self.done = False
+
+    def allowed_tokens(self):
+        nxt = {self.seqs[i][self.pos] for i in self.alive if self.pos < len(self.seqs[i])}
+        if any(self.pos == len(self.seqs[i]) for i in self.alive):
+            nxt.update(self.eos)
+        return sorted(nxt) if nxt else list(self.eos)
+
+    def advance(self, token):
+        self.alive = [i for i in self.alive
+                      if self.pos < len(self.seqs[i]) and self.seqs[i][self.pos] == token]
+        self.pos += 1
+        if any(self.pos == len(self.seqs[i]) for i in self.alive) and \
+                all(self.pos >= len(self.seqs[i]) for i in self.alive):
+            self.done = True
+
+    def is_done(self):
+        return self.done or not self.alive
+
+
+class RegexState(GuidedState):
+    """Token-level constrained decoding by incremental partial regex matching."""
+
+    _vocab_cache: Dict[int, List[str]] = {}
+
+    def __init__(self, pattern: str, tokenizer, vocab_size: int, eos_ids: List[int]):
+        if _re is None:
+            raise RuntimeError("guided_regex needs the `regex` module")
+        self.pat = _re.compile(pattern)
+        self.tok = tokenizer
+        self.eos = list(eos_ids)
+        key = id(tokenizer)
+        if key not in self._vocab_cache:
+            strs = []
+            for i in range(min(vocab_size, len(tokenizer))):
+                try:
+                    strs.append(tokenizer.decode([i], skip_special_tokens=True))
+                except Exception:   # noqa: BLE001
+                    strs.append("")
+            self._vocab_cache[key] = strs
+        self.strs = self._vocab_cache[key]
+        self.text = ""
+        self.done = False
+
+    def allowed_tokens(self):
+        ok = []
+        for i, s in enumerate(self.strs):
+            if not s:
+                continue
+            if self.pat.fullmatch(self.text + s, partial=True) is not None:
+                ok.append(i)
+        if self.pat.fullmatch(self.text) is not None:
+            ok.extend(self.eos)
+        return ok if ok else list(self.eos)
+
+    def advance(self, token):
+        if token in self.eos:
+            self.done = True
+            return
+        self.text += self.strs[token] if token < len(self.strs) else ""
+        m = self.pat.fullmatch(self.text)
+        if m is not None and self.pat.fullmatch(self.text + "￿", partial=True) is None:
+            # complete and cannot be extended: stop
+            self.done = not any(self.pat.fullmatch(self.text + s, partial=True) is not None
+                                for s in self.strs[:512] if s)
+
+    def is_done(self):
+        return self.done
+
+
+def make_guided_state(params, tokenizer, vocab_size: int) -> GuidedState:
+    eos = list(getattr(params, "eos_ids", None) or [getattr(tokenizer, "eos_token_id", 2)])
+    if params.guided_choice:
+        return ChoiceState(list(params.guided_choice), tokenizer, eos)
+    if params.guided_regex:
+        return RegexState(params.guided_regex, tokenizer, vocab_size, eos)
+    return RegexState(schema_to_regex(params.guided_json), tokenizer, vocab_size, eos)

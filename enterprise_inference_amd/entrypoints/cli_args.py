@@ -1,0 +1,167 @@
+"""vLLM-compatible command line + env knobs.
+
+The reference builds the serving container's argv from the Helm chart
+(``--model --served-model-name --port --tensor-parallel-size [--pipeline-parallel-size]``,
+core/helm-charts/vllm/templates/deployment.yaml:66-87) plus each model's
+``extraCmdArgs`` (core/helm-charts/vllm/gaudi-values.yaml:42-550,
+xeon-values.yaml:70-91).  Every flag used there is accepted here; both
+``--max_num_seqs`` and ``--max-num-seqs`` spellings work, unambiguous prefixes
+(``--gpu-memory-util``) resolve through argparse, HPU-only knobs are accepted
+and ignored.  Env vars from ``configMapValues`` map onto the same knobs.
+"""
+
+from __future__ import annotations
+
+import argparse
+import json
+import logging
+import os
+from typing import List, Optional
+
+logger = logging.getLogger(__name__)
+
+# configMapValues that only mean something on Gaudi/HPU or Xeon: accepted, ignored.
+IGNORED_ENV = ("PT_HPU_", "EXPERIMENTAL_WEIGHT_SHARING", "VLLM_DECODE_BLOCK_BUCKET_",
+               "VLLM_PROMPT_BS_BUCKET_STEP", "VLLM_PROMPT_SEQ_BUCKET_STEP",
+               "VLLM_EXPONENTIAL_BUCKETING", "VLLM_GRAPH_PROMPT_RATIO", "VLLM_PROMPT_USE_FUSEDSDPA",
+               "VLLM_CPU_SGL_KERNEL", "VLLM_CPU_NUM_OF_RESERVED_CPU",
+               "OMPI_MCA_btl_vader_single_copy_mechanism", "HABANA_VISIBLE_DEVICES", "HABANA_LOGS")
+
+
+def _truthy(v: Optional[str]) -> bool:
+    return str(v).lower() in ("1", "true", "yes", "on")
+
+
+def normalise_argv(argv: List[str]) -> List[str]:
+    """``--max_num_seqs=8`` -> ``--max-num-seqs=8`` (the reference mixes both spellings)."""
+    out = []
+    for a in argv:
+        if a.startswith("--"):
+            name, eq, val = a.partition("=")
+            out.append(name.replace("_", "-") + eq + val)
+        else:
+            out.append(a)
+    return out
+
+
+def make_parser(description: str = "MI355X OpenAI-compatible LLM server") -> argparse.ArgumentParser:
+    p = argparse.ArgumentParser(description=description, allow_abbrev=True)
+    a = p.add_argument
+    # chart-injected (deployment.yaml:66-87)
+    a("--model", default=os.environ.get("LLM_MODEL_ID", "meta-llama/Llama-3.1-8B-Instruct"))
+    a("--served-model-name", nargs="+", default=None)
+    a("--host", default="0.0.0.0")
+    a("--port", type=int, default=2080)
+    a("--tensor-parallel-size", "-tp", type=int, default=1)
+    a("--pipeline-parallel-size", "-pp", type=int, default=1)
+    # per-model extraCmdArgs
+    a("--block-size", type=int, default=128)
+    a("--dtype", default="bfloat16")
+    a("--max-model-len", type=int, default=None)
+    a("--gpu-memory-utilization", type=float, default=0.90)
+    a("--max-num-seqs", type=int, default=256)
+    a("--max-num-prefill-seqs", type=int, default=None)
+    a("--max-num-batched-tokens", type=int, default=None)
+    a("--num-scheduler-steps", type=int, default=1)
+    a("--use-padding-aware-scheduling", action="store_true")
+    a("--use-v2-block-manager", action="store_true")
+    a("--enable-chunked-prefill", nargs="?", const=True, default=True,
+      type=lambda v: _truthy(v))
+    a("--enable-prefix-caching", nargs="?", const=True, default=True, type=lambda v: _truthy(v))
+    a("--no-enable-prefix-caching", dest="enable_prefix_caching", action="store_false")
+    a("--enforce-eager", action="store_true")
+    a("--distributed-executor-backend", default="mp", choices=["mp", "ray", "uni", "external"])
+    a("--disable-log-requests", action="store_true")
+    a("--disable-log-stats", action="store_true")
+    a("--tool-call-parser", default=None)
+    a("--chat-template", default=None)
+    a("--enable-auto-tool-choice", action="store_true")
+    a("--trust-remote-code", action="store_true")
+    a("--enable-expert-parallel", action="store_true")
+    a("--override-generation-config", type=json.loads, default=None)
+    a("--generation-config", default="auto")
+    a("--tokenizer", default=None)
+    a("--load-format", default="auto", choices=["auto", "safetensors", "pt", "dummy"])
+    a("--download-dir", default=None)
+    a("--seed", type=int, default=0)
+    a("--swap-space", type=float, default=4)
+    a("--api-key", default=os.environ.get("VLLM_API_KEY"))
+    a("--uvicorn-log-level", default="info")
+    a("--disable-custom-all-reduce", action="store_true")
+    a("--max-log-len", type=int, default=None)
+    a("--device", default="auto", choices=["auto", "cuda", "cpu", "rocm"])
+    a("--kv-cache-dtype", default="auto")
+    a("--quantization", "-q", default=None)
+    a("--max-seq-len-to-capture", type=int, default=None)
+    return p
+
+
+def parse_args(argv: Optional[List[str]] = None, parser=None) -> argparse.Namespace:
+    import sys
+
+    parser = parser or make_parser()
+    argv = normalise_argv(list(sys.argv[1:] if argv is None else argv))
+    args, unknown = parser.parse_known_args(argv)
+    if unknown:
+        logger.warning("ignoring unsupported arguments: %s", " ".join(unknown))
+    return args
+
+
+def resolve_model_source(model: str, download_dir: Optional[str] = None):
+    """(model_path or None, config id). Local dirs (e.g. HF_HOME=/data snapshots) load weights."""
+    if os.path.isdir(model) and os.path.exists(os.path.join(model, "config.json")):
+        return model, model
+    for root in filter(None, (download_dir, os.environ.get("HF_HOME"))):
+        snap = os.path.join(root, "hub", "models--" + model.replace("/", "--"), "snapshots")
+        if os.path.isdir(snap):
+            for d in sorted(os.listdir(snap)):
+                p = os.path.join(snap, d)
+                if os.path.exists(os.path.join(p, "config.json")):
+                    return p, p
+    return None, model
+
+
+def engine_config_from_args(args: argparse.Namespace):
+    """Build an EngineConfig from parsed flags + the reference's env knobs."""
+    import torch
+
+    from ..config import (CacheConfig, EngineConfig, ParallelConfig, SchedulerConfig, parse_dtype)
+    from ..models.loader import resolve_model_config
+
+    for k in os.environ:
+        if k.startswith(IGNORED_ENV):
+            logger.debug("ignoring HPU/Xeon-only env %s", k)
+    path, cfg_id = resolve_model_source(args.model, args.download_dir)
+    mcfg = resolve_model_config(cfg_id)
+    dev = args.device
+    if dev in ("auto", "rocm"):
+        dev = "cuda" if torch.cuda.is_available() else "cpu"
+    dtype = parse_dtype(args.dtype) if dev == "cuda" else torch.float32
+    max_len = args.max_model_len or min(mcfg.max_position_embeddings, 32768)
+    mbt = args.max_num_batched_tokens
+    if mbt is None:
+        mbt = int(os.environ.get("VLLM_PROMPT_SEQ_BUCKET_MAX", 0)) or (8192 if dev == "cuda" else 2048)
+    sched = SchedulerConfig(
+        max_num_seqs=args.max_num_seqs, max_num_batched_tokens=max(mbt, args.max_num_seqs),
+        max_num_prefill_seqs=args.max_num_prefill_seqs or 64, max_model_len=max_len,
+        enable_chunked_prefill=bool(args.enable_chunked_prefill),
+        decode_bs_bucket_step=int(os.environ.get("VLLM_DECODE_BS_BUCKET_STEP", 16)),
+        delayed_sampling=_truthy(os.environ.get("VLLM_DELAYED_SAMPLING", "false")))
+    cache = CacheConfig(block_size=args.block_size,
+                        gpu_memory_utilization=args.gpu_memory_utilization,
+                        cpu_kvcache_space_gb=float(os.environ.get("VLLM_CPU_KVCACHE_SPACE", 4)),
+                        enable_prefix_caching=bool(args.enable_prefix_caching))
+    par = ParallelConfig(tensor_parallel_size=args.tensor_parallel_size,
+                         pipeline_parallel_size=args.pipeline_parallel_size,
+                         enable_expert_parallel=args.enable_expert_parallel,
+                         distributed_executor_backend=args.distributed_executor_backend,
+                         disable_custom_all_reduce=args.disable_custom_all_reduce)
+    served = (args.served_model_name or [args.model])[0]
+    enforce_eager = args.enforce_eager or _truthy(os.environ.get("VLLM_SKIP_WARMUP", "false"))
+    return EngineConfig(model=mcfg, cache=cache, scheduler=sched, parallel=par, dtype=dtype,
+                        device=dev, model_path=path if args.load_format != "dummy" else None,
+                        served_model_name=served, tokenizer=args.tokenizer or path, seed=args.seed,
+                        enforce_eager=enforce_eager, load_format=args.load_format,
+                        trust_remote_code=args.trust_remote_code,
+                        engine_iteration_timeout_s=float(
+                            os.environ.get("VLLM_ENGINE_ITERATION_TIMEOUT_S", 120)))

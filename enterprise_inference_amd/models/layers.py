@@ -14,6 +14,7 @@ import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
+from ..ops import gemm
 from ..parallel import comm, state
 
 
@@ -54,7 +55,7 @@ class ColumnParallelLinear(nn.Module):
         param.data.copy_(_shard(loaded, 0, state.tp_rank(), state.tp_size()))
 
     def forward(self, x):
-        y = F.linear(x, self.weight, self.bias)
+        y = gemm.linear(x, self.weight, self.bias)
         if self.gather_output:
             y = comm.all_gather(y, -1)
         return y
@@ -77,6 +78,18 @@ class MergedColumnParallelLinear(ColumnParallelLinear):
         off = sum(self.out_sizes[:shard_id]) // tp
         n = self.out_sizes[shard_id] // tp
         param.data.narrow(0, off, n).copy_(_shard(loaded, 0, r, tp))
+
+    def forward_act_and_mul(self, x, act: str = "silu"):
+        """act(x Wg^T) * (x Wu^T) for a [gate; up] merged projection.
+
+        Decode-sized batches run the fused SwiGLU GEMM (K7: the 2I-wide
+        intermediate never reaches HBM); larger ones hipBLASLt + the K7 kernel.
+        """
+        if act == "silu" and self.bias is None and len(self.out_sizes) == 2 and \
+                x.dim() == 2 and gemm.skinny_ok(x, self.weight, swiglu=True):
+            return gemm.swiglu_gemm(x, self.weight)
+        from ..ops import activation
+        return activation.act_and_mul(gemm.linear(x, self.weight, self.bias), act)
 
 
 class QKVParallelLinear(ColumnParallelLinear):
@@ -147,8 +160,12 @@ class RowParallelLinear(nn.Module):
     def _load(self, param, loaded, shard_id=None):
         param.data.copy_(_shard(loaded, 1, state.tp_rank(), state.tp_size()))
 
-    def forward(self, x):
-        y = F.linear(x, self.weight)
+    def forward(self, x, defer_reduce: bool = False):
+        """With ``defer_reduce`` (TP=1 decode) the result may be a ``gemm.SplitK``
+        whose split-K reduction (+bias) is fused into the consumer's add+RMSNorm."""
+        if defer_reduce and (state.tp_size() == 1 or not self.reduce_results):
+            return gemm.linear(x, self.weight, self.bias, defer_reduce=True)
+        y = gemm.linear(x, self.weight)
         if self.reduce_results:
             y = comm.all_reduce(y)
         if self.bias is not None:
@@ -166,7 +183,7 @@ class ReplicatedLinear(nn.Module):
             self.bias.weight_loader = default_loader
 
     def forward(self, x):
-        return F.linear(x, self.weight, self.bias)
+        return gemm.linear(x, self.weight, self.bias)
 
 
 class VocabParallelEmbedding(nn.Module):
@@ -216,7 +233,7 @@ class ParallelLMHead(nn.Module):
             self.weight.weight_loader = VocabParallelEmbedding._load.__get__(self)
 
     def forward(self, h: torch.Tensor) -> torch.Tensor:
-        logits = F.linear(h, self.weight)
+        logits = gemm.linear(h, self.weight)
         if state.tp_size() > 1:
             logits = comm.all_gather(logits, -1)
         return logits[..., :self.vocab]
@@ -231,6 +248,10 @@ class RMSNorm(nn.Module):
 
     def forward(self, x, residual=None):
         from ..ops import norm
+        if isinstance(x, gemm.SplitK):
+            if residual is not None:
+                return gemm.splitk_add_rmsnorm(x, residual, self.weight, self.eps)
+            x = x.materialize()
         if residual is None:
             return norm.rms_norm(x, self.weight, self.eps)
         return norm.fused_add_rms_norm(x, residual, self.weight, self.eps)
@@ -257,11 +278,14 @@ def init_random_(module: nn.Module, seed: int = 0, std: float = 0.02) -> None:
     Norm weights -> 1, biases -> 0, matrices ~ N(0, std). Generated on the
     parameter's device (fast for 70B on GPU), seeded per-parameter.
     """
+    import re
+
+    norm_w = re.compile(r"(norm|ln\d*|ln_\w+|layer_norm|layernorm)\.weight$", re.IGNORECASE)
     for i, (name, p) in enumerate(module.named_parameters()):
         g = torch.Generator(device=p.device)
         g.manual_seed(seed * 1000003 + i)
         if p.dim() == 1:
-            if "norm" in name or name.endswith("ln.weight") or "layernorm" in name.lower():
+            if norm_w.search(name):
                 p.data.fill_(1.0)
             else:
                 p.data.zero_()

@@ -18,7 +18,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from ..config import ModelConfig
-from ..ops import activation
+from ..ops import activation, gemm  # noqa: F401
 from ..ops.attention import AttentionMetadata, attention
 from ..ops.rotary import RotaryCache, rope_qkv_cache
 from ..parallel import state
@@ -58,7 +58,7 @@ class LlamaAttention(nn.Module):
 
     def forward(self, h: torch.Tensor, md: AttentionMetadata, kv: KVCache) -> torch.Tensor:
         T = h.shape[0]
-        qkv = F.linear(h, self.qkv_proj.weight)
+        qkv = gemm.linear(h, self.qkv_proj.weight)
         q = rope_qkv_cache(qkv, md.positions, self.rotary, md.slot_mapping, kv[0], kv[1],
                            self.num_heads, self.num_kv_heads, self.head_dim,
                            bias=self.qkv_proj.bias,
@@ -66,7 +66,7 @@ class LlamaAttention(nn.Module):
                            k_norm_w=None if self.k_norm is None else self.k_norm.weight,
                            norm_eps=self.cfg.rms_norm_eps)
         o = attention(q, kv[0], kv[1], md, self.scale, self.sliding_window, self.chunk_size)
-        return self.o_proj(o.view(T, self.num_heads * self.head_dim))
+        return self.o_proj(o.view(T, self.num_heads * self.head_dim), defer_reduce=True)
 
 
 class LlamaMLP(nn.Module):
@@ -77,8 +77,8 @@ class LlamaMLP(nn.Module):
         self.down_proj = RowParallelLinear(inter, hidden, dtype=dtype, device=device)
         self.act = "silu" if act in ("silu", "swish") else act
 
-    def forward(self, x: torch.Tensor) -> torch.Tensor:
-        return self.down_proj(activation.act_and_mul(self.gate_up_proj(x), self.act))
+    def forward(self, x: torch.Tensor):
+        return self.down_proj(self.gate_up_proj.forward_act_and_mul(x, self.act), defer_reduce=True)
 
 
 class LlamaDecoderLayer(nn.Module):

@@ -1,0 +1,184 @@
+"""Decode-shaped GEMMs (K6) and the SwiGLU GEMM epilogue (K7) -> csrc/kernels/gemm_skinny.hip.
+
+``linear`` routes a [M, K] x [N, K]^T product:
+  * M <= 128 on the GPU -> the weight-streaming skinny kernel (split over K across
+    workgroups when N alone cannot cover the 256 CUs; the fp32 partial slabs are
+    reduced by ``splitk_reduce`` or fused into the consumer, see ``SplitK``);
+  * otherwise (prefill) -> ``F.linear`` (hipBLASLt), which is MFMA-bound there.
+"""
+
+from __future__ import annotations
+
+import functools
+import json
+import os
+from typing import Optional
+
+import torch
+import torch.nn.functional as F
+
+from ._dispatch import check, lib, ptr, stream, use_hip
+
+MAX_M = 128
+KC = 256
+TARGET_WGS = int(os.environ.get("EIA_SKINNY_TARGET_WGS", "512"))
+DISABLE = os.environ.get("EIA_DISABLE_SKINNY_GEMM", "0") == "1"
+TUNING_FILE = os.environ.get("EIA_GEMM_TUNING",
+                             os.path.join(os.path.dirname(os.path.abspath(__file__)),
+                                          "gemm_tuning.json"))
+
+MODE_BF16, MODE_SPLIT, MODE_SWIGLU = 0, 1, 2
+# kernel configs: bit0 -> 2 W tiles (32 rows) per wave, bit1 -> 4 waves per workgroup
+CFGS = (0, 1, 2, 3)
+
+
+def cfg_rows(cfg: int) -> int:
+    return (2 if cfg & 1 else 1) * (4 if cfg & 2 else 2) * 16
+
+
+def m_bucket(M: int) -> int:
+    return (M + 15) // 16
+
+
+def _load_tuning() -> dict:
+    """(m_tiles, N, K, swiglu) -> (cfg, sk), measured by scripts/bench_gemm.py --tune."""
+    try:
+        with open(TUNING_FILE) as f:
+            raw = json.load(f)
+    except (OSError, ValueError):
+        return {}
+    out = {}
+    for k, v in raw.get("entries", {}).items():
+        mt, n, kk, sw = (int(x) for x in k.split(","))
+        out[(mt, n, kk, bool(sw))] = (int(v[0]), int(v[1]))
+    return out
+
+
+_TUNED = _load_tuning()
+
+
+def valid(N: int, K: int, swiglu: bool, cfg: int, sk: int) -> bool:
+    if K % (sk * KC):
+        return False
+    if swiglu:
+        return sk == 1 and (cfg & 1) == 1 and (N // 2) % ((4 if cfg & 2 else 2) * 16) == 0
+    return N % cfg_rows(cfg) == 0
+
+
+def heuristic_splitk(N: int, K: int, cfg: int, swiglu: bool = False) -> int:
+    """Smallest K split whose grid covers the chip (K/split a multiple of KC)."""
+    if swiglu:
+        return 1
+    tiles = N // cfg_rows(cfg)
+    nk = K // KC
+    best = 1
+    for sk in range(1, nk + 1):
+        if nk % sk:
+            continue
+        best = sk
+        if tiles * sk >= TARGET_WGS:
+            break
+    return best
+
+
+@functools.lru_cache(maxsize=8192)
+def choose(M: int, N: int, K: int, swiglu: bool = False):
+    """(cfg, sk) for this shape: tuned table first, else the heuristic."""
+    key = (m_bucket(M), N, K, swiglu)
+    if key in _TUNED and (_TUNED[key][0] < 0 or valid(N, K, swiglu, *_TUNED[key])):
+        return _TUNED[key]
+    cfg = 3 if m_bucket(M) >= 3 else 1
+    if not valid(N, K, swiglu, cfg, 1):
+        cfg = 1
+    return cfg, heuristic_splitk(N, K, cfg, swiglu)
+
+
+def choose_splitk(N: int, K: int, swiglu: bool = False, M: int = 64) -> int:
+    return choose(M, N, K, swiglu)[1]
+
+
+def skinny_ok(x: torch.Tensor, w: torch.Tensor, swiglu: bool = False) -> bool:
+    if DISABLE or not use_hip(x, w) or x.dtype != torch.bfloat16 or w.dtype != torch.bfloat16:
+        return False
+    M, K = x.shape
+    N = w.shape[0]
+    if M < 1 or M > MAX_M or K % KC or w.shape[1] != K:
+        return False
+    if x.stride(1) != 1 or w.stride(1) != 1 or x.stride(0) % 8 or w.stride(0) % 8:
+        return False
+    cfg, sk = choose(M, N, K, swiglu)
+    return cfg >= 0 and valid(N, K, swiglu, cfg, sk)
+
+
+class SplitK:
+    """fp32 partial sums [sk, M, N] of a GEMM whose reduction is left to the consumer."""
+
+    __slots__ = ("part", "sk", "M", "N", "bias")
+
+    def __init__(self, part: torch.Tensor, sk: int, M: int, N: int,
+                 bias: Optional[torch.Tensor] = None):
+        self.part, self.sk, self.M, self.N, self.bias = part, sk, M, N, bias
+
+    @property
+    def shape(self):
+        return (self.M, self.N)
+
+    def materialize(self, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+        o = out if out is not None else torch.empty(self.M, self.N, dtype=torch.bfloat16,
+                                                    device=self.part.device)
+        check(lib().eia_splitk_reduce(ptr(self.part), self.sk, self.M, self.N, ptr(self.bias),
+                                      ptr(o), o.stride(0), stream(o)), "splitk_reduce")
+        return o
+
+
+def skinny(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = None,
+           defer_reduce: bool = False, cfg: Optional[int] = None, sk: Optional[int] = None):
+    """x [M, K] @ w[N, K]^T on the skinny kernel. Returns a tensor or a SplitK."""
+    M, K = x.shape
+    N = w.shape[0]
+    if cfg is None:
+        cfg, sk = choose(M, N, K, False)
+    if sk == 1:
+        out = torch.empty(M, N, dtype=torch.bfloat16, device=x.device)
+        check(lib().eia_gemm_skinny(ptr(x), x.stride(0), ptr(w), w.stride(0), ptr(bias), ptr(out),
+                                    out.stride(0), M, N, K, 1, MODE_BF16, cfg, stream(x)),
+              "gemm_skinny")
+        return out
+    part = torch.empty(sk, M, N, dtype=torch.float32, device=x.device)
+    check(lib().eia_gemm_skinny(ptr(x), x.stride(0), ptr(w), w.stride(0), None, ptr(part), N, M, N,
+                                K, sk, MODE_SPLIT, cfg, stream(x)), "gemm_skinny")
+    s = SplitK(part, sk, M, N, bias)
+    return s if defer_reduce else s.materialize()
+
+
+def swiglu_gemm(x: torch.Tensor, w_gate_up: torch.Tensor, cfg: Optional[int] = None) -> torch.Tensor:
+    """silu(x Wg^T) * (x Wu^T) with W = [gate; up] stacked on dim 0 (K7)."""
+    M, K = x.shape
+    N = w_gate_up.shape[0]
+    if cfg is None:
+        cfg = choose(M, N, K, True)[0]
+    out = torch.empty(M, N // 2, dtype=torch.bfloat16, device=x.device)
+    check(lib().eia_gemm_skinny(ptr(x), x.stride(0), ptr(w_gate_up), w_gate_up.stride(0), None,
+                                ptr(out), out.stride(0), M, N, K, 1, MODE_SWIGLU, cfg, stream(x)),
+          "gemm_skinny_swiglu")
+    return out
+
+
+def linear(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = None,
+           defer_reduce: bool = False):
+    if x.dim() == 2 and skinny_ok(x, w):
+        return skinny(x, w, bias, defer_reduce)
+    return F.linear(x, w, bias)
+
+
+def splitk_add_rmsnorm(s: SplitK, residual: torch.Tensor, weight: torch.Tensor, eps: float):
+    """residual += reduce(s) (+bias); returns (rmsnorm(residual) * weight, residual)."""
+    if s.bias is not None:
+        h = s.materialize()
+        from .norm import fused_add_rms_norm
+        return fused_add_rms_norm(h, residual, weight, eps)
+    out = torch.empty(s.M, s.N, dtype=torch.bfloat16, device=residual.device)
+    check(lib().eia_splitk_add_rmsnorm(ptr(s.part), s.sk, s.M, s.N, ptr(residual), ptr(weight),
+                                       float(eps), ptr(out), out.stride(0), stream(out)),
+          "splitk_add_rmsnorm")
+    return out, residual

@@ -1,0 +1,133 @@
+#!/usr/bin/env python3
+"""Decode-GEMM microbenchmark + autotuner: skinny HIP kernel vs F.linear (hipBLASLt).
+
+Every variant is captured in a HIP graph of --iters calls (no host launch cost in
+the number) with weights rotating through a pool larger than the 256 MiB Infinity
+Cache, so each call streams its weights from HBM.  Variants are timed in
+interleaved rounds in one process (guide §5.4 rule 24).
+
+  --tune  sweeps (cfg, split-K) per (M-tile bucket, N, K) and writes the winners to
+          enterprise_inference_amd/ops/gemm_tuning.json (read by ops/gemm.py).
+"""
+import argparse
+import json
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import torch  # noqa: E402
+import torch.nn.functional as F  # noqa: E402
+
+from enterprise_inference_amd.ops import gemm  # noqa: E402
+
+SHAPES = {  # name: (N, K, swiglu)
+    "qkv_8b": (6144, 4096, False), "o_8b": (4096, 4096, False),
+    "gate_up_8b": (28672, 4096, True), "down_8b": (4096, 14336, False),
+    "lm_head_8b": (128256, 4096, False),
+    "qkv_70b_tp8": (1280, 8192, False), "o_70b_tp8": (8192, 1024, False),
+    "gate_up_70b_tp8": (7168, 8192, True), "down_70b_tp8": (8192, 3584, False),
+    "lm_head_70b_tp8": (16032, 8192, False),
+}
+
+
+def graph_time(fn, iters, rounds=3):
+    torch.cuda.synchronize()
+    fn(0)
+    g = torch.cuda.CUDAGraph()
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        fn(0)
+        with torch.cuda.graph(g, stream=s):
+            for i in range(iters):
+                fn(i)
+    torch.cuda.current_stream().wait_stream(s)
+    torch.cuda.synchronize()
+    best = 1e30
+    for _ in range(rounds):
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record()
+        g.replay()
+        b.record()
+        torch.cuda.synchronize()
+        best = min(best, a.elapsed_time(b) / iters * 1e3)
+    del g
+    return best   # us per call
+
+
+def candidates(M, N, K, swiglu):
+    out = []
+    nk = K // gemm.KC
+    for cfg in gemm.CFGS:
+        for sk in range(1, nk + 1):
+            if nk % sk or not gemm.valid(N, K, swiglu, cfg, sk):
+                continue
+            rows = gemm.cfg_rows(cfg) if not swiglu else gemm.cfg_rows(cfg)
+            grid = (N // rows) * sk
+            if sk > 1 and grid > 4096:
+                continue
+            if grid < 64 and sk < nk:
+                continue
+            out.append((cfg, sk))
+    return out
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--m", type=int, nargs="+", default=[1, 16, 32, 48, 64, 80, 96, 112, 128])
+    ap.add_argument("--shapes", nargs="+", default=list(SHAPES))
+    ap.add_argument("--iters", type=int, default=20)
+    ap.add_argument("--tune", action="store_true")
+    ap.add_argument("--out", default=None, help="also write the tuning table here")
+    a = ap.parse_args()
+    tuned = {}
+    if a.tune and os.path.exists(gemm.TUNING_FILE):
+        tuned = json.load(open(gemm.TUNING_FILE)).get("entries", {})
+    for name in a.shapes:
+        N, K, swiglu = SHAPES[name]
+        wbytes = N * K * 2
+        pool = max(2, int(600e6 // wbytes) + 1)
+        ws = [(torch.randn(N, K, device="cuda") * 0.02).to(torch.bfloat16) for _ in range(pool)]
+        for M in a.m:
+            x = torch.randn(M, K, device="cuda", dtype=torch.bfloat16)
+            if swiglu:
+                I = N // 2
+                base = lambda i: (lambda y: F.silu(y[:, :I]) * y[:, I:])(F.linear(x, ws[i % pool]))
+            else:
+                base = lambda i: F.linear(x, ws[i % pool])
+            tb = graph_time(base, a.iters)
+            cands = candidates(M, N, K, swiglu) if a.tune else [gemm.choose(M, N, K, swiglu)]
+            results = []
+            for cfg, sk in cands:
+                if swiglu:
+                    f = lambda i, cfg=cfg: gemm.swiglu_gemm(x, ws[i % pool], cfg=cfg)
+                else:
+                    f = lambda i, cfg=cfg, sk=sk: gemm.skinny(x, ws[i % pool], cfg=cfg, sk=sk)
+                results.append((graph_time(f, a.iters), cfg, sk))
+            results.sort()
+            to, cfg, sk = results[0]
+            r = {"shape": name, "M": M, "N": N, "K": K, "cfg": cfg, "sk": sk,
+                 "ours_us": round(to, 2), "hipblaslt_us": round(tb, 2),
+                 "ours_TBps": round(wbytes / to / 1e6, 2), "hipblaslt_TBps": round(wbytes / tb / 1e6, 2),
+                 "speedup": round(tb / to, 2),
+                 "runner_up": [(round(t, 1), c, s) for t, c, s in results[1:4]]}
+            print(json.dumps(r), flush=True)
+            if a.tune:
+                key = f"{gemm.m_bucket(M)},{N},{K},{int(swiglu)}"
+                # cfg -1 = "use hipBLASLt" (the skinny kernel lost on this shape)
+                tuned[key] = [cfg, sk] if to < tb * 1.02 else [-1, 1]
+        del ws
+        torch.cuda.empty_cache()
+    if a.tune:
+        with open(gemm.TUNING_FILE, "w") as f:
+            json.dump({"device": torch.cuda.get_device_name(0), "entries": tuned}, f, indent=0,
+                      sort_keys=True)
+        print("wrote", gemm.TUNING_FILE)
+        if a.out:
+            with open(a.out, "w") as f:
+                json.dump({"device": torch.cuda.get_device_name(0), "entries": tuned}, f, indent=0,
+                          sort_keys=True)
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,79 @@
+"""Skinny decode GEMM (K6) + SwiGLU epilogue (K7) + split-K reductions vs fp32 PyTorch."""
+
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+
+DEV = "cuda"
+BF = torch.bfloat16
+
+
+def _ref(x, w, b=None):
+    y = x.float() @ w.float().t()
+    return y if b is None else y + b.float()
+
+
+def _check(out, ref, msg):
+    err = (out.float() - ref).abs()
+    tol = 2e-2 + 2e-2 * ref.abs()
+    assert not torch.isnan(out.float()).any(), msg
+    assert (err <= tol).all(), f"{msg}: max err {err.max().item():.4g}"
+
+
+@pytest.mark.parametrize("M", [1, 5, 16, 33, 65, 100, 128])
+@pytest.mark.parametrize("N,K", [(4096, 4096), (6144, 4096), (4096, 14336), (1280, 8192), (384, 768)])
+def test_skinny_linear(M, N, K):
+    from enterprise_inference_amd.ops import gemm
+    torch.manual_seed(M * 7 + N)
+    x = torch.randn(M, K, device=DEV, dtype=BF)
+    w = (torch.randn(N, K, device=DEV) * K ** -0.5).to(BF)
+    b = torch.randn(N, device=DEV, dtype=BF)
+    for cfg in gemm.CFGS:
+        for sk in sorted({1, gemm.heuristic_splitk(N, K, cfg)}):
+            if not gemm.valid(N, K, False, cfg, sk):
+                continue
+            out = gemm.skinny(x, w, b, cfg=cfg, sk=sk)
+            _check(out, _ref(x, w, b), f"M={M} N={N} K={K} cfg={cfg} sk={sk}")
+
+
+@pytest.mark.parametrize("M", [1, 17, 65, 128])
+def test_skinny_strided_input(M):
+    from enterprise_inference_amd.ops import gemm
+    big = torch.randn(M, 3 * 1024, device=DEV, dtype=BF)
+    x = big[:, 1024:2048]                       # row stride 3072
+    w = (torch.randn(2048, 1024, device=DEV) * 0.03).to(BF)
+    _check(gemm.linear(x, w), _ref(x, w), "strided")
+
+
+@pytest.mark.parametrize("M", [1, 9, 65, 128])
+@pytest.mark.parametrize("I,K", [(14336, 4096), (3584, 8192), (256, 512)])
+def test_swiglu_gemm(M, I, K):
+    from enterprise_inference_amd.ops import gemm
+    x = torch.randn(M, K, device=DEV, dtype=BF)
+    w = (torch.randn(2 * I, K, device=DEV) * K ** -0.5).to(BF)
+    y = _ref(x, w)
+    ref = F.silu(y[:, :I]) * y[:, I:]
+    for cfg in (1, 3):
+        if gemm.valid(2 * I, K, True, cfg, 1):
+            _check(gemm.swiglu_gemm(x, w, cfg=cfg), ref, f"swiglu M={M} I={I} cfg={cfg}")
+
+
+@pytest.mark.parametrize("M,H", [(1, 4096), (65, 4096), (128, 8192)])
+def test_splitk_add_rmsnorm(M, H):
+    from enterprise_inference_amd.ops import gemm
+    from enterprise_inference_amd.ops import reference as ref
+    K = 4096
+    x = torch.randn(M, K, device=DEV, dtype=BF)
+    w = (torch.randn(H, K, device=DEV) * K ** -0.5).to(BF)
+    res = torch.randn(M, H, device=DEV, dtype=BF)
+    nw = (torch.rand(H, device=DEV) + 0.5).to(BF)
+    s = gemm.skinny(x, w, defer_reduce=True, cfg=1, sk=4)
+    assert isinstance(s, gemm.SplitK) and s.sk > 1
+    y = _ref(x, w)
+    r_ref = (y + res.float()).to(BF)
+    o_ref = ref.rms_norm(r_ref.float(), nw.float(), 1e-5)
+    out, r2 = gemm.splitk_add_rmsnorm(s, res, nw, 1e-5)
+    _check(r2, r_ref.float(), "residual")
+    _check(out, o_ref.float(), "normed")
