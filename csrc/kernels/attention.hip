@@ -130,7 +130,8 @@ paged_decode_kernel(const bf16_t* __restrict__ q, long q_stride,
                     const int* __restrict__ seq_lens,
                     bf16_t* __restrict__ out, long out_stride,
                     float* __restrict__ part_o, float* __restrict__ part_ml,
-                    float scale_log2, int Hq, int Hkv, int bs, int P, int NQG) {
+                    float scale_log2, int Hq, int Hkv, int bs, int P, int NQG,
+                    int sliding_window, int chunk_size) {
   __shared__ float sm[4][16];
   __shared__ float sl[4][16];
   __shared__ float so[4][D][17];
@@ -161,11 +162,16 @@ paged_decode_kernel(const bf16_t* __restrict__ q, long q_stride,
   }
   WaveAcc<D> acc;
   wave_acc_init(acc);
-  const int U = (L + 31) / 32;
-  const int ub = (int)(((long)p * U) / P), ue = (int)(((long)(p + 1) * U) / P);
+  // sliding window (Mistral) / chunked local attention (Llama-4) bound the visible keys
+  int kv_lo = 0;
+  if (L > 0 && sliding_window > 0) kv_lo = max(kv_lo, L - sliding_window);
+  if (L > 0 && chunk_size > 0) kv_lo = max(kv_lo, ((L - 1) / chunk_size) * chunk_size);
+  const int U0 = kv_lo / 32;
+  const int U = (L + 31) / 32 - U0;
+  const int ub = U0 + (int)(((long)p * U) / P), ue = U0 + (int)(((long)(p + 1) * U) / P);
   const int* bt = block_tables + (long)b * bt_stride;
   for (int u = ub + w; u < ue; u += 4)
-    attn_unit<D>(acc, qf, kc, vc, bt, 32 * u, L, kvh, Hkv, bs, scale_log2, 0x7fffffff, 0);
+    attn_unit<D>(acc, qf, kc, vc, bt, 32 * u, L, kvh, Hkv, bs, scale_log2, 0x7fffffff, kv_lo);
 
   float lt = acc.l;
   lt += __shfl_xor(lt, 16, 64);
@@ -299,7 +305,7 @@ EIA_API int eia_paged_decode(const void* q, long q_stride, const void* k_cache, 
                              const int* block_tables, int bt_stride, const int* seq_lens,
                              void* out, long out_stride, float* part_o, float* part_ml,
                              float scale, int B, int Hq, int Hkv, int D, int bs, int P,
-                             hipStream_t st) {
+                             int sliding_window, int chunk_size, hipStream_t st) {
   if (B < 0 || Hkv <= 0 || Hq % Hkv != 0 || bs % 16 != 0 || P < 1) return EIA_BAD_SHAPE;
   if (P > 1 && (part_o == nullptr || part_ml == nullptr)) return EIA_BAD_SHAPE;
   if (B == 0) return EIA_OK;
@@ -310,7 +316,8 @@ EIA_API int eia_paged_decode(const void* q, long q_stride, const void* k_cache, 
 #define DEC(DD)                                                                             \
   hipLaunchKernelGGL((paged_decode_kernel<DD>), grid, block, 0, st, (const bf16_t*)q, q_stride, \
                      (const bf16_t*)k_cache, (const bf16_t*)v_cache, block_tables, bt_stride, \
-                     seq_lens, (bf16_t*)out, out_stride, part_o, part_ml, sl2, Hq, Hkv, bs, P, NQG); \
+                     seq_lens, (bf16_t*)out, out_stride, part_o, part_ml, sl2, Hq, Hkv, bs, P, NQG, \
+                     sliding_window, chunk_size);                                            \
   if (P > 1)                                                                                \
     hipLaunchKernelGGL((paged_decode_reduce_kernel<DD>), dim3(B, Hq), dim3(DD < 256 ? DD : 256), 0, st, \
                        part_o, part_ml, (bf16_t*)out, out_stride, Hq, P);

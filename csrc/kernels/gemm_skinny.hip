@@ -39,8 +39,10 @@ enum Mode : int { MODE_BF16 = 0, MODE_F32_SPLIT = 1, MODE_SWIGLU = 2 };
 
 EIA_DEV float silu(float x) { return x / (1.f + __expf(-x)); }
 
-// Once-read weight stream: non-temporal loads (guide: MI355X_MICROARCH "nt-weights").
-EIA_DEV bf16x8 ld_nt(const bf16_t* p) {
+// Weight-stream load.  Non-temporal loads (EIA_GEMM_NT) measured 1.7x SLOWER on this box for
+// back-to-back decode replays (guide: MI355X_MICROARCH "nt-weights" -- nt gives up what a
+// replay gains from default-policy loads), so plain loads are the default.
+EIA_DEV bf16x8 ld_w(const bf16_t* p) {
 #ifdef EIA_GEMM_NT
   return __builtin_bit_cast(bf16x8, __builtin_nontemporal_load(reinterpret_cast<const s16x8*>(p)));
 #else
@@ -48,12 +50,17 @@ EIA_DEV bf16x8 ld_nt(const bf16_t* p) {
 #endif
 }
 
-// MT: 16-column tiles of X (M <= 16*MT); NT: 16-row W tiles per wave; WAVES per workgroup.
-template <int MT, int NT, int WAVES>
+// MT: 16-column tiles of X (M <= 16*MT per pass); NT: 16-row W tiles per wave; WAVES per
+// workgroup.  GROUPED (MoE, K9): blockIdx.z = expert e, W += e * w_estride, the expert's
+// rows are [offs[e], offs[e+1]) of the expert-sorted token list, X rows are gathered
+// through row_idx (nullptr = identity) and outputs land in sorted order; experts with
+// more than 16*MT rows loop over row chunks (weights re-streamed per chunk).
+template <int MT, int NT, int WAVES, bool GROUPED>
 __global__ void __launch_bounds__(WAVES * 64)
 gemm_skinny_kernel(const bf16_t* __restrict__ X, long ldx, const bf16_t* __restrict__ W, long ldw,
                    const bf16_t* __restrict__ bias, void* __restrict__ out, long ldo, int M, int N,
-                   int krange, int mode, int inter) {
+                   int krange, int mode, int inter, const int* __restrict__ offs,
+                   const int* __restrict__ row_idx, long w_estride) {
   extern __shared__ __align__(16) bf16_t xs[];   // [2][MT*16][XLD]
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
@@ -61,6 +68,16 @@ gemm_skinny_kernel(const bf16_t* __restrict__ X, long ldx, const bf16_t* __restr
   const int k0 = blockIdx.y * krange;
   const int nchunks = krange / KC;
   const int last = nchunks - 1;
+
+  int mbase = 0, Mtot = M;
+  if constexpr (GROUPED) {
+    const int e = blockIdx.z;
+    mbase = offs[e];
+    Mtot = offs[e + 1] - mbase;
+    if (Mtot <= 0) return;                                // uniform over the workgroup
+    W += (long)e * w_estride;
+    if (bias != nullptr) bias += (long)e * N;
+  }
 
   // rows of W owned by this wave's tiles
   const bf16_t* wp[NT];
@@ -79,130 +96,144 @@ gemm_skinny_kernel(const bf16_t* __restrict__ X, long ldx, const bf16_t* __restr
   constexpr int XPT = XV / (WAVES * 64);                // per thread
   static_assert(XV % (WAVES * 64) == 0, "X chunk split");
 
-  auto load_x = [&](int c, bf16x8 (&xr)[XPT]) {
+  for (int m0 = 0; m0 < Mtot; m0 += MT * 16) {
+    const int Mc = min(MT * 16, Mtot - m0);
+    // X row (in the caller's X) of local row `row` of this pass; padded rows clamp to the last
+    // valid one and are never stored
+    auto xrow_of = [&](int row) -> long {
+      const int lr = mbase + m0 + (row < Mc ? row : Mc - 1);
+      if constexpr (GROUPED) return row_idx != nullptr ? (long)row_idx[lr] : (long)lr;
+      return (long)lr;
+    };
+    long xrows[XPT];
 #pragma unroll
-    for (int j = 0; j < XPT; ++j) {
-      const int v = threadIdx.x + j * WAVES * 64;
-      const int row = v / (KC / 8), col = (v % (KC / 8)) * 8;
-      const int xrow = row < M ? row : M - 1;          // clamp: padded columns are never stored
-      xr[j] = *reinterpret_cast<const bf16x8*>(X + (long)xrow * ldx + k0 + c * KC + col);
-    }
-  };
-  auto store_x = [&](int buf, const bf16x8 (&xr)[XPT]) {
+    for (int j = 0; j < XPT; ++j) xrows[j] = xrow_of((threadIdx.x + j * WAVES * 64) / (KC / 8));
+
+    auto load_x = [&](int c, bf16x8 (&xr)[XPT]) {
 #pragma unroll
-    for (int j = 0; j < XPT; ++j) {
-      const int v = threadIdx.x + j * WAVES * 64;
-      const int row = v / (KC / 8), col = (v % (KC / 8)) * 8;
-      *reinterpret_cast<bf16x8*>(xs + (buf * MT * 16 + row) * XLD + col) = xr[j];
-    }
-  };
-  // W fragments of one chunk: [tile][superstep*4 + s]; lane (r, g) covers
-  // k = 128*superstep + 32g + 8s + j of the chunk
-  auto load_w = [&](int c, bf16x8 (&w)[NT][8]) {
+      for (int j = 0; j < XPT; ++j) {
+        const int v = threadIdx.x + j * WAVES * 64;
+        const int col = (v % (KC / 8)) * 8;
+        xr[j] = *reinterpret_cast<const bf16x8*>(X + xrows[j] * ldx + k0 + c * KC + col);
+      }
+    };
+    auto store_x = [&](int buf, const bf16x8 (&xr)[XPT]) {
+#pragma unroll
+      for (int j = 0; j < XPT; ++j) {
+        const int v = threadIdx.x + j * WAVES * 64;
+        const int row = v / (KC / 8), col = (v % (KC / 8)) * 8;
+        *reinterpret_cast<bf16x8*>(xs + (buf * MT * 16 + row) * XLD + col) = xr[j];
+      }
+    };
+    // W fragments of one chunk: [tile][superstep*4 + s]; lane (r, g) covers
+    // k = 128*superstep + 32g + 8s + j of the chunk
+    auto load_w = [&](int c, bf16x8 (&w)[NT][8]) {
+#pragma unroll
+      for (int t = 0; t < NT; ++t)
+#pragma unroll
+        for (int ss = 0; ss < 2; ++ss)
+#pragma unroll
+          for (int s = 0; s < 4; ++s) w[t][ss * 4 + s] = ld_w(wp[t] + c * KC + 128 * ss + 8 * s);
+    };
+
+    f32x4 acc[NT][MT];
 #pragma unroll
     for (int t = 0; t < NT; ++t)
 #pragma unroll
-      for (int ss = 0; ss < 2; ++ss)
-#pragma unroll
-        for (int s = 0; s < 4; ++s) w[t][ss * 4 + s] = ld_nt(wp[t] + c * KC + 128 * ss + 8 * s);
-  };
+      for (int m = 0; m < MT; ++m) acc[t][m] = (f32x4){0.f, 0.f, 0.f, 0.f};
 
-  f32x4 acc[NT][MT];
+    auto compute = [&](int buf, const bf16x8 (&w)[NT][8]) {
+      const bf16_t* xb = xs + (buf * MT * 16 + r) * XLD + 32 * g;
 #pragma unroll
-  for (int t = 0; t < NT; ++t)
+      for (int st = 0; st < 8; ++st) {
+        bf16x8 xf[MT];
 #pragma unroll
-    for (int m = 0; m < MT; ++m) acc[t][m] = (f32x4){0.f, 0.f, 0.f, 0.f};
+        for (int m = 0; m < MT; ++m)
+          xf[m] = *reinterpret_cast<const bf16x8*>(xb + m * 16 * XLD + 128 * (st >> 2) + 8 * (st & 3));
+#pragma unroll
+        for (int m = 0; m < MT; ++m)
+#pragma unroll
+          for (int t = 0; t < NT; ++t)
+            acc[t][m] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w[t][st], xf[m], acc[t][m], 0, 0, 0);
+      }
+    };
 
-  auto compute = [&](int buf, const bf16x8 (&w)[NT][8]) {
-    const bf16_t* xb = xs + (buf * MT * 16 + r) * XLD + 32 * g;
-#pragma unroll
-    for (int st = 0; st < 8; ++st) {
-      bf16x8 xf[MT];
-#pragma unroll
-      for (int m = 0; m < MT; ++m)
-        xf[m] = *reinterpret_cast<const bf16x8*>(xb + m * 16 * XLD + 128 * (st >> 2) + 8 * (st & 3));
-#pragma unroll
-      for (int m = 0; m < MT; ++m)
-#pragma unroll
-        for (int t = 0; t < NT; ++t)
-          acc[t][m] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w[t][st], xf[m], acc[t][m], 0, 0, 0);
+    // Pipeline: two named W register sets (no copies: guide rule 20); each phase
+    // issues X(c+1) then W(c+1) -- pinned ahead of the MFMAs with sched_barrier,
+    // since hipcc otherwise sinks the X loads behind the compute and waits vmcnt(0)
+    // on them -- so the in-order vmcnt wait for X before its ds_write leaves the
+    // weight prefetch in flight.  Loads are unconditional (chunk index clamped)
+    // and the loop body has no early exit, so the vmcnt accounting stays exact.
+    bf16x8 wa[NT][8], wb[NT][8];
+    {
+      bf16x8 xr[XPT];
+      load_x(0, xr);
+      load_w(0, wa);
+      store_x(0, xr);
     }
-  };
-
-  // Pipeline: two named W register sets (no copies: guide rule 20); each phase
-  // issues X(c+1) then W(c+1) -- pinned ahead of the MFMAs with sched_barrier,
-  // since hipcc otherwise sinks the X loads behind the compute and waits vmcnt(0)
-  // on them -- so the in-order vmcnt wait for X before its ds_write leaves the
-  // weight prefetch in flight.  Loads are unconditional (chunk index clamped)
-  // and the loop body has no early exit, so the vmcnt accounting stays exact.
-  bf16x8 wa[NT][8], wb[NT][8];
-  {
-    bf16x8 xr[XPT];
-    load_x(0, xr);
-    load_w(0, wa);
-    store_x(0, xr);
-  }
-  __syncthreads();
+    __syncthreads();
 #define EIA_PHASE(C, WCUR, WNEXT)                 \
-  {                                               \
-    bf16x8 xr[XPT];                               \
-    load_x(min((C) + 1, last), xr);               \
-    load_w(min((C) + 1, last), WNEXT);            \
-    __builtin_amdgcn_sched_barrier(0);            \
-    compute((C) & 1, WCUR);                       \
-    __builtin_amdgcn_sched_barrier(0);            \
-    store_x(((C) + 1) & 1, xr);                   \
-    __syncthreads();                              \
-  }
-  int c = 0;
-  for (; c + 2 <= nchunks; c += 2) {
-    EIA_PHASE(c, wa, wb);
-    EIA_PHASE(c + 1, wb, wa);
-  }
-  if (c < nchunks) EIA_PHASE(c, wa, wb);
+    {                                             \
+      bf16x8 xr[XPT];                             \
+      load_x(min((C) + 1, last), xr);             \
+      load_w(min((C) + 1, last), WNEXT);          \
+      __builtin_amdgcn_sched_barrier(0);          \
+      compute((C) & 1, WCUR);                     \
+      __builtin_amdgcn_sched_barrier(0);          \
+      store_x(((C) + 1) & 1, xr);                 \
+      __syncthreads();                            \
+    }
+    int c = 0;
+    for (; c + 2 <= nchunks; c += 2) {
+      EIA_PHASE(c, wa, wb);
+      EIA_PHASE(c + 1, wb, wa);
+    }
+    if (c < nchunks) EIA_PHASE(c, wa, wb);
 #undef EIA_PHASE
 
-  // epilogue: lane (r, g) holds rows n = tile_base + 4g + i, column m = 16*mt + r
-  if (NT == 2 && mode == MODE_SWIGLU) {
-    bf16_t* o = reinterpret_cast<bf16_t*>(out);
-    const int n = nbase + 4 * g;
-#pragma unroll
-    for (int m = 0; m < MT; ++m) {
-      const int row = m * 16 + r;
-      if (row < M) {
-        bf16x4 v;
-#pragma unroll
-        for (int i = 0; i < 4; ++i) v[i] = f2bf(silu(acc[0][m][i]) * acc[NT - 1][m][i]);
-        *reinterpret_cast<bf16x4*>(o + (long)row * ldo + n) = v;
-      }
-    }
-    return;
-  }
-#pragma unroll
-  for (int t = 0; t < NT; ++t) {
-    const int n = nbase + 16 * t + 4 * g;
-    if (mode == MODE_F32_SPLIT) {
-      float* o = reinterpret_cast<float*>(out) + (long)blockIdx.y * M * N;
-#pragma unroll
-      for (int m = 0; m < MT; ++m) {
-        const int row = m * 16 + r;
-        if (row < M) *reinterpret_cast<f32x4*>(o + (long)row * N + n) = acc[t][m];
-      }
-    } else {
+    // epilogue: lane (r, g) holds rows n = tile_base + 4g + i, column m = 16*mt + r
+    const long orow0 = mbase + m0;
+    if (NT == 2 && mode == MODE_SWIGLU) {
       bf16_t* o = reinterpret_cast<bf16_t*>(out);
-      float b[4] = {0.f, 0.f, 0.f, 0.f};
-      if (bias != nullptr) {
-#pragma unroll
-        for (int i = 0; i < 4; ++i) b[i] = bf2f(bias[n + i]);
-      }
+      const int n = nbase + 4 * g;
 #pragma unroll
       for (int m = 0; m < MT; ++m) {
         const int row = m * 16 + r;
-        if (row < M) {
+        if (row < Mc) {
           bf16x4 v;
 #pragma unroll
-          for (int i = 0; i < 4; ++i) v[i] = f2bf(acc[t][m][i] + b[i]);
-          *reinterpret_cast<bf16x4*>(o + (long)row * ldo + n) = v;
+          for (int i = 0; i < 4; ++i) v[i] = f2bf(silu(acc[0][m][i]) * acc[NT - 1][m][i]);
+          *reinterpret_cast<bf16x4*>(o + (orow0 + row) * ldo + n) = v;
+        }
+      }
+      continue;
+    }
+#pragma unroll
+    for (int t = 0; t < NT; ++t) {
+      const int n = nbase + 16 * t + 4 * g;
+      if (mode == MODE_F32_SPLIT) {
+        float* o = reinterpret_cast<float*>(out) + (long)blockIdx.y * M * N;
+#pragma unroll
+        for (int m = 0; m < MT; ++m) {
+          const int row = m * 16 + r;
+          if (row < Mc) *reinterpret_cast<f32x4*>(o + (orow0 + row) * N + n) = acc[t][m];
+        }
+      } else {
+        bf16_t* o = reinterpret_cast<bf16_t*>(out);
+        float b[4] = {0.f, 0.f, 0.f, 0.f};
+        if (bias != nullptr) {
+#pragma unroll
+          for (int i = 0; i < 4; ++i) b[i] = bf2f(bias[n + i]);
+        }
+#pragma unroll
+        for (int m = 0; m < MT; ++m) {
+          const int row = m * 16 + r;
+          if (row < Mc) {
+            bf16x4 v;
+#pragma unroll
+            for (int i = 0; i < 4; ++i) v[i] = f2bf(acc[t][m][i] + b[i]);
+            *reinterpret_cast<bf16x4*>(o + (orow0 + row) * ldo + n) = v;
+          }
         }
       }
     }
@@ -269,56 +300,47 @@ splitk_add_rmsnorm_kernel(const float* __restrict__ part, int sk, int M, int H,
   }
 }
 
-template <int MT, int NT, int WAVES>
+template <int MT, int NT, int WAVES, bool GROUPED>
 int launch_cfg(const bf16_t* X, long ldx, const bf16_t* W, long ldw, const bf16_t* bias, void* out,
-               long ldo, int M, int N, int K, int sk, int mode, hipStream_t st) {
+               long ldo, int M, int N, int K, int sk, int mode, int experts, const int* offs,
+               const int* row_idx, long w_estride, hipStream_t st) {
   const size_t lds = 2ull * MT * 16 * XLD * sizeof(bf16_t);
   static bool attr_set = false;   // > 64 KiB of dynamic LDS must be opted into
   if (!attr_set) {
-    hipFuncSetAttribute(reinterpret_cast<const void*>(gemm_skinny_kernel<MT, NT, WAVES>),
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(gemm_skinny_kernel<MT, NT, WAVES, GROUPED>),
                         hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     attr_set = true;
   }
-  dim3 grid(mode == MODE_SWIGLU ? (N / 2) / (WAVES * 16) : N / (WAVES * NT * 16), sk);
-  hipLaunchKernelGGL((gemm_skinny_kernel<MT, NT, WAVES>), grid, dim3(WAVES * 64), lds, st, X, ldx,
-                     W, ldw, bias, out, ldo, M, N, K / sk, mode, N / 2);
+  dim3 grid(mode == MODE_SWIGLU ? (N / 2) / (WAVES * 16) : N / (WAVES * NT * 16), sk, experts);
+  hipLaunchKernelGGL((gemm_skinny_kernel<MT, NT, WAVES, GROUPED>), grid, dim3(WAVES * 64), lds, st,
+                     X, ldx, W, ldw, bias, out, ldo, M, N, K / sk, mode, N / 2, offs, row_idx,
+                     w_estride);
   return (int)hipGetLastError();
 }
 
-template <int MT>
+template <int MT, bool GROUPED>
 int launch_mt(int cfg, const bf16_t* X, long ldx, const bf16_t* W, long ldw, const bf16_t* bias,
-              void* out, long ldo, int M, int N, int K, int sk, int mode, hipStream_t st) {
+              void* out, long ldo, int M, int N, int K, int sk, int mode, int experts,
+              const int* offs, const int* row_idx, long w_estride, hipStream_t st) {
+#define EIA_CFG(NT_, W_) \
+  return launch_cfg<MT, NT_, W_, GROUPED>(X, ldx, W, ldw, bias, out, ldo, M, N, K, sk, mode, \
+                                          experts, offs, row_idx, w_estride, st)
   switch (cfg) {   // cfg = (NT - 1) | ((WAVES / 2 - 1) << 1)
-    case 0: return launch_cfg<MT, 1, 2>(X, ldx, W, ldw, bias, out, ldo, M, N, K, sk, mode, st);
-    case 1: return launch_cfg<MT, 2, 2>(X, ldx, W, ldw, bias, out, ldo, M, N, K, sk, mode, st);
-    case 2: return launch_cfg<MT, 1, 4>(X, ldx, W, ldw, bias, out, ldo, M, N, K, sk, mode, st);
-    default: return launch_cfg<MT, 2, 4>(X, ldx, W, ldw, bias, out, ldo, M, N, K, sk, mode, st);
+    case 0: EIA_CFG(1, 2);
+    case 1: EIA_CFG(2, 2);
+    case 2: EIA_CFG(1, 4);
+    default: EIA_CFG(2, 4);
   }
+#undef EIA_CFG
 }
 
-}  // namespace
-
-// mode 0: out bf16 [M][ldo] (+bias), sk must be 1
-// mode 1: out fp32 partial slabs [sk][M][N] (reduce with eia_splitk_reduce / _add_rmsnorm)
-// mode 2: SwiGLU: W = merged [gate; up] (N = 2I rows), out bf16 [M][ldo] = silu(gate) * up
-// cfg: bit0 -> two 16-row W tiles per wave (else one), bit1 -> 4 waves per workgroup (else 2)
-EIA_API int eia_gemm_skinny(const void* X, long ldx, const void* W, long ldw, const void* bias,
-                            void* out, long ldo, int M, int N, int K, int sk, int mode, int cfg,
-                            hipStream_t st) {
-  const int nt = (cfg & 1) ? 2 : 1, waves = (cfg & 2) ? 4 : 2;
-  if (M < 1 || M > 128 || sk < 1 || K % (sk * KC) != 0 || cfg < 0 || cfg > 3) return EIA_BAD_SHAPE;
-  if (mode == MODE_SWIGLU) {
-    if (nt != 2 || sk != 1 || N % 2 != 0 || (N / 2) % (waves * 16) != 0) return EIA_BAD_SHAPE;
-  } else if (N % (waves * nt * 16) != 0) {
-    return EIA_BAD_SHAPE;
-  }
-  if (mode == MODE_BF16 && sk != 1) return EIA_BAD_SHAPE;
-  if ((ldx % 8) || (ldw % 8) || (ldo % 4)) return EIA_BAD_SHAPE;
-  const bf16_t* x = static_cast<const bf16_t*>(X);
-  const bf16_t* w = static_cast<const bf16_t*>(W);
-  const bf16_t* b = static_cast<const bf16_t*>(bias);
-  const int mt = (M + 15) / 16;
-#define EIA_MT(V) return launch_mt<V>(cfg, x, ldx, w, ldw, b, out, ldo, M, N, K, sk, mode, st)
+template <bool GROUPED>
+int dispatch_mt(int mt, int cfg, const bf16_t* x, long ldx, const bf16_t* w, long ldw,
+                const bf16_t* b, void* out, long ldo, int M, int N, int K, int sk, int mode,
+                int experts, const int* offs, const int* row_idx, long w_estride, hipStream_t st) {
+#define EIA_MT(V) \
+  return launch_mt<V, GROUPED>(cfg, x, ldx, w, ldw, b, out, ldo, M, N, K, sk, mode, experts, offs, \
+                               row_idx, w_estride, st)
   switch (mt) {
     case 1: EIA_MT(1);
     case 2: EIA_MT(2);
@@ -330,6 +352,52 @@ EIA_API int eia_gemm_skinny(const void* X, long ldx, const void* W, long ldw, co
     default: EIA_MT(8);
   }
 #undef EIA_MT
+}
+
+int check_shape(int N, int K, int sk, int mode, int cfg) {
+  const int nt = (cfg & 1) ? 2 : 1, waves = (cfg & 2) ? 4 : 2;
+  if (sk < 1 || K % (sk * KC) != 0 || cfg < 0 || cfg > 3) return EIA_BAD_SHAPE;
+  if (mode == MODE_SWIGLU) {
+    if (nt != 2 || sk != 1 || N % 2 != 0 || (N / 2) % (waves * 16) != 0) return EIA_BAD_SHAPE;
+  } else if (N % (waves * nt * 16) != 0) {
+    return EIA_BAD_SHAPE;
+  }
+  if (mode == MODE_BF16 && sk != 1) return EIA_BAD_SHAPE;
+  return EIA_OK;
+}
+
+}  // namespace
+
+// mode 0: out bf16 [M][ldo] (+bias), sk must be 1
+// mode 1: out fp32 partial slabs [sk][M][N] (reduce with eia_splitk_reduce / _add_rmsnorm)
+// mode 2: SwiGLU: W = merged [gate; up] (N = 2I rows), out bf16 [M][ldo] = silu(gate) * up
+// cfg: bit0 -> two 16-row W tiles per wave (else one), bit1 -> 4 waves per workgroup (else 2)
+EIA_API int eia_gemm_skinny(const void* X, long ldx, const void* W, long ldw, const void* bias,
+                            void* out, long ldo, int M, int N, int K, int sk, int mode, int cfg,
+                            hipStream_t st) {
+  if (M < 1 || M > 128) return EIA_BAD_SHAPE;
+  if (int rc = check_shape(N, K, sk, mode, cfg)) return rc;
+  if ((ldx % 8) || (ldw % 8) || (ldo % 4)) return EIA_BAD_SHAPE;
+  return dispatch_mt<false>((M + 15) / 16, cfg, static_cast<const bf16_t*>(X), ldx,
+                            static_cast<const bf16_t*>(W), ldw, static_cast<const bf16_t*>(bias),
+                            out, ldo, M, N, K, sk, mode, 1, nullptr, nullptr, 0, st);
+}
+
+// K9 grouped GEMM for MoE: W = [E][N][K]; expert e multiplies the rows
+// [offs[e], offs[e+1]) of the expert-sorted list (X rows gathered through row_idx, or
+// identity when row_idx == nullptr) and writes them in sorted order into out [rows][ldo].
+// mt_hint = 16-row tiles per pass (the host's estimate of the tokens per expert).
+// mode 0 (bf16, +bias[E][N]) or 2 (SwiGLU: W rows = [gate; up] per expert).
+EIA_API int eia_moe_gemm(const void* X, long ldx, const void* W, long ldw, const void* bias,
+                         void* out, long ldo, int N, int K, int experts, const int* offs,
+                         const int* row_idx, int mt_hint, int mode, int cfg, hipStream_t st) {
+  if (experts < 1 || mode == MODE_F32_SPLIT) return EIA_BAD_SHAPE;
+  if (int rc = check_shape(N, K, 1, mode, cfg)) return rc;
+  if ((ldx % 8) || (ldw % 8) || (ldo % 4)) return EIA_BAD_SHAPE;
+  const int mt = mt_hint < 1 ? 1 : (mt_hint > 8 ? 8 : mt_hint);
+  return dispatch_mt<true>(mt, cfg, static_cast<const bf16_t*>(X), ldx,
+                           static_cast<const bf16_t*>(W), ldw, static_cast<const bf16_t*>(bias),
+                           out, ldo, 0, N, K, 1, mode, experts, offs, row_idx, (long)N * ldw, st);
 }
 
 EIA_API int eia_splitk_reduce(const float* part, int sk, int M, int N, const void* bias, void* out,

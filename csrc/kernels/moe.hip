@@ -1,0 +1,150 @@
+// K9: MoE routing kernels around the grouped skinny GEMM (gemm_skinny.hip, eia_moe_gemm).
+//
+//   router logits [T, E] --topk--> (w [T, k] fp32, ids [T, k] int32)
+//   --align--> expert offsets [E+1], sorted token list (row_idx: sorted pos -> token),
+//              inverse map (inv: t*k + slot -> sorted pos)
+//   grouped GEMM 1 (gate_up + SwiGLU epilogue), grouped GEMM 2 (down) in sorted order
+//   --combine--> out[t] = sum_slot w[t, slot] * y[inv[t*k + slot]]
+//
+// Mixtral-8x7B: E=8, k=2, softmax + renormalise; Llama-4-Scout: E=16, k=1, sigmoid scores
+// (SURVEY §2.9 K9).  Expert-parallel ranks pass [e_lo, e_hi): tokens routed to other
+// ranks' experts are dropped here and summed back by the all-reduce (parallel/comm.py).
+#include "eia_common.h"
+
+namespace {
+
+// One wave per token.  scoring 0: softmax over E then top-k (optionally renormalised);
+// scoring 1: top-k on raw logits, weight = sigmoid(logit) (Llama-4).
+template <int EMAX>
+__global__ void __launch_bounds__(256)
+topk_kernel(const void* __restrict__ logits, int is_bf16, int T, int E, int k, int renorm,
+            int scoring, float* __restrict__ w_out, int* __restrict__ id_out) {
+  const int wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const int lane = threadIdx.x & 63;
+  if (wave >= T) return;
+  float v = -INFINITY;
+  if (lane < E) {
+    v = is_bf16 ? bf2f(static_cast<const bf16_t*>(logits)[(long)wave * E + lane])
+                : static_cast<const float*>(logits)[(long)wave * E + lane];
+  }
+  float p = v;
+  if (scoring == 0) {
+    const float mx = wave_max(v);
+    const float ex = lane < E ? __expf(v - mx) : 0.f;
+    p = ex / wave_sum(ex);
+  }
+  float chosen_sum = 0.f;
+  float sel_w = 0.f;
+  int sel_slot = -1;
+  for (int s = 0; s < k; ++s) {
+    // arg-max over lanes (ties -> lower expert id)
+    float best = lane < E ? p : -INFINITY;
+    int bid = lane;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+      const float ob = __shfl_xor(best, o, 64);
+      const int oi = __shfl_xor(bid, o, 64);
+      if (ob > best || (ob == best && oi < bid)) { best = ob; bid = oi; }
+    }
+    if (lane == bid) {
+      sel_slot = s;
+      sel_w = scoring == 1 ? 1.f / (1.f + __expf(-v)) : p;
+      p = -INFINITY;
+    }
+    chosen_sum += (scoring == 1) ? 0.f : best;
+  }
+  if (sel_slot >= 0) {
+    float wv = sel_w;
+    if (renorm && scoring == 0 && chosen_sum > 0.f) wv /= chosen_sum;
+    w_out[(long)wave * k + sel_slot] = wv;
+    id_out[(long)wave * k + sel_slot] = lane;
+  }
+}
+
+// Single workgroup: counts per expert, exclusive scan, scatter.  n = T*k entries.
+__global__ void __launch_bounds__(1024)
+align_kernel(const int* __restrict__ ids, int n, int E, int e_lo, int e_hi,
+             int* __restrict__ offs, int* __restrict__ row_idx, int* __restrict__ inv, int k) {
+  __shared__ int cnt[256];
+  __shared__ int cur[256];
+  for (int e = threadIdx.x; e < E; e += blockDim.x) cnt[e] = 0;
+  __syncthreads();
+  for (int i = threadIdx.x; i < n; i += blockDim.x) {
+    const int e = ids[i];
+    if (e >= e_lo && e < e_hi) atomicAdd(&cnt[e - e_lo], 1);
+  }
+  __syncthreads();
+  const int El = e_hi - e_lo;
+  if (threadIdx.x == 0) {
+    int acc = 0;
+    for (int e = 0; e < El; ++e) {
+      offs[e] = acc;
+      cur[e] = acc;
+      acc += cnt[e];
+    }
+    offs[El] = acc;
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < n; i += blockDim.x) {
+    const int e = ids[i];
+    if (e >= e_lo && e < e_hi) {
+      const int pos = atomicAdd(&cur[e - e_lo], 1);
+      row_idx[pos] = i / k;          // token of this (token, slot) entry
+      inv[i] = pos;
+    } else {
+      inv[i] = -1;
+    }
+  }
+}
+
+// out[t][:] = sum_s w[t][s] * y[inv[t*k+s]][:]  (bf16 out, fp32 accumulate); one block per token
+__global__ void __launch_bounds__(256)
+combine_kernel(const bf16_t* __restrict__ y, long ldy, const float* __restrict__ w,
+               const int* __restrict__ inv, int k, int H, bf16_t* __restrict__ out, long ldo) {
+  const int t = blockIdx.x;
+  for (int c = threadIdx.x * 8; c < H; c += blockDim.x * 8) {
+    float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    for (int s = 0; s < k; ++s) {
+      const int pos = inv[(long)t * k + s];
+      if (pos < 0) continue;
+      const float ws = w[(long)t * k + s];
+      const bf16x8 v = *reinterpret_cast<const bf16x8*>(y + (long)pos * ldy + c);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) acc[j] += ws * bf2f(v[j]);
+    }
+    bf16x8 o;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) o[j] = f2bf(acc[j]);
+    *reinterpret_cast<bf16x8*>(out + (long)t * ldo + c) = o;
+  }
+}
+
+}  // namespace
+
+EIA_API int eia_moe_topk(const void* logits, int is_bf16, int T, int E, int k, int renorm,
+                         int scoring, float* w_out, int* id_out, hipStream_t st) {
+  if (E < 1 || E > 64 || k < 1 || k > E) return EIA_BAD_SHAPE;
+  if (T == 0) return EIA_OK;
+  const int waves_per_block = 4;
+  hipLaunchKernelGGL(topk_kernel<64>, dim3((T + waves_per_block - 1) / waves_per_block),
+                     dim3(64 * waves_per_block), 0, st, logits, is_bf16, T, E, k, renorm, scoring,
+                     w_out, id_out);
+  EIA_LAUNCH_CHECK();
+}
+
+EIA_API int eia_moe_align(const int* ids, int n, int E, int e_lo, int e_hi, int* offs,
+                          int* row_idx, int* inv, int k, hipStream_t st) {
+  if (E < 1 || E > 256 || e_lo < 0 || e_hi > E || e_lo >= e_hi || k < 1) return EIA_BAD_SHAPE;
+  hipLaunchKernelGGL(align_kernel, dim3(1), dim3(1024), 0, st, ids, n, E, e_lo, e_hi, offs,
+                     row_idx, inv, k);
+  EIA_LAUNCH_CHECK();
+}
+
+EIA_API int eia_moe_combine(const void* y, long ldy, const float* w, const int* inv, int T, int k,
+                            int H, void* out, long ldo, hipStream_t st) {
+  if (H % 8 != 0 || (ldy % 8) || (ldo % 8)) return EIA_BAD_SHAPE;
+  if (T == 0) return EIA_OK;
+  hipLaunchKernelGGL(combine_kernel, dim3(T), dim3(256), 0, st, static_cast<const bf16_t*>(y), ldy,
+                     w, inv, k, H, static_cast<bf16_t*>(out), ldo);
+  EIA_LAUNCH_CHECK();
+}

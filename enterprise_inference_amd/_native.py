@@ -39,16 +39,16 @@ _SIGNATURES = {
     "eia_rms_norm": [P, P, P, P, F, I, I, L, L, S],
     "eia_layer_norm": [P, P, P, P, P, F, I, I, S],
     "eia_rope_qkv_cache": [P, L, IP, P, IP, P, P, P, P, P, P, F, I, I, I, I, I, I, S],
-    "eia_paged_decode": [P, L, P, P, IP, I, IP, P, L, P, P, F, I, I, I, I, I, I, S],
+    "eia_paged_decode": [P, L, P, P, IP, I, IP, P, L, P, P, F, I, I, I, I, I, I, I, I, S],
     "eia_paged_prefill": [P, L, P, L, P, P, IP, I, IP, IP, IP, I, F, I, I, I, I, I, I, I, I, S],
     "eia_act_and_mul": [P, P, I, I, L, L, I, S],
     "eia_act": [P, P, L, I, S],
     "eia_sample": [P, L, I, I, P, P, P, P, P, P, S],
     "eia_apply_penalties": [P, L, P, P, P, I, P, P, P, S],
-    "eia_moe_topk_softmax": [P, I, I, I, I, P, P, I, S],
-    "eia_moe_align": [P, I, I, I, I, P, P, P, P, S],
-    "eia_grouped_gemm": [P, P, P, P, P, P, I, I, I, I, I, I, I, S],
-    "eia_moe_combine": [P, P, P, P, I, I, I, S],
+    "eia_moe_topk": [P, I, I, I, I, I, I, P, P, S],
+    "eia_moe_align": [P, I, I, I, I, P, P, P, I, S],
+    "eia_moe_gemm": [P, L, P, L, P, P, L, I, I, I, P, P, I, I, I, S],
+    "eia_moe_combine": [P, L, P, P, I, I, I, P, L, S],
     "eia_gemm_skinny": [P, L, P, L, P, P, L, I, I, I, I, I, I, S],
     "eia_splitk_reduce": [P, I, I, I, P, P, L, S],
     "eia_splitk_add_rmsnorm": [P, I, I, I, P, P, F, P, L, S],

@@ -161,6 +161,19 @@ class ModelConfig:
             attention_chunk_size=d.get("attention_chunk_size"),
             name=name,
         )
+        extra = {}
+        L = d["num_hidden_layers"]
+        if arch.startswith("Llama4"):
+            extra["no_rope_layers"] = d.get("no_rope_layers") or [
+                int((i + 1) % d.get("no_rope_layer_interval", 4) != 0) for i in range(L)]
+            step = d.get("interleave_moe_layer_step", 1) or 1
+            extra["moe_layers"] = d.get("moe_layers") or [i for i in range(L) if (i + 1) % step == 0]
+            for key in ("use_qk_norm", "attn_temperature_tuning", "floor_scale", "attn_scale",
+                        "intermediate_size_mlp"):
+                if key in d:
+                    extra[key] = d[key]
+            extra["rope_interleaved"] = True
+        kw["extra"] = extra
         if arch.startswith("OPT"):
             kw["position_offset"] = 2
             kw["hidden_act"] = d.get("activation_function", "relu")

@@ -1,0 +1,285 @@
+"""Mixture-of-experts decoders (Mixtral-8x7B #9, Llama-4-Scout #5;
+plus Qwen2-MoE / Qwen3-MoE).
+
+* ``MixtralForCausalLM``  softmax top-2 routing over 8 SwiGLU experts
+  (core/helm-charts/vllm/gaudi-values.yaml:354-375); also Qwen3-MoE
+  (``norm_topk_prob``) and Qwen2-MoE (+ gated shared expert).
+* ``Llama4ForCausalLM``   text path of Llama-4-Scout-17B-16E
+  (core/helm-charts/vllm/gaudi-values.yaml:258-278, gaudi3-values.yaml:492-501):
+  sigmoid top-1 routing applied to the expert *input*, a shared expert, chunked
+  local attention (8192) on RoPE layers, GPT-J-style (interleaved) RoPE, weightless
+  QK L2-norm on RoPE layers, NoPE every 4th layer with attention temperature tuning.
+
+Experts live in one ``FusedMoE`` module ([E, 2I, H] / [E, H, I] tensors, K9 kernels in
+ops/moe.py).  Tensor parallel shards each expert's I; ``--enable-expert-parallel``
+instead gives each rank E/tp whole experts (the reference's EP on Gaudi 3,
+``VLLM_EP_SIZE``); either way the layer output is all-reduced over the TP group.
+"""
+
+from __future__ import annotations
+
+import math
+from typing import Iterable, List, Optional, Tuple
+
+import torch
+import torch.nn as nn
+
+from ..config import ModelConfig
+from ..ops import moe as moe_ops
+from ..parallel import comm, state
+from .layers import MergedColumnParallelLinear, ReplicatedLinear, RowParallelLinear, _param
+from .llama import LlamaAttention, LlamaDecoderLayer, LlamaForCausalLM, LlamaMLP
+
+
+class FusedMoE(nn.Module):
+    def __init__(self, num_experts: int, top_k: int, hidden: int, inter: int,
+                 renormalize: bool = True, scoring: str = "softmax", scale_input: bool = False,
+                 dtype=torch.bfloat16, device=None):
+        super().__init__()
+        tp, r = state.tp_size(), state.tp_rank()
+        self.E, self.k, self.H = num_experts, top_k, hidden
+        self.ep = state.ep_enabled()
+        if self.ep:
+            if num_experts % tp:
+                raise ValueError("num_experts must be divisible by the EP size")
+            self.e_per = num_experts // tp
+            self.e_lo = r * self.e_per
+            self.I_local = inter
+        else:
+            self.e_per, self.e_lo = num_experts, 0
+            if inter % tp:
+                raise ValueError("moe intermediate size must be divisible by tp")
+            self.I_local = inter // tp
+        self.I = inter
+        self.renormalize, self.scoring, self.scale_input = renormalize, scoring, scale_input
+        self.w13 = _param((self.e_per, 2 * self.I_local, hidden), dtype, device)
+        self.w2 = _param((self.e_per, hidden, self.I_local), dtype, device)
+        self.w13.weight_loader = self._load_w13
+        self.w2.weight_loader = self._load_w2
+
+    # shard helpers: loaded tensors are full [I, H] / [H, I] per expert
+    def _local(self, expert: int) -> Optional[int]:
+        e = expert - self.e_lo
+        return e if 0 <= e < self.e_per else None
+
+    def _ishard(self, t: torch.Tensor, dim: int) -> torch.Tensor:
+        if self.ep or state.tp_size() == 1:
+            return t
+        n = self.I_local
+        return t.narrow(dim, state.tp_rank() * n, n)
+
+    def _load_w13(self, param, loaded, shard_id):
+        expert, which = shard_id               # which: "w1" (gate) | "w3" (up) | "w13"
+        e = self._local(expert)
+        if e is None:
+            return
+        if which == "w13":                     # fused [2I, H] (gate rows then up rows)
+            g, u = loaded.chunk(2, dim=0)
+            param.data[e, :self.I_local].copy_(self._ishard(g, 0))
+            param.data[e, self.I_local:].copy_(self._ishard(u, 0))
+            return
+        off = 0 if which == "w1" else self.I_local
+        param.data[e, off:off + self.I_local].copy_(self._ishard(loaded, 0))
+
+    def _load_w2(self, param, loaded, shard_id):
+        expert, _ = shard_id
+        e = self._local(expert)
+        if e is not None:
+            param.data[e].copy_(self._ishard(loaded, 1))
+
+    def forward(self, x: torch.Tensor, router_logits: torch.Tensor, reduce: bool = True):
+        w, ids = moe_ops.topk_route(router_logits, self.k, self.renormalize, self.scoring)
+        if self.scale_input:
+            # Llama-4 applies the routing score to the expert input (k = 1)
+            x = (x.float() * w[:, :1]).to(x.dtype)
+            w = torch.ones_like(w)
+        out = moe_ops.fused_moe(x, self.w13, self.w2, w, ids,
+                                (self.e_lo, self.e_lo + self.e_per) if self.ep else None)
+        if reduce and state.tp_size() > 1:
+            out = comm.all_reduce(out)
+        return out
+
+
+class MixtralMoE(nn.Module):
+    """block_sparse_moe (Mixtral) / mlp (Qwen-MoE): router + FusedMoE [+ shared expert]."""
+
+    def __init__(self, cfg: ModelConfig, dtype, device):
+        super().__init__()
+        H = cfg.hidden_size
+        inter = cfg.moe_intermediate_size or cfg.intermediate_size
+        self.gate = ReplicatedLinear(H, cfg.num_local_experts, dtype=dtype, device=device)
+        renorm = cfg.norm_topk_prob if cfg.architecture.startswith("Qwen") else True
+        self.experts = FusedMoE(cfg.num_local_experts, cfg.num_experts_per_tok, H, inter, renorm,
+                                dtype=dtype, device=device)
+        self.shared_expert = None
+        if cfg.shared_expert_intermediate_size:
+            self.shared_expert = LlamaMLP(H, cfg.shared_expert_intermediate_size, "silu", dtype,
+                                          device)
+            self.shared_expert.down_proj.reduce_results = False   # one all-reduce for the sum
+            self.shared_expert_gate = ReplicatedLinear(H, 1, dtype=dtype, device=device)
+
+    def forward(self, x):
+        out = self.experts(x, self.gate(x), reduce=self.shared_expert is None)
+        if self.shared_expert is not None:
+            s = self.shared_expert(x)
+            s = s.materialize() if hasattr(s, "materialize") else s
+            out = out + torch.sigmoid(self.shared_expert_gate(x).float()).to(x.dtype) * s
+            if state.tp_size() > 1:
+                out = comm.all_reduce(out)
+        return out
+
+
+class MixtralForCausalLM(LlamaForCausalLM):
+    def __init__(self, cfg: ModelConfig, dtype=torch.bfloat16, device=None):
+        super().__init__(cfg, dtype, device, layer_factory=lambda i: LlamaDecoderLayer(
+            cfg, i, self.rotary, dtype, device, mlp=MixtralMoE(cfg, dtype, device)))
+
+    def map_weight_name(self, name: str):
+        n = name.replace("model.", "", 1) if name.startswith("model.") else name
+        n = n.replace("block_sparse_moe.", "mlp.")
+        if n.endswith(".mlp.experts.gate_up_proj"):      # transformers>=5 stacked [E, 2I, H]
+            return n.replace("experts.gate_up_proj", "experts.w13"), "stacked"
+        if n.endswith(".mlp.experts.down_proj"):         # stacked [E, H, I]
+            return n.replace("experts.down_proj", "experts.w2"), "stacked"
+        if ".mlp.experts." in n:
+            pre, rest = n.split(".mlp.experts.", 1)
+            e, _, w = rest.partition(".")
+            which = {"w1": "w1", "w3": "w3", "w2": "w2", "gate_proj": "w1", "up_proj": "w3",
+                     "down_proj": "w2"}[w.split(".")[0]]
+            tgt = f"{pre}.mlp.experts.{'w2' if which == 'w2' else 'w13'}"
+            return tgt, (int(e), which)
+        if ".mlp.shared_expert." in n:
+            for part, sid in (("gate_proj", 0), ("up_proj", 1)):
+                if f".{part}." in n:
+                    return n.replace(part, "gate_up_proj"), sid
+            return n, None
+        return super().map_weight_name(name)
+
+    def load_weights(self, weights: Iterable[Tuple[str, torch.Tensor]]) -> List[str]:
+        return _load_with_stacked_experts(self, weights, super().load_weights)
+
+
+def _load_with_stacked_experts(model, weights, base_load):
+    """Route stacked expert tensors ([E, out, in], or [E, in, out] = "fused_t") through the
+    FusedMoE loaders (which shard per rank); everything else through ``base_load``."""
+    params = dict(model.named_parameters())
+    rest, loaded = [], []
+    for name, t in weights:
+        pname, sid = model.map_weight_name(name)
+        if sid in ("stacked", "fused_t"):
+            p = params[pname]
+            kind = "w13" if pname.endswith("w13") else "w2"
+            for e in range(t.shape[0]):
+                te = t[e].t() if sid == "fused_t" else t[e]
+                p.weight_loader(p, te.to(p.dtype), (e, kind))
+            loaded.append(pname)
+        elif pname != "__skip__":
+            rest.append((name, t))
+    return loaded + base_load(rest)
+
+
+# ----------------------------------------------------------------------------- Llama-4
+
+
+class Llama4Attention(LlamaAttention):
+    def __init__(self, cfg: ModelConfig, idx: int, rotary, dtype, device):
+        super().__init__(cfg, idx, rotary, dtype, device)
+        ex = cfg.extra
+        nope = ex.get("no_rope_layers")
+        self.use_rope = bool(nope[idx]) if nope else True
+        if not self.use_rope:
+            self.rotary = None
+            self.chunk_size = None
+        else:
+            self.chunk_size = cfg.attention_chunk_size
+        self.qk_l2 = bool(ex.get("use_qk_norm", True)) and self.use_rope
+        self.temp_tuning = bool(ex.get("attn_temperature_tuning", True)) and not self.use_rope
+        self.floor_scale = float(ex.get("floor_scale", 8192))
+        self.attn_scale = float(ex.get("attn_scale", 0.1))
+        D = cfg.head_dim
+        if self.qk_l2:   # weightless L2 norm == RMSNorm with unit weight (rotation-invariant)
+            self.register_buffer("ones", torch.ones(D, dtype=dtype, device=device),
+                                 persistent=False)
+
+    def forward(self, h, md, kv):
+        from ..ops.attention import attention
+        from ..ops.rotary import rope_qkv_cache
+        from ..ops import gemm
+
+        T = h.shape[0]
+        qkv = gemm.linear(h, self.qkv_proj.weight)
+        q = rope_qkv_cache(qkv, md.positions, self.rotary, md.slot_mapping, kv[0], kv[1],
+                           self.num_heads, self.num_kv_heads, self.head_dim,
+                           bias=self.qkv_proj.bias,
+                           q_norm_w=self.ones if self.qk_l2 else None,
+                           k_norm_w=self.ones if self.qk_l2 else None,
+                           norm_eps=self.cfg.rms_norm_eps)
+        if self.temp_tuning:
+            pos = md.positions.float()
+            sc = torch.log1p(torch.floor((pos + 1.0) / self.floor_scale)) * self.attn_scale + 1.0
+            q = (q.float() * sc[:, None, None]).to(q.dtype)
+        o = attention(q, kv[0], kv[1], md, self.scale, None, self.chunk_size)
+        return self.o_proj(o.view(T, self.num_heads * self.head_dim), defer_reduce=True)
+
+
+class Llama4MoE(nn.Module):
+    def __init__(self, cfg: ModelConfig, dtype, device):
+        super().__init__()
+        H = cfg.hidden_size
+        self.router = ReplicatedLinear(H, cfg.num_local_experts, dtype=dtype, device=device)
+        self.experts = FusedMoE(cfg.num_local_experts, cfg.num_experts_per_tok, H,
+                                cfg.intermediate_size, renormalize=False, scoring="sigmoid",
+                                scale_input=True, dtype=dtype, device=device)
+        self.shared_expert = LlamaMLP(H, cfg.intermediate_size, "silu", dtype, device)
+        self.shared_expert.down_proj.reduce_results = False   # one all-reduce for the sum
+
+    def forward(self, x):
+        routed = self.experts(x, self.router(x), reduce=False)
+        s = self.shared_expert.down_proj(self.shared_expert.gate_up_proj.forward_act_and_mul(x))
+        out = routed + s
+        if state.tp_size() > 1:
+            out = comm.all_reduce(out)
+        return out
+
+
+class Llama4ForCausalLM(LlamaForCausalLM):
+    def __init__(self, cfg: ModelConfig, dtype=torch.bfloat16, device=None):
+        cfg.extra.setdefault("rope_interleaved", True)
+        moe_layers = set(cfg.extra.get("moe_layers") or range(cfg.num_hidden_layers))
+        inter_mlp = cfg.extra.get("intermediate_size_mlp") or cfg.intermediate_size
+
+        def make(i):
+            mlp = Llama4MoE(cfg, dtype, device) if i in moe_layers else \
+                LlamaMLP(cfg.hidden_size, inter_mlp, "silu", dtype, device)
+            layer = LlamaDecoderLayer(cfg, i, self.rotary, dtype, device, mlp=mlp)
+            layer.self_attn = Llama4Attention(cfg, i, self.rotary, dtype, device)
+            return layer
+
+        super().__init__(cfg, dtype, device, layer_factory=make)
+
+    def map_weight_name(self, name: str):
+        n = name
+        for p in ("language_model.model.", "language_model.", "model."):
+            if n.startswith(p):
+                n = n[len(p):]
+                break
+        if n.startswith("vision_model") or n.startswith("multi_modal_projector"):
+            return "__skip__", None
+        n = n.replace(".feed_forward.", ".mlp.")
+        if ".mlp.experts.gate_up_proj" in n:
+            return n.replace("experts.gate_up_proj", "experts.w13"), "fused_t"
+        if ".mlp.experts.down_proj" in n:
+            return n.replace("experts.down_proj", "experts.w2"), "fused_t"
+        if ".mlp.shared_expert." in n:
+            for part, sid in (("gate_proj", 0), ("up_proj", 1)):
+                if f".{part}." in n:
+                    return n.replace(part, "gate_up_proj"), sid
+            return n, None
+        return super().map_weight_name(name if not name.startswith("language_model.")
+                                       else name[len("language_model."):])
+
+    def load_weights(self, weights: Iterable[Tuple[str, torch.Tensor]]) -> List[str]:
+        strip = lambda n: n[len("language_model."):] if n.startswith("language_model.") else n
+        return _load_with_stacked_experts(
+            self, weights, lambda rest: super(Llama4ForCausalLM, self).load_weights(
+                (strip(n), t) for n, t in rest))

@@ -74,10 +74,12 @@ def paged_decode(q: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tensor,
                  block_tables: torch.Tensor, seq_lens: torch.Tensor, scale: float,
                  partitions: int = 1, part_o: Optional[torch.Tensor] = None,
                  part_ml: Optional[torch.Tensor] = None,
-                 out: Optional[torch.Tensor] = None) -> torch.Tensor:
+                 out: Optional[torch.Tensor] = None, sliding_window: Optional[int] = None,
+                 chunk_size: Optional[int] = None) -> torch.Tensor:
     """q [B, Hq, D] -> out [B, Hq, D]."""
     if not (use_hip(q, k_cache) and q.dtype == torch.bfloat16):
-        r = ref.paged_attention_decode(q, k_cache, v_cache, block_tables, seq_lens, scale)
+        r = ref.paged_attention_decode(q, k_cache, v_cache, block_tables, seq_lens, scale,
+                                       sliding_window, chunk_size)
         if out is not None:
             out.copy_(r)
             return out
@@ -97,7 +99,7 @@ def paged_decode(q: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tensor,
         ptr(q), q.stride(0), ptr(k_cache), ptr(v_cache), ptr(block_tables), block_tables.stride(0),
         ptr(seq_lens), ptr(o), o.stride(0), ptr(part_o) if partitions > 1 else None,
         ptr(part_ml) if partitions > 1 else None, float(scale), B, Hq, Hkv, D, bs, partitions,
-        stream(q)), "paged_decode")
+        sliding_window or 0, chunk_size or 0, stream(q)), "paged_decode")
     return o
 
 
@@ -137,11 +139,13 @@ def attention(q: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tensor,
     nd = md.num_decode
     if md.num_prefill_tokens == 0:
         return paged_decode(q[:nd], k_cache, v_cache, md.decode_block_tables, md.decode_seq_lens,
-                            scale, md.decode_partitions, md.decode_part_o, md.decode_part_ml)
+                            scale, md.decode_partitions, md.decode_part_o, md.decode_part_ml,
+                            sliding_window=sliding_window, chunk_size=chunk_size)
     out = torch.empty_like(q)
     if nd:
         paged_decode(q[:nd], k_cache, v_cache, md.decode_block_tables, md.decode_seq_lens, scale,
-                     md.decode_partitions, md.decode_part_o, md.decode_part_ml, out=out[:nd])
+                     md.decode_partitions, md.decode_part_o, md.decode_part_ml, out=out[:nd],
+                     sliding_window=sliding_window, chunk_size=chunk_size)
     paged_prefill(q[nd:], k_cache, v_cache, md.prefill_block_tables, md.prefill_seq_lens,
                   md.prefill_cu_q, md.prefill_work, md.prefill_n_work, scale, md.causal,
                   sliding_window, chunk_size, out=out[nd:])

@@ -115,13 +115,24 @@ def apply_rope(x: torch.Tensor, positions: torch.Tensor, cos_sin: torch.Tensor) 
     return torch.cat([x1 * cos - x2 * sin, x2 * cos + x1 * sin], dim=-1).to(x.dtype)
 
 
+def apply_rope_gptj(x: torch.Tensor, positions: torch.Tensor, cos_sin: torch.Tensor) -> torch.Tensor:
+    """Interleaved (GPT-J / Llama-4) rotation of pairs (2i, 2i+1) by frequency i."""
+    d2 = x.shape[-1] // 2
+    cs = cos_sin[positions.long()]
+    cos, sin = cs[:, None, :d2], cs[:, None, d2:]
+    xf = x.float()
+    x1, x2 = xf[..., 0::2], xf[..., 1::2]
+    out = torch.stack([x1 * cos - x2 * sin, x2 * cos + x1 * sin], dim=-1)
+    return out.flatten(-2).to(x.dtype)
+
+
 def rope_qkv_cache(qkv: torch.Tensor, positions: torch.Tensor, cos_sin: Optional[torch.Tensor],
                    slot_mapping: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tensor,
                    num_heads: int, num_kv_heads: int, head_dim: int,
                    bias: Optional[torch.Tensor] = None,
                    q_norm_w: Optional[torch.Tensor] = None,
                    k_norm_w: Optional[torch.Tensor] = None,
-                   norm_eps: float = 1e-6) -> torch.Tensor:
+                   norm_eps: float = 1e-6, is_neox: bool = True) -> torch.Tensor:
     """Reference for the fused K4 kernel (bias → qk-norm → RoPE → KV write).
 
     Returns q [T, Hq, D] (rotated). K/V are written into the paged cache at
@@ -138,8 +149,9 @@ def rope_qkv_cache(qkv: torch.Tensor, positions: torch.Tensor, cos_sin: Optional
         q = rms_norm(q, q_norm_w, norm_eps)
         k = rms_norm(k, k_norm_w, norm_eps)
     if cos_sin is not None:
-        q = apply_rope(q, positions, cos_sin)
-        k = apply_rope(k, positions, cos_sin)
+        rot = apply_rope if is_neox else apply_rope_gptj
+        q = rot(q, positions, cos_sin)
+        k = rot(k, positions, cos_sin)
     write_kv_cache(k, v, slot_mapping, k_cache, v_cache)
     return q.contiguous()
 
@@ -193,13 +205,22 @@ def _attend(q, k, v, scale, causal_offset: Optional[int], chunk: Optional[int] =
 
 def paged_attention_decode(q: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tensor,
                            block_tables: torch.Tensor, seq_lens: torch.Tensor,
-                           scale: float) -> torch.Tensor:
+                           scale: float, sliding_window: Optional[int] = None,
+                           chunk_size: Optional[int] = None) -> torch.Tensor:
     """q [B, Hq, D] (one new token per sequence, already in the cache)."""
     out = torch.empty_like(q)
     for b in range(q.shape[0]):
         n = int(seq_lens[b])
+        if n == 0:
+            out[b] = 0
+            continue
+        lo = 0
+        if sliding_window:
+            lo = max(lo, n - sliding_window)
+        if chunk_size:
+            lo = max(lo, ((n - 1) // chunk_size) * chunk_size)
         k, v = _gather_kv(k_cache, v_cache, block_tables[b], n)
-        out[b] = _attend(q[b:b + 1], k, v, scale, None)[0].to(q.dtype)
+        out[b] = _attend(q[b:b + 1], k[lo:], v[lo:], scale, None)[0].to(q.dtype)
     return out
 
 

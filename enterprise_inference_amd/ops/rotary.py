@@ -29,11 +29,9 @@ def rope_qkv_cache(qkv: torch.Tensor, positions: Optional[torch.Tensor],
     """qkv [T, (Hq+2Hkv)*D] -> q [T, Hq, D]; k/v scattered into the paged cache."""
     cos_sin = None if rotary is None else rotary.cos_sin
     if not (use_hip(qkv, k_cache) and qkv.dtype == torch.bfloat16):
-        if rotary is not None and not rotary.is_neox:
-            raise NotImplementedError("GPT-J style RoPE only on the HIP path")
         return ref.rope_qkv_cache(qkv, positions, cos_sin, slot_mapping, k_cache, v_cache,
                                   num_heads, num_kv_heads, head_dim, bias, q_norm_w, k_norm_w,
-                                  norm_eps)
+                                  norm_eps, rotary is None or rotary.is_neox)
     T = qkv.shape[0]
     require(qkv.stride(-1) == 1 and qkv.shape[1] == (num_heads + 2 * num_kv_heads) * head_dim,
             "rope_qkv_cache: qkv shape")

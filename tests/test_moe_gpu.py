@@ -1,0 +1,71 @@
+"""K9 MoE kernels (routing, alignment, grouped skinny GEMM, combine) vs the fp32 reference,
+plus windowed decode attention (Mistral sliding window / Llama-4 chunks)."""
+
+import pytest
+import torch
+
+from enterprise_inference_amd.ops import reference as ref
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+BF = torch.bfloat16
+
+
+@pytest.mark.parametrize("T,E,k,scoring", [(1, 8, 2, "softmax"), (65, 8, 2, "softmax"),
+                                           (130, 16, 1, "sigmoid"), (7, 64, 6, "softmax")])
+def test_topk(T, E, k, scoring):
+    from enterprise_inference_amd.ops import moe
+    lg = torch.randn(T, E, device=DEV, dtype=BF)
+    w, ids = moe.topk_route(lg, k, True, scoring)
+    if scoring == "softmax":
+        rw, rids = ref.topk_softmax(lg.float(), k, True)
+    else:
+        v, rids = torch.topk(lg.float(), k, dim=-1)
+        rw = torch.sigmoid(v)
+    assert torch.equal(ids.sort(-1).values.cpu(), rids.int().sort(-1).values.cpu())
+    o1, o2 = ids.argsort(-1), rids.argsort(-1)
+    assert torch.allclose(w.gather(1, o1).cpu(), rw.gather(1, o2).float().cpu(), atol=1e-5)
+
+
+@pytest.mark.parametrize("T,E,k,H,I", [(1, 8, 2, 512, 256), (33, 8, 2, 1024, 512),
+                                       (65, 8, 2, 4096, 1792), (200, 4, 2, 512, 256)])
+def test_fused_moe_grouped(T, E, k, H, I):
+    from enterprise_inference_amd.ops import moe
+    torch.manual_seed(T)
+    x = torch.randn(T, H, device=DEV, dtype=BF)
+    w13 = (torch.randn(E, 2 * I, H, device=DEV) * H ** -0.5).to(BF)
+    w2 = (torch.randn(E, H, I, device=DEV) * I ** -0.5).to(BF)
+    w, ids = moe.topk_route(torch.randn(T, E, device=DEV), k, True)
+    out = moe.fused_moe(x, w13, w2, w, ids)
+    r = ref.fused_moe(x.cpu(), w13.cpu(), w2.cpu(), w.cpu(), ids.cpu())
+    err = (out.float().cpu() - r.float()).abs()
+    assert err.max() < 3e-2 + 3e-2 * r.float().abs().max(), err.max()
+
+
+def test_fused_moe_expert_parallel_slices_sum():
+    from enterprise_inference_amd.ops import moe
+    T, E, k, H, I = 40, 8, 2, 512, 256
+    x = torch.randn(T, H, device=DEV, dtype=BF)
+    w13 = (torch.randn(E, 2 * I, H, device=DEV) * H ** -0.5).to(BF)
+    w2 = (torch.randn(E, H, I, device=DEV) * I ** -0.5).to(BF)
+    w, ids = moe.topk_route(torch.randn(T, E, device=DEV), k, True)
+    full = moe.fused_moe(x, w13, w2, w, ids).float()
+    part = sum(moe.fused_moe(x, w13[r * 2:(r + 1) * 2], w2[r * 2:(r + 1) * 2], w, ids,
+                             (r * 2, r * 2 + 2)).float() for r in range(4))
+    assert (full - part).abs().max() < 5e-2
+
+
+@pytest.mark.parametrize("window,chunk", [(64, None), (None, 96)])
+def test_decode_window(window, chunk):
+    from enterprise_inference_amd.ops import attention as A
+    B, Hq, Hkv, D, bs, L = 3, 8, 2, 128, 128, 300
+    nb = B * 3
+    kc = torch.randn(nb, Hkv, bs, D, device=DEV, dtype=BF)
+    vc = torch.randn(nb, Hkv, D, bs, device=DEV, dtype=BF)
+    bt = torch.arange(nb, dtype=torch.int32, device=DEV).view(B, 3)
+    lens = torch.tensor([L, 129, 37], dtype=torch.int32, device=DEV)
+    q = torch.randn(B, Hq, D, device=DEV, dtype=BF)
+    out = A.paged_decode(q, kc, vc, bt, lens, 0.088, sliding_window=window, chunk_size=chunk)
+    r = ref.paged_attention_decode(q.cpu(), kc.cpu(), vc.cpu(), bt.cpu(), lens.cpu(), 0.088,
+                                   window, chunk)
+    assert (out.float().cpu() - r.float()).abs().max() < 3e-2
