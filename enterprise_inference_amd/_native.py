@@ -52,8 +52,11 @@ _SIGNATURES = {
     "eia_gemm_skinny": [P, L, P, L, P, P, L, I, I, I, I, I, I, S],
     "eia_splitk_reduce": [P, I, I, I, P, P, L, S],
     "eia_splitk_add_rmsnorm": [P, I, I, I, P, P, F, P, L, S],
-    "eia_ar_oneshot": [P, P, P, P, I, I, I, L, I, S],
-    "eia_ar_twoshot": [P, P, P, P, I, I, I, L, I, S],
+    "eia_ar_alloc": [P, L],
+    "eia_ar_free": [P],
+    "eia_ar_signal_bytes": [],
+    "eia_ar_run": [P, P, I, I, P, P, L, L, I, I, S],
+    "eia_ar_read_err": [P, P],
 }
 
 

@@ -220,7 +220,7 @@ class ParallelConfig:
     enable_expert_parallel: bool = False
     distributed_executor_backend: str = "mp"
     # Custom xGMI all-reduce (one-shot/two-shot) below this many bytes; RCCL above.
-    custom_allreduce_max_bytes: int = 64 * 1024 * 1024
+    custom_allreduce_max_bytes: int = 16 * 1024 * 1024
     disable_custom_all_reduce: bool = False
 
     @property

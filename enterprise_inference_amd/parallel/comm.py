@@ -42,9 +42,9 @@ def all_gather(x: torch.Tensor, dim: int = -1) -> torch.Tensor:
     if ws == 1:
         return x
     dim = dim % x.dim()
-    out = torch.empty((ws,) + tuple(x.shape), dtype=x.dtype, device=x.device)
-    dist.all_gather_into_tensor(out, x.contiguous(), group=state.tp_group())
-    out = out.movedim(0, dim)
+    flat = torch.empty(ws * x.numel(), dtype=x.dtype, device=x.device)
+    dist.all_gather_into_tensor(flat, x.contiguous().view(-1), group=state.tp_group())
+    out = flat.view((ws,) + tuple(x.shape)).movedim(0, dim)
     shape = list(x.shape)
     shape[dim] *= ws
     return out.reshape(shape)

@@ -1,20 +1,25 @@
-"""Custom xGMI all-reduce (K12) for decode-sized TP messages.
+"""Custom xGMI all-reduce (K12) for decode-sized TP messages (SURVEY §2.10 C1-C3, §2.12).
 
-Each rank registers one IPC-shared device buffer (hipIpcGetMemHandle, exchanged
-over the gloo group) plus a signal area.  Per call every rank copies its input
-into its own buffer, raises a flag, and the kernel in csrc/kernels/allreduce.hip
-either
-  * one-shot: reads all peers' buffers and sums (1 sync; small messages), or
-  * two-shot: reduce-scatter its 1/n slice from all peers, then all-gather the
-    reduced slices (2 syncs; every xGMI link carries 2S/n bytes).
-Larger messages go to RCCL (parallel/comm.py).  See SURVEY §2.12 for the xGMI
-arithmetic behind the crossover.
+Every rank allocates an UNCACHED signal block and a double-buffered data region
+(``eia_ar_alloc`` -> hipExtMallocWithFlags(hipDeviceMallocUncached)), exports them with
+hipIpcGetMemHandle, and the handles are exchanged once over the gloo TP group.  Each
+call is ONE kernel (csrc/kernels/allreduce.hip): blocks stage their share of the input
+into the own buffer, meet the same block of every peer at a flag barrier, then
+  * one-shot: sum all W peers' buffers directly (1 sync; small messages), or
+  * two-shot: reduce-scatter + all-gather over all links (2 syncs; every xGMI link
+    carries 2S/W bytes).
+No host-side state changes between calls, so TP decode steps stay HIP-graph capturable.
+Messages above ``max_bytes`` go to RCCL (parallel/comm.py).
+
+The one-shot/two-shot crossover defaults to 512 KiB (SURVEY §2.12 xGMI arithmetic:
+one-shot moves S per link with one sync, two-shot 2S/W with two).
 """
 
 from __future__ import annotations
 
 import ctypes
 import logging
+import os
 from typing import List, Optional
 
 import torch
@@ -31,7 +36,12 @@ _hip = None
 def _hiprt():
     global _hip
     if _hip is None:
-        _hip = ctypes.CDLL("libamdhip64.so.7")
+        for name in ("libamdhip64.so", "libamdhip64.so.7", "libamdhip64.so.6"):
+            try:
+                _hip = ctypes.CDLL(name)
+                break
+            except OSError:
+                continue
     return _hip
 
 
@@ -39,7 +49,7 @@ class _IpcHandle(ctypes.Structure):
     _fields_ = [("reserved", ctypes.c_char * 64)]
 
 
-def _ipc_get(ptr: int) -> bytes:
+def ipc_get(ptr: int) -> bytes:
     h = _IpcHandle()
     rc = _hiprt().hipIpcGetMemHandle(ctypes.byref(h), ctypes.c_void_p(ptr))
     if rc != 0:
@@ -47,7 +57,7 @@ def _ipc_get(ptr: int) -> bytes:
     return bytes(h.reserved)
 
 
-def _ipc_open(handle: bytes) -> int:
+def ipc_open(handle: bytes) -> int:
     h = _IpcHandle()
     ctypes.memmove(ctypes.addressof(h), handle, 64)
     p = ctypes.c_void_p()
@@ -59,47 +69,85 @@ def _ipc_open(handle: bytes) -> int:
 
 class CustomAllReduce:
     MAX_RANKS = 8
-    SIGNAL_BYTES = 64 * 1024
 
-    def __init__(self, max_bytes: int):
-        self.rank = state.tp_rank()
-        self.world = state.tp_size()
+    def __init__(self, max_bytes: int, group=None, cpu_group=None, rank: Optional[int] = None,
+                 world: Optional[int] = None, nblocks: int = 32,
+                 oneshot_max: Optional[int] = None):
+        self.rank = state.tp_rank() if rank is None else rank
+        self.world = state.tp_size() if world is None else world
+        self.cpu_group = cpu_group if cpu_group is not None else state.tp_cpu_group()
         self.max_bytes = max_bytes
-        dev = torch.device("cuda", torch.cuda.current_device())
-        # data buffer (+ signal area at the end), zero-initialised
-        self.buf = torch.zeros(max_bytes + self.SIGNAL_BYTES, dtype=torch.uint8, device=dev)
-        torch.cuda.synchronize()
-        my = _ipc_get(self.buf.data_ptr())
-        handles: List[Optional[bytes]] = [None] * self.world
-        dist.all_gather_object(handles, my, group=state.tp_cpu_group())
-        ptrs = []
-        for r, h in enumerate(handles):
-            ptrs.append(self.buf.data_ptr() if r == self.rank else _ipc_open(h))
-        self.peer_ptrs = torch.tensor(ptrs + [0] * (self.MAX_RANKS - self.world), dtype=torch.int64,
-                                      device=dev)
-        self.epoch = torch.zeros(1, dtype=torch.int32, device=dev)
+        self.nblocks = nblocks
+        self.oneshot_max = oneshot_max or int(os.environ.get("EIA_AR_ONESHOT_MAX", 512 * 1024))
         self.lib = _native.kernels()
-        self.oneshot_max = 512 * 1024
+        sig_bytes = self.lib.eia_ar_signal_bytes()
+        self._own = []
+        sig = self._alloc(sig_bytes)
+        data = self._alloc(2 * max_bytes)
+        mine = (ipc_get(sig), ipc_get(data))
+        handles: List[Optional[tuple]] = [None] * self.world
+        dist.all_gather_object(handles, mine, group=self.cpu_group)
+        self._opened = []
+        sigs, datas = [], []
+        for r, (hs, hd) in enumerate(handles):
+            if r == self.rank:
+                sigs.append(sig)
+                datas.append(data)
+            else:
+                ps, pd = ipc_open(hs), ipc_open(hd)
+                self._opened += [ps, pd]
+                sigs.append(ps)
+                datas.append(pd)
+        self._sig_arr = (ctypes.c_void_p * self.world)(*sigs)
+        self._data_arr = (ctypes.c_void_p * self.world)(*datas)
+        self.own_sig = sig
+        dist.barrier(group=self.cpu_group)
+
+    def _alloc(self, nbytes: int) -> int:
+        p = ctypes.c_void_p()
+        rc = self.lib.eia_ar_alloc(ctypes.byref(p), ctypes.c_long(nbytes))
+        if rc != 0:
+            raise RuntimeError(f"eia_ar_alloc({nbytes}) failed ({rc})")
+        self._own.append(p.value)
+        return p.value
 
     def should_use(self, x: torch.Tensor) -> bool:
         n = x.numel() * x.element_size()
         return (x.is_cuda and x.dtype == torch.bfloat16 and x.is_contiguous() and n <= self.max_bytes
-                and n % 16 == 0)
+                and x.numel() % 8 == 0)
 
-    def all_reduce(self, x: torch.Tensor) -> torch.Tensor:
+    def all_reduce(self, x: torch.Tensor, out: Optional[torch.Tensor] = None,
+                   kind: Optional[int] = None) -> torch.Tensor:
+        """In place by default (out = x)."""
+        out = x if out is None else out
         n = x.numel()
-        fn = self.lib.eia_ar_oneshot if n * 2 <= self.oneshot_max else self.lib.eia_ar_twoshot
+        if kind is None:
+            kind = 0 if n * 2 <= self.oneshot_max else 1
         st = torch.cuda.current_stream().cuda_stream
-        rc = fn(x.data_ptr(), x.data_ptr(), self.peer_ptrs.data_ptr(), self.epoch.data_ptr(),
-                self.rank, self.world, n, self.max_bytes, 0, st)
+        rc = self.lib.eia_ar_run(ctypes.cast(self._sig_arr, ctypes.c_void_p),
+                                 ctypes.cast(self._data_arr, ctypes.c_void_p), self.rank,
+                                 self.world, x.data_ptr(), out.data_ptr(), n, self.max_bytes, kind,
+                                 self.nblocks, st)
         _native.check(rc, "custom_allreduce")
-        return x
+        return out
+
+    def error_flag(self) -> int:
+        v = ctypes.c_int(0)
+        _native.check(self.lib.eia_ar_read_err(ctypes.c_void_p(self.own_sig), ctypes.byref(v)),
+                      "ar_read_err")
+        return v.value
+
+    def close(self) -> None:
+        hip = _hiprt()
+        for p in self._opened:
+            hip.hipIpcCloseMemHandle(ctypes.c_void_p(p))
+        for p in self._own:
+            self.lib.eia_ar_free(ctypes.c_void_p(p))
+        self._opened, self._own = [], []
 
 
 def init_custom_allreduce(max_bytes: int) -> Optional[CustomAllReduce]:
     if state.tp_size() == 1 or not torch.cuda.is_available():
-        return None
-    if not hasattr(_native.kernels(), "eia_ar_oneshot"):
         return None
     if state.tp_size() > CustomAllReduce.MAX_RANKS:
         return None

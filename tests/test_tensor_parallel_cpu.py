@@ -1,0 +1,59 @@
+"""Tensor / expert parallelism on the CPU path: one process per rank over gloo (the
+RCCL-over-xGMI code path with the CPU backend), driver + spawned worker through the
+native shm ring.  TP=2 (and EP=2 for MoE) must reproduce the TP=1 greedy tokens from the
+same safetensors checkpoint -- the weight loaders shard the full tensors per rank."""
+
+import json
+
+import pytest
+import torch
+
+from enterprise_inference_amd.config import (CacheConfig, EngineConfig, ModelConfig,
+                                             ParallelConfig, SchedulerConfig)
+from enterprise_inference_amd.engine.llm_engine import LLMEngine
+from enterprise_inference_amd.engine.sampling_params import SamplingParams
+from enterprise_inference_amd.models.catalog import tiny_config
+
+
+def _ckpt(tmp_path, d):
+    import transformers
+    from safetensors.torch import save_file
+    arch = d["architectures"][0]
+    cfg_cls = {"LlamaForCausalLM": "LlamaConfig", "MixtralForCausalLM": "MixtralConfig",
+               "Qwen2ForCausalLM": "Qwen2Config"}[arch]
+    hc = getattr(transformers, cfg_cls)(**{k: v for k, v in d.items() if k != "architectures"})
+    torch.manual_seed(0)
+    hf = getattr(transformers, arch)(hc).eval()
+    sd = {k: v.contiguous() for k, v in hf.state_dict().items()}
+    save_file(sd, str(tmp_path / "model.safetensors"))
+    (tmp_path / "config.json").write_text(json.dumps(d))
+    return str(tmp_path)
+
+
+def _run(path, d, tp, ep=False):
+    cfg = EngineConfig(model=ModelConfig.from_hf_dict(d), model_path=path,
+                       cache=CacheConfig(block_size=16, num_gpu_blocks=64),
+                       scheduler=SchedulerConfig(max_num_seqs=4, max_num_batched_tokens=40,
+                                                 max_model_len=256),
+                       parallel=ParallelConfig(tensor_parallel_size=tp, enable_expert_parallel=ep),
+                       device="cpu", dtype=torch.float32)
+    eng = LLMEngine(cfg)
+    try:
+        prompts = [[5, 6, 7, 8, 9, 10] * 8, [11, 12, 13], list(range(40, 90))]
+        outs = eng.generate(prompt_token_ids=prompts,
+                            params=SamplingParams(max_tokens=6, temperature=0, ignore_eos=True))
+        return [o.outputs[0].token_ids for o in outs]
+    finally:
+        eng.shutdown()
+        from enterprise_inference_amd.parallel import state
+        state.destroy_distributed()
+
+
+@pytest.mark.parametrize("arch,ep", [("LlamaForCausalLM", False), ("Qwen2ForCausalLM", False),
+                                     ("MixtralForCausalLM", False), ("MixtralForCausalLM", True)])
+def test_tp2_matches_tp1(tmp_path, arch, ep):
+    d = tiny_config(arch)
+    path = _ckpt(tmp_path, d)
+    ref = _run(path, d, 1)
+    got = _run(path, d, 2, ep)
+    assert got == ref
