@@ -1,0 +1,8 @@
+{{- define "teirerank.fullname" -}}
+{{- if contains .Chart.Name .Release.Name -}}{{ .Release.Name | trunc 63 | trimSuffix "-" }}
+{{- else -}}{{ printf "%s-%s" .Release.Name .Chart.Name | trunc 63 | trimSuffix "-" }}{{- end -}}
+{{- end -}}
+{{- define "teirerank.prefix" -}}
+{{- $last := .Values.RERANK_MODEL_ID | splitList "/" | last -}}
+{{- if .Values.accelDevice -}}{{ $last }}{{- else -}}{{ $last }}-teirerankcpu{{- end -}}
+{{- end -}}
