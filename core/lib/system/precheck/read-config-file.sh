@@ -58,8 +58,9 @@ read_config_file() {
 normalise_platform() {
     case "${cpu_or_gpu,,}" in
         c|cpu|xeon|epyc) cpu_or_gpu="c"; gpu_platform="cpu"; deploy_amd_gpu_operator="no" ;;
-        g|gpu|amd|mi355x) cpu_or_gpu="g"; gpu_platform="mi355x"; deploy_amd_gpu_operator="${deploy_amd_gpu_operator:-yes}" ;;
-        mi300x|mi325x) cpu_or_gpu="g"; gpu_platform="${cpu_or_gpu,,}"; deploy_amd_gpu_operator="${deploy_amd_gpu_operator:-yes}" ;;
+        g|gpu|amd) cpu_or_gpu="g"; gpu_platform="${gpu_platform:-mi355x}"; deploy_amd_gpu_operator="${deploy_amd_gpu_operator:-yes}" ;;
+        mi355x) cpu_or_gpu="g"; gpu_platform="mi355x"; deploy_amd_gpu_operator="${deploy_amd_gpu_operator:-yes}" ;;
+        mi300x|mi325x) gpu_platform="${cpu_or_gpu,,}"; cpu_or_gpu="g"; deploy_amd_gpu_operator="${deploy_amd_gpu_operator:-yes}" ;;
         gaudi2|gaudi3)
             echo "cpu_or_gpu=${cpu_or_gpu}: Intel Gaudi is not supported by this stack; use mi355x" >&2
             return 1 ;;

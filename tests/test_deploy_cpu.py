@@ -1,0 +1,106 @@
+"""Deployment layer checks (SURVEY §4 deploy tests): YAML validity of charts/playbooks/inventory,
+model catalog consistency with the MI355X Helm values, and the bash libs (model selection,
+config parsing, tag building) exercised through bash."""
+
+from __future__ import annotations
+
+import glob
+import os
+import shutil
+import subprocess
+
+import pytest
+import yaml
+
+ROOT = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "core")
+CATALOG = os.path.join(ROOT, "inventory/metadata/vars/model_catalog.yml")
+
+pytestmark = pytest.mark.skipif(shutil.which("bash") is None, reason="bash missing")
+
+
+def _bash(script: str, **env) -> subprocess.CompletedProcess:
+    e = dict(os.environ, CORE_DIR=ROOT, model_catalog_file=CATALOG, **env)
+    pre = (f'source "{ROOT}/lib/models/model-catalog.sh"; '
+           f'source "{ROOT}/lib/models/model-selection.sh"; '
+           f'source "{ROOT}/lib/models/install-model.sh"; '
+           f'source "{ROOT}/lib/system/precheck/read-config-file.sh"; ')
+    return subprocess.run(["bash", "-c", pre + script], capture_output=True, text=True, env=e,
+                          timeout=60)
+
+
+def test_all_yaml_parses():
+    files = [f for f in glob.glob(ROOT + "/**/*.y*ml", recursive=True) if "/templates/" not in f]
+    assert len(files) > 30
+    for f in files:
+        list(yaml.safe_load_all(open(f)))
+
+
+def test_all_shell_scripts_syntax():
+    for f in glob.glob(ROOT + "/**/*.sh", recursive=True):
+        r = subprocess.run(["bash", "-n", f], capture_output=True, text=True)
+        assert r.returncode == 0, (f, r.stderr)
+
+
+def test_catalog_consistent_with_values():
+    cat = yaml.safe_load(open(CATALOG))["model_catalog"]
+    nums = [m["number"] for m in cat]
+    assert len(set(nums)) == len(nums)
+    assert len({m["release"] for m in cat}) == len(cat)
+    vals = yaml.safe_load(open(os.path.join(ROOT, "helm-charts/vllm/mi355x-values.yaml")))
+    cfgs = vals["modelConfigs"]
+    for m in cat:
+        assert m["chart"] in ("vllm", "tei", "teirerank")
+        assert m["platform"] in ("gpu", "cpu")
+        if m["chart"] == "vllm" and m["platform"] == "gpu":
+            assert m["model_id"] in cfgs, m["model_id"]
+            assert 1 <= m["tensor_parallel_size"] <= 8
+    # the flagship serving config runs one MI355X per Llama-3.1-8B replica
+    assert next(m for m in cat if m["name"] == "llama-8b")["tensor_parallel_size"] == 1
+
+
+def test_catalog_models_resolve_in_framework():
+    """Every GPU LLM in the catalog maps to a model class this framework implements."""
+    from enterprise_inference_amd.models import catalog as mc
+    cat = yaml.safe_load(open(CATALOG))["model_catalog"]
+    for m in cat:
+        if m["chart"] != "vllm":
+            continue
+        assert mc.get_preset(m["model_id"])["architectures"], m["model_id"]
+
+
+def test_get_model_names_gpu_and_cpu():
+    r = _bash("get_model_names", models="1,2", cpu_or_gpu="g")
+    assert r.returncode == 0, r.stderr
+    assert r.stdout.split() == ["llama-8b", "llama-70b"]
+    r = _bash("get_model_names", models="1", cpu_or_gpu="c")
+    assert r.returncode != 0 and "GPU model identifier" in r.stderr
+    r = _bash("get_model_names", models="x", cpu_or_gpu="g")
+    assert r.returncode != 0 and "invalid" in r.stderr
+    r = _bash("get_model_names", models="999", cpu_or_gpu="g")
+    assert r.returncode != 0 and "unknown" in r.stderr
+
+
+def test_build_model_tags():
+    r = _bash("build_model_tags install", model_name_list="llama-8b llama-70b",
+              deploy_genai_gateway="yes", deploy_keycloak="no", huggingface_model_deployment_name="")
+    assert r.stdout.strip() == "install-llama-8b,install-llama-70b,install-genai-gateway"
+    r = _bash("build_model_tags uninstall", model_name_list="llama-8b",
+              deploy_genai_gateway="yes", huggingface_model_deployment_name="my-model")
+    assert r.stdout.strip() == "uninstall-llama-8b,uninstall-my-model"
+
+
+def test_read_config_file_and_platform(tmp_path):
+    cfg = tmp_path / "inference-config.cfg"
+    cfg.write_text("cluster_url=api.example.com\ncpu_or_gpu=mi355x  # comment\n"
+                   "deploy_keycloak_apisix=on\ndeploy_observability=off\n")
+    r = _bash(f'read_config_file "{cfg}" && '
+              'echo "$cluster_url|$cpu_or_gpu|$gpu_platform|$deploy_observability"')
+    assert r.returncode == 0, r.stderr
+    assert r.stdout.strip().splitlines()[-1] == "api.example.com|g|mi355x|no"
+    cfg.write_text("cpu_or_gpu=gaudi3\n")
+    r = _bash(f'read_config_file "{cfg}" && normalise_platform')
+    assert r.returncode != 0
+    cfg.write_text("cpu_or_gpu=mi300x\n")
+    r = _bash(f'read_config_file "{cfg}" && normalise_platform && echo "$cpu_or_gpu $gpu_platform"')
+    assert r.returncode == 0, r.stderr
+    assert r.stdout.strip().splitlines()[-1] == "g mi300x"
