@@ -32,57 +32,60 @@ EIA_DEV void wave_acc_init(WaveAcc<D>& a) {
   a.l = 0.f;
 }
 
-// Process tokens [tb, tb+32) of one sequence for one wave.
+// K/V fragments of one 32-token unit.  Token permutation: S^T tile 0 row rho holds token
+// 8*(rho>>2) + (rho&3), tile 1 row rho token 8*(rho>>2) + 4 + (rho&3), so after the QK MFMAs
+// lane group g owns tokens 8g..8g+7 (4 from each tile, in order) -- exactly the P^T B operand
+// of the PV MFMA -- and the matching V^T A operand is ONE 16-B load of 8 consecutive tokens
+// from the dim-major V cache (instead of two 8-B loads).  Lanes resolve their own block, so
+// any block size that is a multiple of 16 works.
+template <int D>
+struct KVFrag {
+  bf16x8 k0[D / 32], k1[D / 32];
+  bf16x8 v[D / 16];
+};
+
+template <int D>
+EIA_DEV void load_unit(KVFrag<D>& f, const bf16_t* __restrict__ kc, const bf16_t* __restrict__ vc,
+                       const int* __restrict__ bt, int tb, int L, int kvh, int Hkv, int bs) {
+  const int lane = threadIdx.x & 63;
+  const int c = lane & 15, g = lane >> 4;
+  const int tk0 = tb + 8 * (c >> 2) + (c & 3), tk1 = tk0 + 4;
+  const int tv = tb + 8 * g;
+  const int lastb = (L - 1) / bs;   // tokens past L may lie in unallocated table slots: clamp
+  const long hk = (long)bs * D;
+  const bf16_t* kp0 = kc + ((long)bt[min(tk0 / bs, lastb)] * Hkv + kvh) * hk + (long)(tk0 % bs) * D + 8 * g;
+  const bf16_t* kp1 = kc + ((long)bt[min(tk1 / bs, lastb)] * Hkv + kvh) * hk + (long)(tk1 % bs) * D + 8 * g;
+  const bf16_t* vp = vc + ((long)bt[min(tv / bs, lastb)] * Hkv + kvh) * hk + (tv % bs);
+#pragma unroll
+  for (int s = 0; s < D / 32; ++s) {
+    f.k0[s] = *reinterpret_cast<const bf16x8*>(kp0 + 32 * s);
+    f.k1[s] = *reinterpret_cast<const bf16x8*>(kp1 + 32 * s);
+  }
+#pragma unroll
+  for (int dt = 0; dt < D / 16; ++dt)
+    f.v[dt] = *reinterpret_cast<const bf16x8*>(vp + (long)(16 * dt + c) * bs);
+}
+
+// Tokens [tb, tb+32) of one sequence for one wave (fragments already loaded).
 //   qf      : Q^T B-operand fragments (pre-loaded)
 //   q_abs   : absolute position of this lane's query column (INT_MAX: no causal mask)
 //   kv_lo   : first token this lane's column may attend to (sliding window / chunk)
+// Tokens >= L inside the last block hold finite stale/zero data and are masked to p = 0.
 template <int D>
-EIA_DEV void attn_unit(WaveAcc<D>& acc, const bf16x8 (&qf)[D / 32],
-                       const bf16_t* __restrict__ kc, const bf16_t* __restrict__ vc,
-                       const int* __restrict__ bt, int tb, int L, int kvh, int Hkv, int bs,
-                       float scale_log2, int q_abs, int kv_lo) {
+EIA_DEV void compute_unit(WaveAcc<D>& acc, const bf16x8 (&qf)[D / 32], const KVFrag<D>& f, int tb,
+                          int L, float scale_log2, int q_abs, int kv_lo) {
   const int lane = threadIdx.x & 63;
-  const int c = lane & 15, g = lane >> 4;
-  const bool has1 = (tb + 16) < L;
-  const long head_stride_k = (long)bs * D;
-  const int blk0 = bt[tb / bs];
-  const int blk1 = has1 ? bt[(tb + 16) / bs] : blk0;
-  const int offt0 = tb % bs;
-  const int offt1 = has1 ? (tb + 16) % bs : offt0;
-
+  const int g = lane >> 4;
   f32x4 s0 = {0.f, 0.f, 0.f, 0.f}, s1 = {0.f, 0.f, 0.f, 0.f};
-  {
-    const bf16_t* kp0 = kc + ((long)blk0 * Hkv + kvh) * head_stride_k + (long)(offt0 + c) * D + 8 * g;
-    const bf16_t* kp1 = kc + ((long)blk1 * Hkv + kvh) * head_stride_k + (long)(offt1 + c) * D + 8 * g;
-    bf16x8 ka[D / 32], kb[D / 32];
 #pragma unroll
-    for (int s = 0; s < D / 32; ++s) ka[s] = *reinterpret_cast<const bf16x8*>(kp0 + 32 * s);
-    if (has1) {
-#pragma unroll
-      for (int s = 0; s < D / 32; ++s) kb[s] = *reinterpret_cast<const bf16x8*>(kp1 + 32 * s);
-    }
-#pragma unroll
-    for (int s = 0; s < D / 32; ++s) s0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ka[s], qf[s], s0, 0, 0, 0);
-    if (has1) {
-#pragma unroll
-      for (int s = 0; s < D / 32; ++s) s1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kb[s], qf[s], s1, 0, 0, 0);
-    }
+  for (int s = 0; s < D / 32; ++s) {
+    s0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(f.k0[s], qf[s], s0, 0, 0, 0);
+    s1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(f.k1[s], qf[s], s1, 0, 0, 0);
   }
-  // issue the V loads early (independent of the softmax)
-  const bf16_t* vp0 = vc + ((long)blk0 * Hkv + kvh) * (long)D * bs + offt0 + 4 * g;
-  const bf16_t* vp1 = vc + ((long)blk1 * Hkv + kvh) * (long)D * bs + offt1 + 4 * g;
-  bf16x4 vlo[D / 16], vhi[D / 16];
-#pragma unroll
-  for (int dt = 0; dt < D / 16; ++dt) {
-    const long d = 16 * dt + c;
-    vlo[dt] = *reinterpret_cast<const bf16x4*>(vp0 + d * bs);
-    vhi[dt] = *reinterpret_cast<const bf16x4*>(vp1 + d * bs);
-  }
-
   float v[8];
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
-    const int t0 = tb + 4 * g + i, t1 = tb + 16 + 4 * g + i;
+    const int t0 = tb + 8 * g + i, t1 = t0 + 4;
     const bool ok0 = (t0 < L) && (t0 <= q_abs) && (t0 >= kv_lo);
     const bool ok1 = (t1 < L) && (t1 <= q_abs) && (t1 >= kv_lo);
     v[i] = ok0 ? s0[i] * scale_log2 : NEG_INF;
@@ -112,26 +115,58 @@ EIA_DEV void attn_unit(WaveAcc<D>& acc, const bf16x8 (&qf)[D / 32],
     for (int dt = 0; dt < D / 16; ++dt) acc.o[dt] *= alpha;
   }
 #pragma unroll
-  for (int dt = 0; dt < D / 16; ++dt) {
-    bf16x8 a;
-    a[0] = vlo[dt][0]; a[1] = vlo[dt][1]; a[2] = vlo[dt][2]; a[3] = vlo[dt][3];
-    a[4] = vhi[dt][0]; a[5] = vhi[dt][1]; a[6] = vhi[dt][2]; a[7] = vhi[dt][3];
-    acc.o[dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, pb, acc.o[dt], 0, 0, 0);
+  for (int dt = 0; dt < D / 16; ++dt)
+    acc.o[dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(f.v[dt], pb, acc.o[dt], 0, 0, 0);
+}
+
+template <int D>
+EIA_DEV void attn_unit(WaveAcc<D>& acc, const bf16x8 (&qf)[D / 32],
+                       const bf16_t* __restrict__ kc, const bf16_t* __restrict__ vc,
+                       const int* __restrict__ bt, int tb, int L, int kvh, int Hkv, int bs,
+                       float scale_log2, int q_abs, int kv_lo) {
+  KVFrag<D> f;
+  load_unit<D>(f, kc, vc, bt, tb, L, kvh, Hkv, bs);
+  compute_unit<D>(acc, qf, f, tb, L, scale_log2, q_abs, kv_lo);
+}
+
+// Units ub+w, ub+w+4, ... (< ue) of one wave with the next unit's K/V in flight while the
+// current one is multiplied (two named fragment sets; the prefetch index is clamped instead
+// of predicated so the vmcnt accounting stays static).
+template <int D>
+EIA_DEV void attn_units_pipelined(WaveAcc<D>& acc, const bf16x8 (&qf)[D / 32],
+                                  const bf16_t* __restrict__ kc, const bf16_t* __restrict__ vc,
+                                  const int* __restrict__ bt, int ub, int ue, int w, int L, int kvh,
+                                  int Hkv, int bs, float scale_log2, int kv_lo) {
+  int u = ub + w;
+  if (u >= ue) return;
+  KVFrag<D> fa, fb;
+  load_unit<D>(fa, kc, vc, bt, 32 * u, L, kvh, Hkv, bs);
+  for (;;) {
+    load_unit<D>(fb, kc, vc, bt, 32 * min(u + 4, ue - 1), L, kvh, Hkv, bs);
+    compute_unit<D>(acc, qf, fa, 32 * u, L, scale_log2, 0x7fffffff, kv_lo);
+    u += 4;
+    if (u >= ue) break;
+    load_unit<D>(fa, kc, vc, bt, 32 * min(u + 4, ue - 1), L, kvh, Hkv, bs);
+    compute_unit<D>(acc, qf, fb, 32 * u, L, scale_log2, 0x7fffffff, kv_lo);
+    u += 4;
+    if (u >= ue) break;
   }
 }
 
 // ---------------------------------------------------------------------------------- decode
 
 template <int D>
-__global__ void __launch_bounds__(256)
+__global__ void __launch_bounds__(256, D <= 128 ? 2 : 1)
 paged_decode_kernel(const bf16_t* __restrict__ q, long q_stride,
                     const bf16_t* __restrict__ kc, const bf16_t* __restrict__ vc,
                     const int* __restrict__ block_tables, int bt_stride,
                     const int* __restrict__ seq_lens,
                     bf16_t* __restrict__ out, long out_stride,
                     float* __restrict__ part_o, float* __restrict__ part_ml,
+                    int* __restrict__ part_cnt,
                     float scale_log2, int Hq, int Hkv, int bs, int P, int NQG,
                     int sliding_window, int chunk_size) {
+  __shared__ int s_last;
   __shared__ float sm[4][16];
   __shared__ float sl[4][16];
   __shared__ float so[4][D][17];
@@ -170,8 +205,7 @@ paged_decode_kernel(const bf16_t* __restrict__ q, long q_stride,
   const int U = (L + 31) / 32 - U0;
   const int ub = U0 + (int)(((long)p * U) / P), ue = U0 + (int)(((long)(p + 1) * U) / P);
   const int* bt = block_tables + (long)b * bt_stride;
-  for (int u = ub + w; u < ue; u += 4)
-    attn_unit<D>(acc, qf, kc, vc, bt, 32 * u, L, kvh, Hkv, bs, scale_log2, 0x7fffffff, kv_lo);
+  attn_units_pipelined<D>(acc, qf, kc, vc, bt, ub, ue, w, L, kvh, Hkv, bs, scale_log2, kv_lo);
 
   float lt = acc.l;
   lt += __shfl_xor(lt, 16, 64);
@@ -207,6 +241,35 @@ paged_decode_kernel(const bf16_t* __restrict__ q, long q_stride,
       if (d == 0) { part_ml[2 * pi] = M; part_ml[2 * pi + 1] = Ls; }
     }
   }
+  if (P == 1 || part_cnt == nullptr) return;
+  // Fused partition merge: the last of the P workgroups of this (b, kv head, q group) merges
+  // the partials (no separate reduce launch).  Agent-scope fences write back / invalidate the
+  // per-XCD L2s so partials written on another XCD are visible; the last arrival resets the
+  // counter, keeping the kernel replayable inside a HIP graph.
+  __threadfence();
+  __syncthreads();
+  int* cnt = part_cnt + ((long)b * Hkv + kvh) * NQG + qg;
+  if (threadIdx.x == 0) s_last = (atomicAdd(cnt, 1) == P - 1);
+  __syncthreads();
+  if (!s_last) return;
+  __threadfence();
+  for (int idx = threadIdx.x; idx < 16 * D; idx += blockDim.x) {
+    const int cq = idx / D, d = idx % D;
+    if (cq >= nq) continue;
+    const long base = ((long)b * Hq + hq0 + cq) * P;
+    float M = NEG_INF;
+    for (int pp = 0; pp < P; ++pp) M = fmaxf(M, __builtin_nontemporal_load(part_ml + 2 * (base + pp)));
+    float Ls = 0.f, O = 0.f;
+    if (M != NEG_INF) {
+      for (int pp = 0; pp < P; ++pp) {
+        const float f = exp2f(__builtin_nontemporal_load(part_ml + 2 * (base + pp)) - M);
+        Ls += __builtin_nontemporal_load(part_ml + 2 * (base + pp) + 1) * f;
+        O += __builtin_nontemporal_load(part_o + (base + pp) * D + d) * f;
+      }
+    }
+    out[(long)b * out_stride + (long)(hq0 + cq) * D + d] = f2bf(Ls > 0.f ? O / Ls : 0.f);
+  }
+  if (threadIdx.x == 0) *cnt = 0;
 }
 
 template <int D>
@@ -304,7 +367,7 @@ paged_prefill_kernel(const bf16_t* __restrict__ q, long q_stride,
 EIA_API int eia_paged_decode(const void* q, long q_stride, const void* k_cache, const void* v_cache,
                              const int* block_tables, int bt_stride, const int* seq_lens,
                              void* out, long out_stride, float* part_o, float* part_ml,
-                             float scale, int B, int Hq, int Hkv, int D, int bs, int P,
+                             int* part_cnt, float scale, int B, int Hq, int Hkv, int D, int bs, int P,
                              int sliding_window, int chunk_size, hipStream_t st) {
   if (B < 0 || Hkv <= 0 || Hq % Hkv != 0 || bs % 16 != 0 || P < 1) return EIA_BAD_SHAPE;
   if (P > 1 && (part_o == nullptr || part_ml == nullptr)) return EIA_BAD_SHAPE;
@@ -316,9 +379,9 @@ EIA_API int eia_paged_decode(const void* q, long q_stride, const void* k_cache, 
 #define DEC(DD)                                                                             \
   hipLaunchKernelGGL((paged_decode_kernel<DD>), grid, block, 0, st, (const bf16_t*)q, q_stride, \
                      (const bf16_t*)k_cache, (const bf16_t*)v_cache, block_tables, bt_stride, \
-                     seq_lens, (bf16_t*)out, out_stride, part_o, part_ml, sl2, Hq, Hkv, bs, P, NQG, \
-                     sliding_window, chunk_size);                                            \
-  if (P > 1)                                                                                \
+                     seq_lens, (bf16_t*)out, out_stride, part_o, part_ml, part_cnt, sl2, Hq, Hkv, bs, \
+                     P, NQG, sliding_window, chunk_size);                                    \
+  if (P > 1 && part_cnt == nullptr)                                                         \
     hipLaunchKernelGGL((paged_decode_reduce_kernel<DD>), dim3(B, Hq), dim3(DD < 256 ? DD : 256), 0, st, \
                        part_o, part_ml, (bf16_t*)out, out_stride, Hq, P);
   switch (D) {

@@ -8,10 +8,10 @@
 // targets the ~6 TB/s HBM ceiling:
 //
 //  * W is the MFMA A operand (rows = n), X the B operand (columns = m), with
-//    v_mfma_f32_16x16x32_bf16.  Within a 128-deep K "super-step" lane (r, g)
-//    of a wave reads W[n0 + r][kb + 32g .. kb + 32g + 32) -- 64 contiguous bytes
-//    per row as four 16-B loads -- and MFMA step s consumes elements 8s..8s+7
-//    of that run.  Any k permutation is legal as long as X uses the same one,
+//    v_mfma_f32_16x16x32_bf16.  Within a 128-deep K "super-step" the four lane
+//    groups g of a row read one contiguous 64-B run per load instruction (KLANE /
+//    KSTEP below) and MFMA step s consumes the s-th run.  Any k permutation is
+//    legal as long as X uses the same one,
 //    so W is streamed in its native layout with full-row coalescing and no
 //    re-layout (prefill keeps using the same tensor through hipBLASLt).
 //  * X (tiny, L2-resident) is staged per 256-deep K chunk into LDS (register
@@ -34,10 +34,19 @@ namespace {
 constexpr int KC = 256;             // K chunk per pipeline stage
 constexpr int XPAD = 8;             // LDS row padding (elements)
 constexpr int XLD = KC + XPAD;      // LDS row stride (elements)
+// k permutation inside a 128-deep super-step: lane group g, MFMA step s, element j covers
+// k = KLANE*g + KSTEP*s + j.  KLANE = 8 / KSTEP = 32 makes each W load instruction read one
+// contiguous 64-B run per row (4 lanes x 16 B; the 4 steps walk the row), i.e. 16 half cache
+// lines per instruction instead of 32 lines touched at 64-B stride (KLANE 32 / KSTEP 8).
+#ifndef EIA_GEMM_KLANE
+#define EIA_GEMM_KLANE 8
+#endif
+constexpr int KLANE = EIA_GEMM_KLANE;
+constexpr int KSTEP = KLANE == 8 ? 32 : 8;
 
 enum Mode : int { MODE_BF16 = 0, MODE_F32_SPLIT = 1, MODE_SWIGLU = 2 };
 
-EIA_DEV float silu(float x) { return x / (1.f + __expf(-x)); }
+EIA_DEV float silu(float x) { return __fdividef(x, 1.f + __expf(-x)); }
 
 // Weight-stream load.  Non-temporal loads (EIA_GEMM_NT) measured 1.7x SLOWER on this box for
 // back-to-back decode replays (guide: MI355X_MICROARCH "nt-weights" -- nt gives up what a
@@ -55,7 +64,8 @@ EIA_DEV bf16x8 ld_w(const bf16_t* p) {
 // rows are [offs[e], offs[e+1]) of the expert-sorted token list, X rows are gathered
 // through row_idx (nullptr = identity) and outputs land in sorted order; experts with
 // more than 16*MT rows loop over row chunks (weights re-streamed per chunk).
-template <int MT, int NT, int WAVES, bool GROUPED>
+// S: W pipeline stages (register sets); S-1 chunks of weights stay in flight.
+template <int MT, int NT, int WAVES, int S, bool GROUPED>
 __global__ void __launch_bounds__(WAVES * 64)
 gemm_skinny_kernel(const bf16_t* __restrict__ X, long ldx, const bf16_t* __restrict__ W, long ldw,
                    const bf16_t* __restrict__ bias, void* __restrict__ out, long ldo, int M, int N,
@@ -84,12 +94,12 @@ gemm_skinny_kernel(const bf16_t* __restrict__ X, long ldx, const bf16_t* __restr
   int nbase;
   if (NT == 2 && mode == MODE_SWIGLU) {
     nbase = blockIdx.x * (WAVES * 16) + wave * 16;      // output column block
-    wp[0] = W + (long)(nbase + r) * ldw + k0 + 32 * g;
-    wp[NT - 1] = W + (long)(inter + nbase + r) * ldw + k0 + 32 * g;
+    wp[0] = W + (long)(nbase + r) * ldw + k0 + KLANE * g;
+    wp[NT - 1] = W + (long)(inter + nbase + r) * ldw + k0 + KLANE * g;
   } else {
     nbase = blockIdx.x * (WAVES * NT * 16) + wave * (NT * 16);
 #pragma unroll
-    for (int t = 0; t < NT; ++t) wp[t] = W + (long)(nbase + 16 * t + r) * ldw + k0 + 32 * g;
+    for (int t = 0; t < NT; ++t) wp[t] = W + (long)(nbase + 16 * t + r) * ldw + k0 + KLANE * g;
   }
 
   constexpr int XV = MT * 16 * (KC / 8);                // 16-B vectors per X chunk
@@ -100,12 +110,12 @@ gemm_skinny_kernel(const bf16_t* __restrict__ X, long ldx, const bf16_t* __restr
     const int Mc = min(MT * 16, Mtot - m0);
     // X row (in the caller's X) of local row `row` of this pass; padded rows clamp to the last
     // valid one and are never stored
-    auto xrow_of = [&](int row) -> long {
+    auto xrow_of = [&](int row) -> int {
       const int lr = mbase + m0 + (row < Mc ? row : Mc - 1);
-      if constexpr (GROUPED) return row_idx != nullptr ? (long)row_idx[lr] : (long)lr;
-      return (long)lr;
+      if constexpr (GROUPED) return row_idx != nullptr ? row_idx[lr] : lr;
+      return lr;
     };
-    long xrows[XPT];
+    int xrows[XPT];   // 32-bit: 64-bit row offsets cost 2*XPT live VGPRs
 #pragma unroll
     for (int j = 0; j < XPT; ++j) xrows[j] = xrow_of((threadIdx.x + j * WAVES * 64) / (KC / 8));
 
@@ -114,7 +124,7 @@ gemm_skinny_kernel(const bf16_t* __restrict__ X, long ldx, const bf16_t* __restr
       for (int j = 0; j < XPT; ++j) {
         const int v = threadIdx.x + j * WAVES * 64;
         const int col = (v % (KC / 8)) * 8;
-        xr[j] = *reinterpret_cast<const bf16x8*>(X + xrows[j] * ldx + k0 + c * KC + col);
+        xr[j] = *reinterpret_cast<const bf16x8*>(X + (long)xrows[j] * ldx + k0 + c * KC + col);
       }
     };
     auto store_x = [&](int buf, const bf16x8 (&xr)[XPT]) {
@@ -133,7 +143,7 @@ gemm_skinny_kernel(const bf16_t* __restrict__ X, long ldx, const bf16_t* __restr
 #pragma unroll
         for (int ss = 0; ss < 2; ++ss)
 #pragma unroll
-          for (int s = 0; s < 4; ++s) w[t][ss * 4 + s] = ld_w(wp[t] + c * KC + 128 * ss + 8 * s);
+          for (int s = 0; s < 4; ++s) w[t][ss * 4 + s] = ld_w(wp[t] + c * KC + 128 * ss + KSTEP * s);
     };
 
     f32x4 acc[NT][MT];
@@ -142,54 +152,73 @@ gemm_skinny_kernel(const bf16_t* __restrict__ X, long ldx, const bf16_t* __restr
 #pragma unroll
       for (int m = 0; m < MT; ++m) acc[t][m] = (f32x4){0.f, 0.f, 0.f, 0.f};
 
+    // X fragments are read from LDS one MFMA step ahead (two named sets); the sched_barriers
+    // stop hipcc from hoisting all 8 steps' ds_reads (MT*32 VGPRs) to the top, which left no
+    // registers for deeper weight pipelines.
     auto compute = [&](int buf, const bf16x8 (&w)[NT][8]) {
-      const bf16_t* xb = xs + (buf * MT * 16 + r) * XLD + 32 * g;
-#pragma unroll
-      for (int st = 0; st < 8; ++st) {
-        bf16x8 xf[MT];
+      const bf16_t* xb = xs + (buf * MT * 16 + r) * XLD + KLANE * g;
+      auto ldx = [&](int st, bf16x8 (&xf)[MT]) {
 #pragma unroll
         for (int m = 0; m < MT; ++m)
-          xf[m] = *reinterpret_cast<const bf16x8*>(xb + m * 16 * XLD + 128 * (st >> 2) + 8 * (st & 3));
+          xf[m] = *reinterpret_cast<const bf16x8*>(xb + m * 16 * XLD + 128 * (st >> 2) + KSTEP * (st & 3));
+      };
+      auto mma = [&](int st, const bf16x8 (&xf)[MT]) {
 #pragma unroll
         for (int m = 0; m < MT; ++m)
 #pragma unroll
           for (int t = 0; t < NT; ++t)
             acc[t][m] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w[t][st], xf[m], acc[t][m], 0, 0, 0);
+      };
+      bf16x8 xa[MT], xc[MT];
+      ldx(0, xa);
+#pragma unroll
+      for (int st = 0; st < 8; st += 2) {
+        ldx(st + 1, xc);
+        __builtin_amdgcn_sched_barrier(0);
+        mma(st, xa);
+        __builtin_amdgcn_sched_barrier(0);
+        if (st + 2 < 8) ldx(st + 2, xa);
+        __builtin_amdgcn_sched_barrier(0);
+        mma(st + 1, xc);
+        __builtin_amdgcn_sched_barrier(0);
       }
     };
 
-    // Pipeline: two named W register sets (no copies: guide rule 20); each phase
-    // issues X(c+1) then W(c+1) -- pinned ahead of the MFMAs with sched_barrier,
-    // since hipcc otherwise sinks the X loads behind the compute and waits vmcnt(0)
-    // on them -- so the in-order vmcnt wait for X before its ds_write leaves the
-    // weight prefetch in flight.  Loads are unconditional (chunk index clamped)
-    // and the loop body has no early exit, so the vmcnt accounting stays exact.
-    bf16x8 wa[NT][8], wb[NT][8];
+    // Pipeline: S W register sets (S-1 chunks of weights in flight while one is multiplied;
+    // indices are compile-time after unrolling -- no runtime-indexed register arrays, guide
+    // rule 20).  Each phase issues X(c+1) then W(c+S-1) -- pinned ahead of the MFMAs with
+    // sched_barrier, since hipcc otherwise sinks the X loads behind the compute and waits
+    // vmcnt(0) on them -- so the in-order vmcnt wait for X before its ds_write only drains
+    // W(c+1) (needed next phase anyway) and leaves W(c+2..c+S-1) in flight.  Loads are
+    // unconditional (chunk index clamped) and full groups of S phases have no early exit, so
+    // the vmcnt accounting stays exact; the <S leftover phases run once as a guarded tail.
+    bf16x8 w[S][NT][8];
     {
       bf16x8 xr[XPT];
       load_x(0, xr);
-      load_w(0, wa);
+#pragma unroll
+      for (int s = 0; s < S - 1; ++s) load_w(min(s, last), w[s]);
       store_x(0, xr);
     }
     __syncthreads();
-#define EIA_PHASE(C, WCUR, WNEXT)                 \
-    {                                             \
-      bf16x8 xr[XPT];                             \
-      load_x(min((C) + 1, last), xr);             \
-      load_w(min((C) + 1, last), WNEXT);          \
-      __builtin_amdgcn_sched_barrier(0);          \
-      compute((C) & 1, WCUR);                     \
-      __builtin_amdgcn_sched_barrier(0);          \
-      store_x(((C) + 1) & 1, xr);                 \
-      __syncthreads();                            \
-    }
+    auto phase = [&](int cc, bf16x8 (&wcur)[NT][8], bf16x8 (&wnext)[NT][8]) {
+      bf16x8 xr[XPT];
+      load_x(min(cc + 1, last), xr);
+      load_w(min(cc + S - 1, last), wnext);
+      __builtin_amdgcn_sched_barrier(0);
+      compute(cc & 1, wcur);
+      __builtin_amdgcn_sched_barrier(0);
+      store_x((cc + 1) & 1, xr);
+      __syncthreads();
+    };
     int c = 0;
-    for (; c + 2 <= nchunks; c += 2) {
-      EIA_PHASE(c, wa, wb);
-      EIA_PHASE(c + 1, wb, wa);
+    for (; c + S <= nchunks; c += S) {
+#pragma unroll
+      for (int s = 0; s < S; ++s) phase(c + s, w[s], w[(s + S - 1) % S]);
     }
-    if (c < nchunks) EIA_PHASE(c, wa, wb);
-#undef EIA_PHASE
+#pragma unroll
+    for (int s = 0; s < S - 1; ++s)
+      if (c + s < nchunks) phase(c + s, w[s], w[(s + S - 1) % S]);
 
     // epilogue: lane (r, g) holds rows n = tile_base + 4g + i, column m = 16*mt + r
     const long orow0 = mbase + m0;
@@ -300,19 +329,19 @@ splitk_add_rmsnorm_kernel(const float* __restrict__ part, int sk, int M, int H,
   }
 }
 
-template <int MT, int NT, int WAVES, bool GROUPED>
+template <int MT, int NT, int WAVES, int S, bool GROUPED>
 int launch_cfg(const bf16_t* X, long ldx, const bf16_t* W, long ldw, const bf16_t* bias, void* out,
                long ldo, int M, int N, int K, int sk, int mode, int experts, const int* offs,
                const int* row_idx, long w_estride, hipStream_t st) {
   const size_t lds = 2ull * MT * 16 * XLD * sizeof(bf16_t);
   static bool attr_set = false;   // > 64 KiB of dynamic LDS must be opted into
   if (!attr_set) {
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(gemm_skinny_kernel<MT, NT, WAVES, GROUPED>),
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(gemm_skinny_kernel<MT, NT, WAVES, S, GROUPED>),
                         hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     attr_set = true;
   }
   dim3 grid(mode == MODE_SWIGLU ? (N / 2) / (WAVES * 16) : N / (WAVES * NT * 16), sk, experts);
-  hipLaunchKernelGGL((gemm_skinny_kernel<MT, NT, WAVES, GROUPED>), grid, dim3(WAVES * 64), lds, st,
+  hipLaunchKernelGGL((gemm_skinny_kernel<MT, NT, WAVES, S, GROUPED>), grid, dim3(WAVES * 64), lds, st,
                      X, ldx, W, ldw, bias, out, ldo, M, N, K / sk, mode, N / 2, offs, row_idx,
                      w_estride);
   return (int)hipGetLastError();
@@ -322,14 +351,32 @@ template <int MT, bool GROUPED>
 int launch_mt(int cfg, const bf16_t* X, long ldx, const bf16_t* W, long ldw, const bf16_t* bias,
               void* out, long ldo, int M, int N, int K, int sk, int mode, int experts,
               const int* offs, const int* row_idx, long w_estride, hipStream_t st) {
-#define EIA_CFG(NT_, W_) \
-  return launch_cfg<MT, NT_, W_, GROUPED>(X, ldx, W, ldw, bias, out, ldo, M, N, K, sk, mode, \
-                                          experts, offs, row_idx, w_estride, st)
-  switch (cfg) {   // cfg = (NT - 1) | ((WAVES / 2 - 1) << 1)
-    case 0: EIA_CFG(1, 2);
-    case 1: EIA_CFG(2, 2);
-    case 2: EIA_CFG(1, 4);
-    default: EIA_CFG(2, 4);
+#define EIA_CFG(NT_, W_, S_) \
+  return launch_cfg<MT, NT_, W_, S_, GROUPED>(X, ldx, W, ldw, bias, out, ldo, M, N, K, sk, mode, \
+                                              experts, offs, row_idx, w_estride, st)
+  // cfg = (NT - 1) | ((WAVES / 2 - 1) << 1) | ((S - 2) << 2); grouped (MoE) uses S = 2
+  if constexpr (GROUPED) {
+    switch (cfg & 3) {
+      case 0: EIA_CFG(1, 2, 2);
+      case 1: EIA_CFG(2, 2, 2);
+      case 2: EIA_CFG(1, 4, 2);
+      default: EIA_CFG(2, 4, 2);
+    }
+  } else {
+    switch (cfg) {
+      case 0: EIA_CFG(1, 2, 2);
+      case 1: EIA_CFG(2, 2, 2);
+      case 2: EIA_CFG(1, 4, 2);
+      case 3: EIA_CFG(2, 4, 2);
+      case 4: EIA_CFG(1, 2, 3);
+      case 5: EIA_CFG(2, 2, 3);
+      case 6: EIA_CFG(1, 4, 3);
+      case 7: EIA_CFG(2, 4, 3);
+      case 8: EIA_CFG(1, 2, 4);
+      case 9: EIA_CFG(2, 2, 4);
+      case 10: EIA_CFG(1, 4, 4);
+      default: EIA_CFG(2, 4, 4);
+    }
   }
 #undef EIA_CFG
 }
@@ -356,7 +403,7 @@ int dispatch_mt(int mt, int cfg, const bf16_t* x, long ldx, const bf16_t* w, lon
 
 int check_shape(int N, int K, int sk, int mode, int cfg) {
   const int nt = (cfg & 1) ? 2 : 1, waves = (cfg & 2) ? 4 : 2;
-  if (sk < 1 || K % (sk * KC) != 0 || cfg < 0 || cfg > 3) return EIA_BAD_SHAPE;
+  if (sk < 1 || K % (sk * KC) != 0 || cfg < 0 || cfg > 11) return EIA_BAD_SHAPE;
   if (mode == MODE_SWIGLU) {
     if (nt != 2 || sk != 1 || N % 2 != 0 || (N / 2) % (waves * 16) != 0) return EIA_BAD_SHAPE;
   } else if (N % (waves * nt * 16) != 0) {
@@ -371,7 +418,8 @@ int check_shape(int N, int K, int sk, int mode, int cfg) {
 // mode 0: out bf16 [M][ldo] (+bias), sk must be 1
 // mode 1: out fp32 partial slabs [sk][M][N] (reduce with eia_splitk_reduce / _add_rmsnorm)
 // mode 2: SwiGLU: W = merged [gate; up] (N = 2I rows), out bf16 [M][ldo] = silu(gate) * up
-// cfg: bit0 -> two 16-row W tiles per wave (else one), bit1 -> 4 waves per workgroup (else 2)
+// cfg: bit0 -> two 16-row W tiles per wave (else one), bit1 -> 4 waves per workgroup (else 2),
+// bits 2-3 -> W pipeline stages - 2 (2..4)
 EIA_API int eia_gemm_skinny(const void* X, long ldx, const void* W, long ldw, const void* bias,
                             void* out, long ldo, int M, int N, int K, int sk, int mode, int cfg,
                             hipStream_t st) {

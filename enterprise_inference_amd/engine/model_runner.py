@@ -108,6 +108,9 @@ class ModelRunner:
                                   device=dev) if self.is_gpu else None
         self.part_ml = torch.empty(S * self.num_heads * pmax * 2, dtype=torch.float32,
                                    device=dev) if self.is_gpu else None
+        # arrival counters of the in-kernel partition merge (kernels leave them zeroed)
+        self.part_cnt = torch.zeros(S * self.num_heads, dtype=torch.int32,
+                                    device=dev) if self.is_gpu else None
 
     # ------------------------------------------------------------------ KV cache
     def kv_block_bytes(self) -> int:
@@ -217,7 +220,7 @@ class ModelRunner:
             num_decode=Bp, num_prefill_tokens=0, slot_mapping=d[2 * S:2 * S + Bp],
             positions=d[S:S + Bp], decode_block_tables=self.d_g_bt[:Bp * self.maxb].view(Bp, self.maxb),
             decode_seq_lens=d[3 * S:3 * S + Bp], decode_partitions=P, decode_part_o=self.part_o,
-            decode_part_ml=self.part_ml)
+            decode_part_ml=self.part_ml, decode_part_cnt=self.part_cnt)
         return d[:Bp], md
 
     def _prepare_eager(self, bm: BlockManager, out: SchedulerOutput) -> dict:
@@ -296,6 +299,7 @@ class ModelRunner:
             decode_block_tables=d[o["dbt"]:o["dbt"] + nd * mb_d].view(nd, mb_d) if nd else None,
             decode_seq_lens=d[o["dlen"]:o["dlen"] + nd] if nd else None,
             decode_partitions=plan["P"], decode_part_o=self.part_o, decode_part_ml=self.part_ml,
+            decode_part_cnt=self.part_cnt,
             prefill_block_tables=d[o["pbt"]:o["pbt"] + npf * mb_p].view(npf, mb_p) if npf else None,
             prefill_seq_lens=d[o["plen"]:o["plen"] + npf] if npf else None,
             prefill_cu_q=d[o["cu"]:o["cu"] + npf + 1] if npf else None,

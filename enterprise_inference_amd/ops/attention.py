@@ -57,6 +57,7 @@ class AttentionMetadata:
     decode_partitions: int = 1
     decode_part_o: Optional[torch.Tensor] = None
     decode_part_ml: Optional[torch.Tensor] = None
+    decode_part_cnt: Optional[torch.Tensor] = None      # zeroed int32 [Bd*Hkv*ceil(G/16)]
     # prefill part
     prefill_block_tables: Optional[torch.Tensor] = None  # [Sp, maxb] int32
     prefill_seq_lens: Optional[torch.Tensor] = None      # [Sp] int32 (context + new)
@@ -75,8 +76,13 @@ def paged_decode(q: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tensor,
                  partitions: int = 1, part_o: Optional[torch.Tensor] = None,
                  part_ml: Optional[torch.Tensor] = None,
                  out: Optional[torch.Tensor] = None, sliding_window: Optional[int] = None,
-                 chunk_size: Optional[int] = None) -> torch.Tensor:
-    """q [B, Hq, D] -> out [B, Hq, D]."""
+                 chunk_size: Optional[int] = None,
+                 part_cnt: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """q [B, Hq, D] -> out [B, Hq, D].
+
+    With ``partitions > 1`` the context is split over grid.z; ``part_cnt`` (zeroed int32,
+    >= B*Hkv*ceil(G/16) entries, left zeroed by the kernel) lets the last partition merge the
+    partials in-kernel, otherwise a separate reduce kernel runs."""
     if not (use_hip(q, k_cache) and q.dtype == torch.bfloat16):
         r = ref.paged_attention_decode(q, k_cache, v_cache, block_tables, seq_lens, scale,
                                        sliding_window, chunk_size)
@@ -95,10 +101,16 @@ def paged_decode(q: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tensor,
         need = B * Hq * partitions
         require(part_o is not None and part_o.numel() >= need * D and part_ml.numel() >= need * 2,
                 "decode workspace too small")
+        if part_cnt is not None:
+            G = Hq // Hkv
+            require(part_cnt.dtype == torch.int32 and
+                    part_cnt.numel() >= B * Hkv * ((G + 15) // 16), "decode counters too small")
     check(lib().eia_paged_decode(
         ptr(q), q.stride(0), ptr(k_cache), ptr(v_cache), ptr(block_tables), block_tables.stride(0),
         ptr(seq_lens), ptr(o), o.stride(0), ptr(part_o) if partitions > 1 else None,
-        ptr(part_ml) if partitions > 1 else None, float(scale), B, Hq, Hkv, D, bs, partitions,
+        ptr(part_ml) if partitions > 1 else None,
+        ptr(part_cnt) if (partitions > 1 and part_cnt is not None) else None,
+        float(scale), B, Hq, Hkv, D, bs, partitions,
         sliding_window or 0, chunk_size or 0, stream(q)), "paged_decode")
     return o
 
@@ -140,12 +152,14 @@ def attention(q: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tensor,
     if md.num_prefill_tokens == 0:
         return paged_decode(q[:nd], k_cache, v_cache, md.decode_block_tables, md.decode_seq_lens,
                             scale, md.decode_partitions, md.decode_part_o, md.decode_part_ml,
-                            sliding_window=sliding_window, chunk_size=chunk_size)
+                            sliding_window=sliding_window, chunk_size=chunk_size,
+                            part_cnt=md.decode_part_cnt)
     out = torch.empty_like(q)
     if nd:
         paged_decode(q[:nd], k_cache, v_cache, md.decode_block_tables, md.decode_seq_lens, scale,
                      md.decode_partitions, md.decode_part_o, md.decode_part_ml, out=out[:nd],
-                     sliding_window=sliding_window, chunk_size=chunk_size)
+                     sliding_window=sliding_window, chunk_size=chunk_size,
+                     part_cnt=md.decode_part_cnt)
     paged_prefill(q[nd:], k_cache, v_cache, md.prefill_block_tables, md.prefill_seq_lens,
                   md.prefill_cu_q, md.prefill_work, md.prefill_n_work, scale, md.causal,
                   sliding_window, chunk_size, out=out[nd:])

@@ -29,7 +29,7 @@ TUNING_FILE = os.environ.get("EIA_GEMM_TUNING",
 
 MODE_BF16, MODE_SPLIT, MODE_SWIGLU = 0, 1, 2
 # kernel configs: bit0 -> 2 W tiles (32 rows) per wave, bit1 -> 4 waves per workgroup
-CFGS = (0, 1, 2, 3)
+CFGS = tuple(range(12))   # bit0 NT=2, bit1 WAVES=4, bits2-3 pipeline stages-2
 
 
 def cfg_rows(cfg: int) -> int:

@@ -55,7 +55,7 @@ def test_swiglu_gemm(M, I, K):
     w = (torch.randn(2 * I, K, device=DEV) * K ** -0.5).to(BF)
     y = _ref(x, w)
     ref = F.silu(y[:, :I]) * y[:, I:]
-    for cfg in (1, 3):
+    for cfg in (1, 3, 5, 7, 9, 11):
         if gemm.valid(2 * I, K, True, cfg, 1):
             _check(gemm.swiglu_gemm(x, w, cfg=cfg), ref, f"swiglu M={M} I={I} cfg={cfg}")
 

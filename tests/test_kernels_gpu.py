@@ -137,8 +137,8 @@ def _random_tables(lens, bs, nb_total):
                                            (65, 32, 8, 128, 128), (3, 8, 1, 128, 64),
                                            (4, 12, 12, 64, 32), (2, 12, 4, 256, 16),
                                            (3, 64, 8, 128, 128), (2, 20, 1, 128, 32)])
-@pytest.mark.parametrize("P", [1, 3])
-def test_paged_decode(B, Hq, Hkv, D, bs, P):
+@pytest.mark.parametrize("P,fused", [(1, False), (3, False), (3, True), (16, True)])
+def test_paged_decode(B, Hq, Hkv, D, bs, P, fused):
     from enterprise_inference_amd.ops import attention
     torch.manual_seed(B * 7 + Hq)
     lens = [random.Random(i + B).randint(1, 700) for i in range(B)]
@@ -151,10 +151,15 @@ def test_paged_decode(B, Hq, Hkv, D, bs, P):
     scale = D ** -0.5
     po = torch.empty(B * Hq * P * D, device=DEV)
     pml = torch.empty(B * Hq * P * 2, device=DEV)
-    o = attention.paged_decode(q, k, v, bt, sl, scale, P, po, pml)
+    cnt = torch.zeros(B * Hq, dtype=torch.int32, device=DEV) if fused else None
+    o = attention.paged_decode(q, k, v, bt, sl, scale, P, po, pml, part_cnt=cnt)
     r = ref.paged_attention_decode(q.cpu().float(), k.cpu().float(), v.cpu().float(), bt.cpu(),
                                    sl.cpu(), scale)
     _close(o, r, 2e-2, 2e-2, "decode")
+    if fused:   # counters are left zeroed, so a second call (graph replay) merges correctly
+        assert int(cnt.abs().sum()) == 0
+        o2 = attention.paged_decode(q, k, v, bt, sl, scale, P, po, pml, part_cnt=cnt)
+        assert torch.equal(o, o2)
 
 
 def test_paged_decode_zero_len_rows():
