@@ -6,15 +6,20 @@
 //   v_cache[blk][h][d][off]   (dim-major: V^T, consumed by the MFMA P·V as A operand)
 // slot = blk * block_size + off; slot < 0 = padding token (no write).
 //
+// SPLIT: the input is the QKV GEMM's split-K fp32 partial slabs [sk][T][N] (K6 MODE_F32_SPLIT);
+// the reduction (rounded to bf16 exactly like the GEMM epilogue) is fused here, so the decode
+// QKV projection needs no separate reduce kernel.
+//
 // Mapping: one workgroup per token; each head is handled by TPH = D/16 lanes,
 // each lane owning 8 rotation pairs (two 16-B vectors), so q/k/v are read with
 // 16-B loads and written with 16-B stores (V: 2-B scattered stores into V^T,
 // merged by L2 since consecutive tokens of a block share lines).
 #include "eia_common.h"
 
-template <int D, bool NEOX, bool QK_NORM, bool HAS_BIAS>
+template <int D, bool NEOX, bool QK_NORM, bool HAS_BIAS, bool SPLIT>
 __global__ void __launch_bounds__(256)
 rope_qkv_cache_kernel(const bf16_t* __restrict__ qkv, long qkv_stride,
+                      const float* __restrict__ part, int sk, long slab,
                       const int* __restrict__ positions, const float* __restrict__ cos_sin,
                       const int* __restrict__ slot_mapping,
                       bf16_t* __restrict__ k_cache, bf16_t* __restrict__ v_cache,
@@ -53,11 +58,26 @@ rope_qkv_cache_kernel(const bf16_t* __restrict__ qkv, long qkv_stride,
     float a[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
     float b[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
     if (active) {
-      const bf16_t* hp = row + (long)h * D;
-      bf16x8 va = *reinterpret_cast<const bf16x8*>(hp + e0);
-      bf16x8 vb = *reinterpret_cast<const bf16x8*>(hp + e1);
+      if constexpr (SPLIT) {
+        const float* pp = part + (long)t * ntot * D + (long)h * D;
+        for (int k = 0; k < sk; ++k, pp += slab) {
 #pragma unroll
-      for (int j = 0; j < 8; ++j) { a[j] = bf2f(va[j]); b[j] = bf2f(vb[j]); }
+          for (int q4 = 0; q4 < 2; ++q4) {
+            const f32x4 xa = *reinterpret_cast<const f32x4*>(pp + e0 + 4 * q4);
+            const f32x4 xb = *reinterpret_cast<const f32x4*>(pp + e1 + 4 * q4);
+#pragma unroll
+            for (int j = 0; j < 4; ++j) { a[4 * q4 + j] += xa[j]; b[4 * q4 + j] += xb[j]; }
+          }
+        }
+#pragma unroll
+        for (int j = 0; j < 8; ++j) { a[j] = bf2f(f2bf(a[j])); b[j] = bf2f(f2bf(b[j])); }
+      } else {
+        const bf16_t* hp = row + (long)h * D;
+        bf16x8 va = *reinterpret_cast<const bf16x8*>(hp + e0);
+        bf16x8 vb = *reinterpret_cast<const bf16x8*>(hp + e1);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) { a[j] = bf2f(va[j]); b[j] = bf2f(vb[j]); }
+      }
       if constexpr (HAS_BIAS) {
         const bf16_t* bp = bias + (long)h * D;
         bf16x8 ba = *reinterpret_cast<const bf16x8*>(bp + e0);
@@ -144,7 +164,9 @@ rope_qkv_cache_kernel(const bf16_t* __restrict__ qkv, long qkv_stride,
 // pairs (e0+2j, e0+2j+1) -> freq sub*8 + j (j<4), pairs (e1+2j, ..) -> sub*8 + 4 + j.
 // The c[]/s[] loads above read freqs sub*8 .. sub*8+7, matching that order.
 
-EIA_API int eia_rope_qkv_cache(const void* qkv, long qkv_stride, const int* positions,
+// part != nullptr: read the split-K slabs part[sk][T][(Hq+2Hkv)*D] instead of qkv.
+EIA_API int eia_rope_qkv_cache(const void* qkv, long qkv_stride, const float* part, int sk,
+                               const int* positions,
                                const float* cos_sin, const int* slot_mapping, void* k_cache,
                                void* v_cache, void* q_out, const void* bias, const void* q_norm_w,
                                const void* k_norm_w, float eps, int T, int Hq, int Hkv, int D,
@@ -152,12 +174,24 @@ EIA_API int eia_rope_qkv_cache(const void* qkv, long qkv_stride, const int* posi
   if (T < 0 || Hq <= 0 || Hkv <= 0 || block_size <= 0) return EIA_BAD_SHAPE;
   if (T == 0) return EIA_OK;
   if ((q_norm_w == nullptr) != (k_norm_w == nullptr)) return EIA_BAD_SHAPE;
+  if (part != nullptr && sk < 1) return EIA_BAD_SHAPE;
   dim3 grid(T), block(256);
-#define ROPE_LAUNCH(DD, NX, QN, HB)                                                          \
-  hipLaunchKernelGGL((rope_qkv_cache_kernel<DD, NX, QN, HB>), grid, block, 0, st,           \
-                     (const bf16_t*)qkv, qkv_stride, positions, cos_sin, slot_mapping,       \
-                     (bf16_t*)k_cache, (bf16_t*)v_cache, (bf16_t*)q_out, (const bf16_t*)bias, \
-                     (const bf16_t*)q_norm_w, (const bf16_t*)k_norm_w, eps, Hq, Hkv, block_size)
+  const long slab = (long)T * (Hq + 2 * Hkv) * D;
+#define ROPE_LAUNCH(DD, NX, QN, HB)                                                             \
+  do {                                                                                         \
+    if (part != nullptr)                                                                       \
+      hipLaunchKernelGGL((rope_qkv_cache_kernel<DD, NX, QN, HB, true>), grid, block, 0, st,    \
+                         (const bf16_t*)qkv, qkv_stride, part, sk, slab, positions, cos_sin,    \
+                         slot_mapping, (bf16_t*)k_cache, (bf16_t*)v_cache, (bf16_t*)q_out,     \
+                         (const bf16_t*)bias, (const bf16_t*)q_norm_w, (const bf16_t*)k_norm_w, \
+                         eps, Hq, Hkv, block_size);                                             \
+    else                                                                                       \
+      hipLaunchKernelGGL((rope_qkv_cache_kernel<DD, NX, QN, HB, false>), grid, block, 0, st,   \
+                         (const bf16_t*)qkv, qkv_stride, nullptr, 0, 0L, positions, cos_sin,    \
+                         slot_mapping, (bf16_t*)k_cache, (bf16_t*)v_cache, (bf16_t*)q_out,     \
+                         (const bf16_t*)bias, (const bf16_t*)q_norm_w, (const bf16_t*)k_norm_w, \
+                         eps, Hq, Hkv, block_size);                                             \
+  } while (0)
 #define ROPE_D(DD)                                                                \
   {                                                                               \
     const bool qn = q_norm_w != nullptr, hb = bias != nullptr;                    \

@@ -38,7 +38,7 @@ S = ctypes.c_void_p   # hipStream_t
 _SIGNATURES = {
     "eia_rms_norm": [P, P, P, P, F, I, I, L, L, S],
     "eia_layer_norm": [P, P, P, P, P, F, I, I, S],
-    "eia_rope_qkv_cache": [P, L, IP, P, IP, P, P, P, P, P, P, F, I, I, I, I, I, I, S],
+    "eia_rope_qkv_cache": [P, L, P, I, IP, P, IP, P, P, P, P, P, P, F, I, I, I, I, I, I, S],
     "eia_paged_decode": [P, L, P, P, IP, I, IP, P, L, P, P, P, F, I, I, I, I, I, I, I, I, S],
     "eia_paged_prefill": [P, L, P, L, P, P, IP, I, IP, IP, IP, I, F, I, I, I, I, I, I, I, I, S],
     "eia_act_and_mul": [P, P, I, I, L, L, I, S],

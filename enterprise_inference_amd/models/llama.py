@@ -58,7 +58,7 @@ class LlamaAttention(nn.Module):
 
     def forward(self, h: torch.Tensor, md: AttentionMetadata, kv: KVCache) -> torch.Tensor:
         T = h.shape[0]
-        qkv = gemm.linear(h, self.qkv_proj.weight)
+        qkv = gemm.linear(h, self.qkv_proj.weight, defer_reduce=True)   # split-K summed in K4
         q = rope_qkv_cache(qkv, md.positions, self.rotary, md.slot_mapping, kv[0], kv[1],
                            self.num_heads, self.num_kv_heads, self.head_dim,
                            bias=self.qkv_proj.bias,

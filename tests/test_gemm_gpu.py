@@ -77,3 +77,29 @@ def test_splitk_add_rmsnorm(M, H):
     out, r2 = gemm.splitk_add_rmsnorm(s, res, nw, 1e-5)
     _check(r2, r_ref.float(), "residual")
     _check(out, o_ref.float(), "normed")
+
+
+@pytest.mark.parametrize("M,bias", [(1, False), (65, False), (65, True)])
+def test_rope_cache_from_splitk(M, bias):
+    """K4 summing the QKV GEMM's split-K slabs == K4 on the reduced bf16 output."""
+    from enterprise_inference_amd.ops import gemm
+    from enterprise_inference_amd.ops.rotary import RotaryCache, rope_qkv_cache
+    Hq, Hkv, D, K, bs = 32, 8, 128, 4096, 128
+    N = (Hq + 2 * Hkv) * D
+    torch.manual_seed(M)
+    x = torch.randn(M, K, device=DEV, dtype=BF)
+    w = (torch.randn(N, K, device=DEV) * K ** -0.5).to(BF)
+    b = (torch.randn(N, device=DEV) * 0.1).to(BF) if bias else None
+    rot = RotaryCache(D, 4096, 500000.0, None, torch.device(DEV))
+    pos = torch.randint(0, 4000, (M,), device=DEV, dtype=torch.int32)
+    slots = torch.randperm(4 * bs, device=DEV)[:M].to(torch.int32)
+    outs = []
+    for split in (False, True):
+        kc = torch.zeros(4, Hkv, bs, D, device=DEV, dtype=BF)
+        vc = torch.zeros(4, Hkv, D, bs, device=DEV, dtype=BF)
+        s = gemm.skinny(x, w, defer_reduce=True, cfg=2, sk=4)
+        qkv = s if split else s.materialize()
+        q = rope_qkv_cache(qkv, pos, rot, slots, kc, vc, Hq, Hkv, D, bias=b)
+        outs.append((q, kc, vc))
+    for a, c in zip(outs[0], outs[1]):
+        assert torch.equal(a, c)
