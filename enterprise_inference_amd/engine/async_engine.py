@@ -18,6 +18,7 @@ Failure handling:
 from __future__ import annotations
 
 import asyncio
+import concurrent.futures
 import logging
 import os
 import queue
@@ -100,6 +101,13 @@ class AsyncLLMEngine:
         self._cmds.put(("abort", request_id))
         self._wake.set()
 
+    def call_in_engine_thread(self, fn) -> "concurrent.futures.Future":
+        """Run ``fn()`` on the engine thread between steps (profiler start/stop, stats)."""
+        fut: concurrent.futures.Future = concurrent.futures.Future()
+        self._cmds.put(("call", fn, fut))
+        self._wake.set()
+        return fut
+
     def shutdown(self) -> None:
         self._stop = True
         self._wake.set()
@@ -127,6 +135,12 @@ class AsyncLLMEngine:
                         logger.info("request %s added", rid)
                 except Exception as e:   # noqa: BLE001 - validation errors go to the client
                     self._deliver(rid, e)
+            elif cmd[0] == "call":
+                _, fn, fut = cmd
+                try:
+                    fut.set_result(fn())
+                except Exception as e:   # noqa: BLE001 - returned to the caller
+                    fut.set_exception(e)
             else:
                 self.engine.abort_request(cmd[1])
 

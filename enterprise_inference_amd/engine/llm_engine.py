@@ -115,6 +115,9 @@ class LLMEngine:
         self.finished_log: List[RequestOutput] = []      # consumed by the metrics exporter
         self.served_model_name = cfg.served_model_name or m.name or "model"
         self._step_listeners = []
+        from ..utils.profiling import StepProfiler, invariants_enabled
+        self.profiler = StepProfiler()
+        self._check_invariants = invariants_enabled()
 
     # ------------------------------------------------------------------ requests
     def add_request(self, request_id: str, prompt: Optional[str] = None,
@@ -180,8 +183,11 @@ class LLMEngine:
         self.scheduler.finished_since_last.clear()
         if sched.empty:
             return self._emit(touched, {})
-        res = self.executor.execute(self.scheduler.bm, sched)
+        res = self.profiler.step(lambda: self.executor.execute(self.scheduler.bm, sched))
         self.scheduler.update_after_step(sched)
+        if self._check_invariants:
+            from ..utils.profiling import check_engine_invariants
+            check_engine_invariants(self)
         now = time.time()
         self.stats.num_steps += 1
         self.stats.num_preemptions = self.scheduler.num_preemptions

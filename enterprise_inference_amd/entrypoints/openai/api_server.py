@@ -129,6 +129,24 @@ def build_app(ctx: ServingContext, metrics=None, embedder=None, api_key: Optiona
         async def detokenize(body: dict):
             return {"prompt": ctx.tokenizer.decode(body.get("tokens", []))}
 
+        from ...utils.profiling import profiler_dir
+        if profiler_dir():
+            # vLLM-compatible profiler control (only with EIA/VLLM_TORCH_PROFILER_DIR set)
+            import asyncio as _asyncio
+
+            @app.post("/start_profile")
+            async def start_profile():
+                eng = ctx.engine
+                await _asyncio.wrap_future(eng.call_in_engine_thread(eng.engine.profiler.start))
+                return Response(status_code=200)
+
+            @app.post("/stop_profile")
+            async def stop_profile():
+                eng = ctx.engine
+                path = await _asyncio.wrap_future(
+                    eng.call_in_engine_thread(eng.engine.profiler.stop))
+                return JSONResponse({"trace": path})
+
     if embedder is not None:
         from ..tei.server import register_openai_embeddings
         register_openai_embeddings(app, embedder, model_name)

@@ -1,0 +1,144 @@
+"""Auxiliary subsystems: profiler control, block-manager invariant checks,
+fault injection -> health, engine watchdog, and a concurrent-streaming stress test."""
+
+import asyncio
+import json
+import os
+import time
+
+import pytest
+from fastapi.testclient import TestClient
+
+from enterprise_inference_amd.entrypoints.cli_args import parse_args
+
+
+def _build(tmp_path, extra=()):
+    from enterprise_inference_amd.entrypoints.openai.api_server import build_from_args
+    from enterprise_inference_amd.models import catalog
+    d = tmp_path / "tiny"
+    d.mkdir(exist_ok=True)
+    (d / "config.json").write_text(json.dumps(catalog.tiny_config(vocab_size=300)))
+    args = parse_args(["--model", str(d), "--served-model-name", "tiny", "--device", "cpu",
+                       "--load-format", "dummy", "--max-model-len", "512", "--max-num-seqs", "16",
+                       "--max-num-batched-tokens", "256", "--block-size", "16",
+                       "--disable-log-requests", *extra])
+    return build_from_args(args)
+
+
+def test_profiler_start_stop(tmp_path, monkeypatch):
+    monkeypatch.setenv("EIA_TORCH_PROFILER_DIR", str(tmp_path / "prof"))
+    app, aeng = _build(tmp_path)
+    try:
+        with TestClient(app) as c:
+            assert c.post("/start_profile").status_code == 200
+            r = c.post("/v1/completions", json={"model": "tiny", "prompt": "hello", "max_tokens": 4})
+            assert r.status_code == 200
+            trace = c.post("/stop_profile").json()["trace"]
+        assert os.path.exists(trace)
+        assert "engine_step" in open(trace).read()
+    finally:
+        aeng.shutdown()
+
+
+def test_profiler_routes_absent_without_env(tmp_path, monkeypatch):
+    monkeypatch.delenv("EIA_TORCH_PROFILER_DIR", raising=False)
+    monkeypatch.delenv("VLLM_TORCH_PROFILER_DIR", raising=False)
+    app, aeng = _build(tmp_path)
+    try:
+        with TestClient(app) as c:
+            assert c.post("/start_profile").status_code == 404
+    finally:
+        aeng.shutdown()
+
+
+def test_invariant_checker_runs_and_fires(tmp_path, monkeypatch):
+    from enterprise_inference_amd.engine.sampling_params import SamplingParams
+    monkeypatch.setenv("EIA_CHECK_INVARIANTS", "1")
+    app, aeng = _build(tmp_path)
+    try:
+        eng = aeng.engine
+        aeng.shutdown()          # drive the engine synchronously from here
+        outs = eng.generate(["a b c", "d e f g"], SamplingParams(max_tokens=5, temperature=0))
+        assert all(len(o.outputs[0].token_ids) == 5 for o in outs)
+        assert eng.scheduler.bm.check_invariants() == ""
+        eng.scheduler.bm.check_invariants = lambda: "refcount mismatch (injected)"
+        eng.add_request("x", "hi", SamplingParams(max_tokens=2))
+        with pytest.raises(RuntimeError, match="invariant"):
+            while eng.has_unfinished_requests():
+                eng.step()
+    finally:
+        pass
+
+
+def test_fault_injection_crash_marks_unhealthy(tmp_path, monkeypatch):
+    monkeypatch.setenv("EIA_FAULT_INJECT", "crash_after:1")
+    app, aeng = _build(tmp_path)
+    try:
+        with TestClient(app) as c:
+            r = c.post("/v1/completions", json={"model": "tiny", "prompt": "x", "max_tokens": 8})
+            assert r.status_code == 500
+            assert c.get("/health").status_code == 500
+            text = c.get("/metrics").text
+            assert 'eia:engine_healthy{model_name="tiny"} 0.0' in text
+    finally:
+        aeng._stop = True
+
+
+def test_watchdog_step_timeout(tmp_path, monkeypatch):
+    monkeypatch.setenv("EIA_FAULT_INJECT", "delay_step:1.5")
+    monkeypatch.setenv("VLLM_ENGINE_ITERATION_TIMEOUT_S", "0.5")
+    app, aeng = _build(tmp_path)
+    try:
+        with TestClient(app) as c:
+            import threading
+            t = threading.Thread(target=lambda: c.post(
+                "/v1/completions", json={"model": "tiny", "prompt": "x", "max_tokens": 1}))
+            t.start()
+            deadline = time.time() + 10
+            seen = False
+            while time.time() < deadline and not seen:
+                seen = c.get("/health").status_code == 503
+                time.sleep(0.1)
+            assert seen, "watchdog never reported the stuck step"
+            t.join()
+    finally:
+        aeng.shutdown()
+
+
+def test_concurrent_streaming_stress(tmp_path):
+    """32 concurrent SSE streams: every stream is well-formed, ends with [DONE] and carries
+    exactly max_tokens tokens (include_usage)."""
+    import httpx
+    app, aeng = _build(tmp_path)
+
+    async def one(client, i):
+        body = {"model": "tiny", "prompt": f"req {i}", "max_tokens": 6 + i % 5, "stream": True,
+                "stream_options": {"include_usage": True}, "ignore_eos": True,
+                "temperature": 0.8, "seed": i}
+        chunks, done = [], False
+        async with client.stream("POST", "/v1/completions", json=body) as r:
+            assert r.status_code == 200
+            async for line in r.aiter_lines():
+                if not line:
+                    continue
+                assert line.startswith("data: ")
+                payload = line[6:]
+                if payload == "[DONE]":
+                    done = True
+                    break
+                chunks.append(json.loads(payload))
+        assert done
+        usage = chunks[-1]["usage"]
+        assert usage["completion_tokens"] == 6 + i % 5
+        return usage["completion_tokens"]
+
+    async def main():
+        transport = httpx.ASGITransport(app=app)
+        async with httpx.AsyncClient(transport=transport, base_url="http://t") as client:
+            return await asyncio.gather(*[one(client, i) for i in range(32)])
+
+    try:
+        toks = asyncio.run(main())
+        assert sum(toks) == sum(6 + i % 5 for i in range(32))
+    finally:
+        aeng.shutdown()
