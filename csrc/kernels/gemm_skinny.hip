@@ -401,6 +401,11 @@ int dispatch_mt(int mt, int cfg, const bf16_t* x, long ldx, const bf16_t* w, lon
 #undef EIA_MT
 }
 
+// (MT, cfg) pairs whose kernels spill to scratch on gfx950 (hipcc -Rpass-analysis=
+// kernel-resource-usage; 512 VGPR+AGPR budget at 1 wave/SIMD): rejected -- a spilling weight
+// pipeline is slow, and MT=5 cfg=5 also produced wrong results on MI355X.
+constexpr unsigned kSpillCfg[9] = {0x0, 0x200, 0xa00, 0xa20, 0xa20, 0xba0, 0xba2, 0xfb3, 0xfbb};
+
 int check_shape(int N, int K, int sk, int mode, int cfg) {
   const int nt = (cfg & 1) ? 2 : 1, waves = (cfg & 2) ? 4 : 2;
   if (sk < 1 || K % (sk * KC) != 0 || cfg < 0 || cfg > 11) return EIA_BAD_SHAPE;
@@ -425,6 +430,7 @@ EIA_API int eia_gemm_skinny(const void* X, long ldx, const void* W, long ldw, co
                             hipStream_t st) {
   if (M < 1 || M > 128) return EIA_BAD_SHAPE;
   if (int rc = check_shape(N, K, sk, mode, cfg)) return rc;
+  if ((kSpillCfg[(M + 15) / 16] >> cfg) & 1u) return EIA_BAD_SHAPE;
   if ((ldx % 8) || (ldw % 8) || (ldo % 4)) return EIA_BAD_SHAPE;
   return dispatch_mt<false>((M + 15) / 16, cfg, static_cast<const bf16_t*>(X), ldx,
                             static_cast<const bf16_t*>(W), ldw, static_cast<const bf16_t*>(bias),

@@ -37,10 +37,10 @@ def _free_port() -> int:
 
 
 def _agree_num_blocks(nb: int) -> int:
-    if pstate.tp_size() == 1:
+    if len(pstate.replica_ranks()) == 1:
         return nb
     t = torch.tensor([nb], dtype=torch.int64)
-    dist.all_reduce(t, op=dist.ReduceOp.MIN, group=pstate.tp_cpu_group())
+    dist.all_reduce(t, op=dist.ReduceOp.MIN, group=pstate.replica_cpu_group())
     return int(t.item())
 
 
@@ -91,17 +91,18 @@ def _spawned_worker(cfg: EngineConfig, rank: int, world: int, port: int, ring_na
     if torch.cuda.is_available():
         torch.cuda.set_device(rank)
     pstate.init_distributed(cfg.parallel.tensor_parallel_size,
-                            enable_expert_parallel=cfg.parallel.enable_expert_parallel)
+                            enable_expert_parallel=cfg.parallel.enable_expert_parallel,
+                            pp_size=cfg.parallel.pipeline_parallel_size)
     runner = setup_runner(cfg)
     worker_loop(runner, ring_name)
     pstate.destroy_distributed()
 
 
 class TPExecutor:
-    """Driver side of tensor parallelism."""
+    """Driver side of tensor (and pipeline) parallelism: one process per rank of the replica."""
 
     def __init__(self, cfg: EngineConfig, spawn: bool = True):
-        tp = cfg.parallel.tensor_parallel_size
+        tp = cfg.parallel.tensor_parallel_size * cfg.parallel.pipeline_parallel_size
         self.procs = []
         self.ring_name = f"/eia_ring_{os.getpid()}_{id(self) & 0xffff}"
         rt = _native.runtime()
@@ -118,7 +119,9 @@ class TPExecutor:
                               MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
             if torch.cuda.is_available():
                 torch.cuda.set_device(0)
-            pstate.init_distributed(tp, enable_expert_parallel=cfg.parallel.enable_expert_parallel)
+            pstate.init_distributed(cfg.parallel.tensor_parallel_size,
+                                    enable_expert_parallel=cfg.parallel.enable_expert_parallel,
+                                    pp_size=cfg.parallel.pipeline_parallel_size)
         self.runner = setup_runner(cfg)
         self.num_blocks = self.runner.num_blocks
 
@@ -146,7 +149,7 @@ class TPExecutor:
 
 
 def make_executor(cfg: EngineConfig):
-    if cfg.parallel.tensor_parallel_size > 1:
+    if cfg.parallel.tensor_parallel_size * cfg.parallel.pipeline_parallel_size > 1:
         if dist.is_initialized():
             # launched under torchrun: this process is TP rank 0 of its group
             return TPExecutor(cfg, spawn=False)

@@ -67,6 +67,10 @@ class ModelRunner:
         self.load_time = time.time() - t0
         m = cfg.model
         self.num_layers = m.num_hidden_layers
+        self.pp = pstate.pp_size()
+        self.layer_lo, self.layer_hi = pstate.stage_layer_range(self.num_layers)
+        self.num_local_layers = self.layer_hi - self.layer_lo
+        self.hidden_size = m.hidden_size
         self.head_dim = m.head_dim
         self.num_kv_heads = self.model.kv_heads_per_rank()
         self.block_size = cfg.cache.block_size
@@ -115,7 +119,7 @@ class ModelRunner:
     # ------------------------------------------------------------------ KV cache
     def kv_block_bytes(self) -> int:
         e = torch.tensor([], dtype=self.cfg.cache.cache_dtype).element_size()
-        return self.num_layers * 2 * self.num_kv_heads * self.block_size * self.head_dim * e
+        return self.num_local_layers * 2 * self.num_kv_heads * self.block_size * self.head_dim * e
 
     def determine_num_blocks(self) -> int:
         cc = self.cfg.cache
@@ -166,9 +170,14 @@ class ModelRunner:
             prefill_cu_q=cu, prefill_work=torch.tensor(work, dtype=torch.int32, device=self.device),
             prefill_n_work=len(work) // 2, causal=False)
         with torch.no_grad():
-            h = self.model(ids, md, [(k, v)] * self.num_layers)
-            idx = torch.arange(min(n, self.max_num_seqs), device=self.device)
-            self.model.compute_logits(h[idx])
+            inter = None
+            if self.pp > 1 and not pstate.is_first_stage():
+                z = torch.zeros(n, self.hidden_size, dtype=self.cfg.dtype, device=self.device)
+                inter = (z, z.clone())
+            h = self._forward(ids, md, [(k, v)] * self.num_layers, inter)
+            if self.pp == 1 or pstate.is_last_stage():
+                idx = torch.arange(min(n, self.max_num_seqs), device=self.device)
+                self.model.compute_logits(h[idx])
         del h
 
     def allocate_kv_cache(self, num_blocks: Optional[int] = None) -> int:
@@ -177,10 +186,13 @@ class ModelRunner:
         Hkv, bs, D = self.num_kv_heads, self.block_size, self.head_dim
         per_layer = nb * Hkv * bs * D
         # zero-filled: never-written slots must stay finite (masked P=0 times V)
-        buf = torch.zeros(self.num_layers, 2, per_layer, dtype=self.cfg.cache.cache_dtype,
+        # only this pipeline stage's layers get cache memory (others: None)
+        buf = torch.zeros(self.num_local_layers, 2, per_layer, dtype=self.cfg.cache.cache_dtype,
                           device=self.device)
         self.kv_buf = buf
-        self.kv_caches = [(buf[l, 0].view(nb, Hkv, bs, D), buf[l, 1].view(nb, Hkv, D, bs))
+        lo = self.layer_lo
+        self.kv_caches = [(buf[l - lo, 0].view(nb, Hkv, bs, D), buf[l - lo, 1].view(nb, Hkv, D, bs))
+                          if self.layer_lo <= l < self.layer_hi else None
                           for l in range(self.num_layers)]
         logger.info("KV cache: %d blocks x %d tokens (%.1f GiB)", nb, bs,
                     buf.numel() * buf.element_size() / 2**30)
@@ -342,10 +354,50 @@ class ModelRunner:
         off = plan["off"]
         self.d_e_buf[:off].copy_(self.e_buf[:off], non_blocking=True)
         ids, md, lidx = self._eager_inputs(plan)
+        if self.pp > 1:
+            return self._run_stage(ids, md, lidx, plan["n_lidx"])
         h = self.model(ids, md, self.kv_caches)
         if plan["n_lidx"] == 0:
             return None
         return self.model.compute_logits(h.index_select(0, lidx))
+
+    def _forward(self, ids, md, kv_caches, intermediate=None):
+        if self.pp > 1:
+            return self.model(ids, md, kv_caches, intermediate)
+        return self.model(ids, md, kv_caches)
+
+    def _run_stage(self, ids, md, lidx, n_lidx: int) -> Optional[torch.Tensor]:
+        """Pipeline-parallel step (synchronous stage hand-off, CPU-path parity with vLLM's
+        ``--pipeline-parallel-size``): (hidden, residual) flow stage -> stage over
+        torch.distributed send/recv; the last stage's TP rank 0 returns the sampling rows'
+        logits to the replica driver, which samples."""
+        import torch.distributed as dist
+        T = ids.shape[0]
+        inter = None
+        if not pstate.is_first_stage():
+            hb = torch.empty(T, self.hidden_size, dtype=self.cfg.dtype, device=self.device)
+            rb = torch.empty_like(hb)
+            dist.recv(hb, src=pstate.pp_prev_rank())
+            dist.recv(rb, src=pstate.pp_prev_rank())
+            inter = (hb, rb)
+        out = self.model(ids, md, self.kv_caches, inter)
+        driver = pstate.replica_ranks()[0]
+        last_tp0 = pstate.replica_ranks()[(self.pp - 1) * pstate.tp_size()]
+        if not pstate.is_last_stage():
+            h, r = out
+            dist.send(h.contiguous(), dst=pstate.pp_next_rank())
+            dist.send(r.contiguous(), dst=pstate.pp_next_rank())
+            if pstate.is_driver() and n_lidx > 0:
+                logits = torch.empty(n_lidx, self.vocab, dtype=torch.float32, device=self.device)
+                dist.recv(logits, src=last_tp0)
+                return logits
+            return None
+        if n_lidx == 0:
+            return None
+        logits = self.model.compute_logits(out.index_select(0, lidx)).contiguous()
+        if pstate.tp_rank() == 0:
+            dist.send(logits, dst=driver)
+        return logits
 
     # ------------------------------------------------------------------ sampling
     def _sampling_tensors(self, items: List[ScheduledSeq]):
@@ -412,7 +464,7 @@ class ModelRunner:
     # ------------------------------------------------------------------ graphs
     @torch.no_grad()
     def capture_graphs(self, buckets: Optional[List[int]] = None) -> float:
-        if not self.is_gpu or self.cfg.enforce_eager:
+        if not self.is_gpu or self.cfg.enforce_eager or self.pp > 1:
             return 0.0
         t0 = time.time()
         buckets = buckets or graph_buckets(self.max_num_seqs, self.cfg.scheduler.decode_bs_bucket_step)

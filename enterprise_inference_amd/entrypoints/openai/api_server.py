@@ -171,11 +171,12 @@ def build_from_args(args):
         metrics = EngineMetrics(cfg.served_model_name)
         return build_app(None, metrics, embedder=emb, api_key=args.api_key,
                          served_model_name=cfg.served_model_name), None
-    if cfg.parallel.tensor_parallel_size > 1 or os.environ.get("WORLD_SIZE"):
+    if cfg.parallel.world_size > 1 or os.environ.get("WORLD_SIZE"):
         from ...parallel import state as pstate
         if os.environ.get("WORLD_SIZE"):
             pstate.init_distributed(cfg.parallel.tensor_parallel_size,
-                                    enable_expert_parallel=cfg.parallel.enable_expert_parallel)
+                                    enable_expert_parallel=cfg.parallel.enable_expert_parallel,
+                                    pp_size=cfg.parallel.pipeline_parallel_size)
     engine = LLMEngine(cfg)
     metrics = EngineMetrics(cfg.served_model_name)
     aengine = AsyncLLMEngine(engine, metrics, log_requests=not args.disable_log_requests)

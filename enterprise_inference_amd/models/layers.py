@@ -272,18 +272,27 @@ class LayerNorm(nn.Module):
         return norm.layer_norm(x, self.weight, self.bias, self.eps, residual)
 
 
+class PPMissingLayer(nn.Module):
+    """Placeholder for a decoder layer owned by another pipeline stage (no parameters)."""
+
+    def forward(self, *args, **kwargs):   # pragma: no cover - never called
+        raise RuntimeError("layer belongs to another pipeline stage")
+
+
 def init_random_(module: nn.Module, seed: int = 0, std: float = 0.02) -> None:
     """Deterministic random init of every parameter (north star: random weights).
 
     Norm weights -> 1, biases -> 0, matrices ~ N(0, std). Generated on the
-    parameter's device (fast for 70B on GPU), seeded per-parameter.
+    parameter's device (fast for 70B on GPU), seeded per parameter NAME so that
+    a pipeline stage holding a subset of the layers gets the same values.
     """
     import re
+    import zlib
 
     norm_w = re.compile(r"(norm|ln\d*|ln_\w+|layer_norm|layernorm)\.weight$", re.IGNORECASE)
-    for i, (name, p) in enumerate(module.named_parameters()):
+    for name, p in module.named_parameters():
         g = torch.Generator(device=p.device)
-        g.manual_seed(seed * 1000003 + i)
+        g.manual_seed(seed * 1000003 + zlib.crc32(name.encode()))
         if p.dim() == 1:
             if norm_w.search(name):
                 p.data.fill_(1.0)

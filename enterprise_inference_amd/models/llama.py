@@ -22,8 +22,9 @@ from ..ops import activation, gemm  # noqa: F401
 from ..ops.attention import AttentionMetadata, attention
 from ..ops.rotary import RotaryCache, rope_qkv_cache
 from ..parallel import state
-from .layers import (MergedColumnParallelLinear, ParallelLMHead, QKVParallelLinear, RMSNorm,
-                     RowParallelLinear, VocabParallelEmbedding, default_loader)
+from ..ops.gemm import SplitK
+from .layers import (MergedColumnParallelLinear, ParallelLMHead, PPMissingLayer, QKVParallelLinear,
+                     RMSNorm, RowParallelLinear, VocabParallelEmbedding, default_loader)
 
 KVCache = Tuple[torch.Tensor, torch.Tensor]
 
@@ -105,6 +106,8 @@ class LlamaDecoderLayer(nn.Module):
 class LlamaForCausalLM(nn.Module):
     """Also serves MistralForCausalLM / Qwen2ForCausalLM / Qwen3ForCausalLM."""
 
+    supports_pp = True
+
     def __init__(self, cfg: ModelConfig, dtype=torch.bfloat16, device=None,
                  layer_factory=None):
         super().__init__()
@@ -114,23 +117,39 @@ class LlamaForCausalLM(nn.Module):
         self.rotary = RotaryCache(cfg.head_dim, cfg.max_position_embeddings, cfg.rope_theta,
                                   cfg.rope_scaling, device,
                                   is_neox=not cfg.extra.get("rope_interleaved", False))
-        self.embed_tokens = VocabParallelEmbedding(cfg.vocab_size, cfg.hidden_size, dtype, device)
+        # pipeline stage: own layers [start, end); embeddings on the first stage (and the last
+        # when tied), final norm + LM head on the last
+        self.first, self.last = state.is_first_stage(), state.is_last_stage()
+        self.start_layer, self.end_layer = state.stage_layer_range(cfg.num_hidden_layers)
+        need_embed = self.first or (self.last and cfg.tie_word_embeddings)
+        self.embed_tokens = VocabParallelEmbedding(cfg.vocab_size, cfg.hidden_size, dtype,
+                                                   device) if need_embed else None
         make = layer_factory or (lambda i: LlamaDecoderLayer(cfg, i, self.rotary, dtype, device))
-        self.layers = nn.ModuleList([make(i) for i in range(cfg.num_hidden_layers)])
-        self.norm = RMSNorm(cfg.hidden_size, cfg.rms_norm_eps, dtype, device)
+        self.layers = nn.ModuleList([make(i) if self.start_layer <= i < self.end_layer
+                                     else PPMissingLayer() for i in range(cfg.num_hidden_layers)])
+        self.norm = RMSNorm(cfg.hidden_size, cfg.rms_norm_eps, dtype, device) if self.last else None
         self.lm_head = ParallelLMHead(cfg.vocab_size, cfg.hidden_size, dtype, device,
-                                      tied=self.embed_tokens if cfg.tie_word_embeddings else None)
+                                      tied=self.embed_tokens if cfg.tie_word_embeddings else None
+                                      ) if self.last else None
 
     # kv-cache geometry for the engine
     def kv_heads_per_rank(self) -> int:
-        return self.layers[0].self_attn.num_kv_heads
+        return self.layers[self.start_layer].self_attn.num_kv_heads
 
     def forward(self, input_ids: torch.Tensor, md: AttentionMetadata,
-                kv_caches: List[KVCache]) -> torch.Tensor:
-        h = self.embed_tokens(input_ids)
-        residual = None
-        for layer, kv in zip(self.layers, kv_caches):
-            h, residual = layer(h, residual, md, kv)
+                kv_caches: List[KVCache], intermediate=None):
+        """Last stage: final hidden states.  Other stages: (hidden, residual) for the next
+        stage, which passes them back in as ``intermediate``."""
+        if self.first:
+            h, residual = self.embed_tokens(input_ids), None
+        else:
+            h, residual = intermediate
+        for i in range(self.start_layer, self.end_layer):
+            h, residual = self.layers[i](h, residual, md, kv_caches[i])
+        if not self.last:
+            if isinstance(h, SplitK):
+                h = h.materialize()
+            return h, residual
         h, _ = self.norm(h, residual)
         return h
 

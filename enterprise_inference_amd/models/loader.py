@@ -42,6 +42,10 @@ def iter_torch_bins(path: str) -> Iterator[Tuple[str, torch.Tensor]]:
 
 def build_model(cfg: EngineConfig, device: torch.device) -> nn.Module:
     cls = get_model_class(cfg.model.architecture)
+    from ..parallel import state as pstate
+    if pstate.pp_size() > 1 and not getattr(cls, "supports_pp", False):
+        raise NotImplementedError(f"{cfg.model.architecture} does not support "
+                                  "--pipeline-parallel-size > 1 (Llama/Qwen/Mistral/Mixtral do)")
     model = cls(cfg.model, dtype=cfg.dtype, device=device)
     model.eval()
     fmt = cfg.load_format

@@ -167,6 +167,8 @@ def _load_with_stacked_experts(model, weights, base_load):
     for name, t in weights:
         pname, sid = model.map_weight_name(name)
         if sid in ("stacked", "fused_t"):
+            if pname not in params:          # layer of another pipeline stage
+                continue
             p = params[pname]
             kind = "w13" if pname.endswith("w13") else "w2"
             for e in range(t.shape[0]):

@@ -57,8 +57,14 @@ def _load_tuning() -> dict:
 _TUNED = _load_tuning()
 
 
-def valid(N: int, K: int, swiglu: bool, cfg: int, sk: int) -> bool:
+# (M-tile bucket -> cfgs whose kernel spills registers; mirrors kSpillCfg in gemm_skinny.hip)
+SPILL_CFGS = {1: (9,), 2: (9, 11), 3: (5, 9, 11), 4: (5, 9, 11), 5: (5, 7, 8, 9, 11), 6: (1, 5, 7, 8, 9, 11), 7: (0, 1, 4, 5, 7, 8, 9, 10, 11), 8: (0, 1, 3, 4, 5, 7, 8, 9, 10, 11)}
+
+
+def valid(N: int, K: int, swiglu: bool, cfg: int, sk: int, M: Optional[int] = None) -> bool:
     if K % (sk * KC):
+        return False
+    if M is not None and cfg in SPILL_CFGS.get(m_bucket(M), ()):
         return False
     if swiglu:
         return sk == 1 and (cfg & 1) == 1 and (N // 2) % ((4 if cfg & 2 else 2) * 16) == 0
@@ -85,11 +91,11 @@ def heuristic_splitk(N: int, K: int, cfg: int, swiglu: bool = False) -> int:
 def choose(M: int, N: int, K: int, swiglu: bool = False):
     """(cfg, sk) for this shape: tuned table first, else the heuristic."""
     key = (m_bucket(M), N, K, swiglu)
-    if key in _TUNED and (_TUNED[key][0] < 0 or valid(N, K, swiglu, *_TUNED[key])):
+    if key in _TUNED and (_TUNED[key][0] < 0 or valid(N, K, swiglu, *_TUNED[key], M=M)):
         return _TUNED[key]
     cfg = 3 if m_bucket(M) >= 3 else 1
-    if not valid(N, K, swiglu, cfg, 1):
-        cfg = 1
+    if not valid(N, K, swiglu, cfg, 1, M=M):
+        cfg = 2 if valid(N, K, swiglu, 2, 1, M=M) else 1
     return cfg, heuristic_splitk(N, K, cfg, swiglu)
 
 
@@ -107,7 +113,7 @@ def skinny_ok(x: torch.Tensor, w: torch.Tensor, swiglu: bool = False) -> bool:
     if x.stride(1) != 1 or w.stride(1) != 1 or x.stride(0) % 8 or w.stride(0) % 8:
         return False
     cfg, sk = choose(M, N, K, swiglu)
-    return cfg >= 0 and valid(N, K, swiglu, cfg, sk)
+    return cfg >= 0 and valid(N, K, swiglu, cfg, sk, M=M)
 
 
 class SplitK:

@@ -3,9 +3,13 @@
 Replaces the reference's implicit HCCL setup inside vLLM-Gaudi
 (``PT_HPU_ENABLE_LAZY_COLLECTIVES``, core/helm-charts/vllm/gaudi-values.yaml:168):
 here ``torch.distributed`` with backend "nccl" is RCCL over xGMI on ROCm, and
-"gloo" serves the CPU path / CPU tests.  With world = DP x TP, rank r belongs to
-TP group r // TP and DP group r % TP.  EP (``--enable-expert-parallel``,
-core/helm-charts/vllm/gaudi3-values.yaml:492) reuses the TP group.
+"gloo" serves the CPU path / CPU tests.  World = DP x PP x TP; global rank
+r = replica * (PP*TP) + stage * TP + tp_rank, so a TP group is TP consecutive ranks of one
+pipeline stage, a PP group is the ranks of one replica with the same tp_rank, and DP groups
+join the same position of every replica.  EP (``--enable-expert-parallel``,
+core/helm-charts/vllm/gaudi3-values.yaml:492) reuses the TP group.  PP mirrors the
+reference's CPU-only ``--pipeline-parallel-size`` (core/helm-charts/vllm/templates/
+deployment.yaml:75-81); on MI355X a 405B bf16 model fits one node's HBM with TP=8.
 """
 
 from __future__ import annotations
@@ -24,6 +28,11 @@ _TP_RANK = 0
 _TP_SIZE = 1
 _TP_RANKS: List[int] = [0]
 _EP_ENABLED = False
+_PP_RANK = 0
+_PP_SIZE = 1
+_PP_RANKS: List[int] = [0]           # global ranks of my PP group, by stage
+_REPLICA_RANKS: List[int] = [0]      # all PP*TP ranks of my model replica
+_REPLICA_CPU_GROUP: Optional[dist.ProcessGroup] = None
 
 
 def env_rank() -> int:
@@ -39,16 +48,21 @@ def env_local_rank() -> int:
 
 
 def init_distributed(tp_size: int = 1, backend: Optional[str] = None,
-                     enable_expert_parallel: bool = False, timeout_s: float = 600.0) -> None:
+                     enable_expert_parallel: bool = False, timeout_s: float = 600.0,
+                     pp_size: int = 1) -> None:
     """Initialise torch.distributed from the torchrun env (no-op for a single process)."""
     global _TP_GROUP, _DP_GROUP, _CPU_GROUP, _TP_RANK, _TP_SIZE, _TP_RANKS, _EP_ENABLED
+    global _PP_RANK, _PP_SIZE, _PP_RANKS, _REPLICA_RANKS, _REPLICA_CPU_GROUP
     world = env_world()
     _EP_ENABLED = enable_expert_parallel
-    if world == 1 and tp_size == 1:
+    if world == 1 and tp_size == 1 and pp_size == 1:
         _TP_RANK, _TP_SIZE, _TP_RANKS = 0, 1, [0]
+        _PP_RANK, _PP_SIZE, _PP_RANKS, _REPLICA_RANKS = 0, 1, [0], [0]
         return
-    if world % tp_size != 0:
-        raise ValueError(f"WORLD_SIZE={world} not divisible by tensor_parallel_size={tp_size}")
+    rep = tp_size * pp_size
+    if world % rep != 0:
+        raise ValueError(f"WORLD_SIZE={world} not divisible by tensor_parallel_size x "
+                         f"pipeline_parallel_size = {rep}")
     if backend is None:
         backend = "nccl" if torch.cuda.is_available() else "gloo"
     if not dist.is_initialized():
@@ -67,21 +81,34 @@ def init_distributed(tp_size: int = 1, backend: Optional[str] = None,
         cpu = dist.new_group(ranks, backend="gloo") if tp_size > 1 else None
         if rank in ranks:
             _TP_GROUP, _CPU_GROUP, _TP_RANKS = grp, cpu, ranks
-    for i in range(tp_size):
-        ranks = list(range(i, world, tp_size))
+    for r0 in range(0, world, rep):
+        for t in range(tp_size):
+            ranks = [r0 + s * tp_size + t for s in range(pp_size)]
+            if rank in ranks:
+                _PP_RANKS = ranks
+        ranks = list(range(r0, r0 + rep))
+        cpu = dist.new_group(ranks, backend="gloo") if rep > 1 else None
+        if rank in ranks:
+            _REPLICA_RANKS, _REPLICA_CPU_GROUP = ranks, cpu
+    for i in range(rep):
+        ranks = list(range(i, world, rep))
         grp = dist.new_group(ranks) if len(ranks) > 1 else None
         if rank in ranks:
             _DP_GROUP = grp
     _TP_SIZE = tp_size
     _TP_RANK = rank % tp_size
+    _PP_SIZE = pp_size
+    _PP_RANK = (rank % rep) // tp_size
 
 
 def destroy_distributed() -> None:
     global _TP_GROUP, _DP_GROUP, _CPU_GROUP, _TP_RANK, _TP_SIZE, _TP_RANKS
+    global _PP_RANK, _PP_SIZE, _PP_RANKS, _REPLICA_RANKS, _REPLICA_CPU_GROUP
     if dist.is_initialized():
         dist.destroy_process_group()
-    _TP_GROUP = _DP_GROUP = _CPU_GROUP = None
+    _TP_GROUP = _DP_GROUP = _CPU_GROUP = _REPLICA_CPU_GROUP = None
     _TP_RANK, _TP_SIZE, _TP_RANKS = 0, 1, [0]
+    _PP_RANK, _PP_SIZE, _PP_RANKS, _REPLICA_RANKS = 0, 1, [0], [0]
 
 
 def tp_rank() -> int:
@@ -113,7 +140,50 @@ def ep_enabled() -> bool:
 
 
 def is_driver() -> bool:
-    return _TP_RANK == 0
+    """Rank 0 of its model replica (owns the scheduler)."""
+    return _TP_RANK == 0 and _PP_RANK == 0
+
+
+def pp_rank() -> int:
+    return _PP_RANK
+
+
+def pp_size() -> int:
+    return _PP_SIZE
+
+
+def is_first_stage() -> bool:
+    return _PP_RANK == 0
+
+
+def is_last_stage() -> bool:
+    return _PP_RANK == _PP_SIZE - 1
+
+
+def pp_prev_rank() -> int:
+    return _PP_RANKS[_PP_RANK - 1]
+
+
+def pp_next_rank() -> int:
+    return _PP_RANKS[_PP_RANK + 1]
+
+
+def replica_ranks() -> List[int]:
+    return list(_REPLICA_RANKS)
+
+
+def replica_cpu_group() -> Optional[dist.ProcessGroup]:
+    return _REPLICA_CPU_GROUP
+
+
+def stage_layer_range(num_layers: int, stage: Optional[int] = None,
+                      stages: Optional[int] = None) -> "tuple[int, int]":
+    """Contiguous layer range of a pipeline stage; the remainder goes to the first stages."""
+    stage = _PP_RANK if stage is None else stage
+    stages = _PP_SIZE if stages is None else stages
+    base, rem = divmod(num_layers, stages)
+    start = stage * base + min(stage, rem)
+    return start, start + base + (1 if stage < rem else 0)
 
 
 def set_tp_for_testing(rank: int, size: int) -> None:

@@ -60,7 +60,7 @@ def candidates(M, N, K, swiglu):
     nk = K // gemm.KC
     for cfg in gemm.CFGS:
         for sk in range(1, nk + 1):
-            if nk % sk or not gemm.valid(N, K, swiglu, cfg, sk):
+            if nk % sk or not gemm.valid(N, K, swiglu, cfg, sk, M=M):
                 continue
             rows = gemm.cfg_rows(cfg) if not swiglu else gemm.cfg_rows(cfg)
             grid = (N // rows) * sk

@@ -32,7 +32,7 @@ def test_skinny_linear(M, N, K):
     b = torch.randn(N, device=DEV, dtype=BF)
     for cfg in gemm.CFGS:
         for sk in sorted({1, gemm.heuristic_splitk(N, K, cfg)}):
-            if not gemm.valid(N, K, False, cfg, sk):
+            if not gemm.valid(N, K, False, cfg, sk, M=M):
                 continue
             out = gemm.skinny(x, w, b, cfg=cfg, sk=sk)
             _check(out, _ref(x, w, b), f"M={M} N={N} K={K} cfg={cfg} sk={sk}")
@@ -56,7 +56,7 @@ def test_swiglu_gemm(M, I, K):
     y = _ref(x, w)
     ref = F.silu(y[:, :I]) * y[:, I:]
     for cfg in (1, 3, 5, 7, 9, 11):
-        if gemm.valid(2 * I, K, True, cfg, 1):
+        if gemm.valid(2 * I, K, True, cfg, 1, M=M):
             _check(gemm.swiglu_gemm(x, w, cfg=cfg), ref, f"swiglu M={M} I={I} cfg={cfg}")
 
 

@@ -30,12 +30,13 @@ def _ckpt(tmp_path, d):
     return str(tmp_path)
 
 
-def _run(path, d, tp, ep=False):
+def _run(path, d, tp, ep=False, pp=1):
     cfg = EngineConfig(model=ModelConfig.from_hf_dict(d), model_path=path,
                        cache=CacheConfig(block_size=16, num_gpu_blocks=64),
                        scheduler=SchedulerConfig(max_num_seqs=4, max_num_batched_tokens=40,
                                                  max_model_len=256),
-                       parallel=ParallelConfig(tensor_parallel_size=tp, enable_expert_parallel=ep),
+                       parallel=ParallelConfig(tensor_parallel_size=tp, enable_expert_parallel=ep,
+                                               pipeline_parallel_size=pp),
                        device="cpu", dtype=torch.float32)
     eng = LLMEngine(cfg)
     try:
@@ -56,4 +57,18 @@ def test_tp2_matches_tp1(tmp_path, arch, ep):
     path = _ckpt(tmp_path, d)
     ref = _run(path, d, 1)
     got = _run(path, d, 2, ep)
+    assert got == ref
+
+
+@pytest.mark.parametrize("arch,tp,pp,layers", [("LlamaForCausalLM", 1, 2, 3),
+                                               ("MixtralForCausalLM", 1, 2, 2),
+                                               ("Qwen2ForCausalLM", 2, 2, 4)])
+def test_pipeline_parallel_matches_single(tmp_path, arch, tp, pp, layers):
+    """--pipeline-parallel-size (CPU path, reference xeon-values.yaml): stages own contiguous
+    layer ranges (uneven split with 3 layers), hand (hidden, residual) over send/recv, and the
+    last stage returns logits to the driver; tokens equal the single-process run."""
+    d = tiny_config(arch, num_hidden_layers=layers)
+    path = _ckpt(tmp_path, d)
+    ref = _run(path, d, 1)
+    got = _run(path, d, tp, pp=pp)
     assert got == ref
