@@ -17,6 +17,9 @@ def worker(rank: int, world: int) -> None:
     torch.cuda.set_device(0)
     torch.zeros(1, device="cuda")
     hip = ctypes.CDLL("libamdhip64.so")
+
+    class H(ctypes.Structure):            # hipIpcMemHandle_t is passed BY VALUE
+        _fields_ = [("reserved", ctypes.c_char * 64)]
     res = {}
     handles = {}
     for k, fl in KINDS.items():
@@ -25,15 +28,16 @@ def worker(rank: int, world: int) -> None:
             rc = hip.hipMalloc(ctypes.byref(p), ctypes.c_size_t(1 << 20))
         else:
             rc = hip.hipExtMallocWithFlags(ctypes.byref(p), ctypes.c_size_t(1 << 20), ctypes.c_uint(fl))
-        h = (ctypes.c_char * 64)()
-        rg = hip.hipIpcGetMemHandle(h, p) if rc == 0 else -1
+        h = H()
+        rg = hip.hipIpcGetMemHandle(ctypes.byref(h), p) if rc == 0 else -1
         res[k] = [rc, rg]
-        handles[k] = bytes(h)
+        handles[k] = bytes(h.reserved)
     allh = [None] * world
     dist.all_gather_object(allh, handles)
     for k in KINDS:
         peer = allh[(rank + 1) % world][k]
-        h = (ctypes.c_char * 64).from_buffer_copy(peer)
+        h = H()
+        ctypes.memmove(ctypes.addressof(h), peer, 64)
         q = ctypes.c_void_p()
         ro = hip.hipIpcOpenMemHandle(ctypes.byref(q), h, ctypes.c_uint(1))
         res[k].append(ro)

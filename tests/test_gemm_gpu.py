@@ -69,7 +69,7 @@ def test_splitk_add_rmsnorm(M, H):
     w = (torch.randn(H, K, device=DEV) * K ** -0.5).to(BF)
     res = torch.randn(M, H, device=DEV, dtype=BF)
     nw = (torch.rand(H, device=DEV) + 0.5).to(BF)
-    s = gemm.skinny(x, w, defer_reduce=True, cfg=1, sk=4)
+    s = gemm.skinny(x, w, defer_reduce=True, cfg=2, sk=4)
     assert isinstance(s, gemm.SplitK) and s.sk > 1
     y = _ref(x, w)
     r_ref = (y + res.float()).to(BF)
