@@ -130,6 +130,15 @@ class SplitK:
         return (self.M, self.N)
 
     def materialize(self, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+        if not self.part.is_cuda:    # CPU reference (tests / CPU path)
+            r = self.part.sum(0)
+            if self.bias is not None:
+                r = r + self.bias.float()
+            r = r.to(torch.bfloat16)
+            if out is not None:
+                out.copy_(r)
+                return out
+            return r
         o = out if out is not None else torch.empty(self.M, self.N, dtype=torch.bfloat16,
                                                     device=self.part.device)
         check(lib().eia_splitk_reduce(ptr(self.part), self.sk, self.M, self.N, ptr(self.bias),

@@ -36,12 +36,12 @@ def rope_qkv_cache(qkv, positions: Optional[torch.Tensor],
     if isinstance(qkv, SplitK):
         if qkv.bias is not None:
             require(bias is None, "rope_qkv_cache: bias given twice")
-            bias = qkv.bias
         if use_hip(qkv.part, k_cache):
-            part, sk = qkv, qkv.sk
+            part = qkv
+            bias = qkv.bias if qkv.bias is not None else bias   # added by the kernel
         else:
-            qkv = qkv.materialize()
-    if not (use_hip(qkv, k_cache) and qkv.dtype == torch.bfloat16):
+            qkv = qkv.materialize()                             # includes the bias
+    if part is None and not (use_hip(qkv, k_cache) and qkv.dtype == torch.bfloat16):
         return ref.rope_qkv_cache(qkv, positions, cos_sin, slot_mapping, k_cache, v_cache,
                                   num_heads, num_kv_heads, head_dim, bias, q_norm_w, k_norm_w,
                                   norm_eps, rotary is None or rotary.is_neox)

@@ -70,3 +70,28 @@ def test_llama4_text_matches_transformers():
     eng.executor.runner.model.load_weights(hf.state_dict().items())
     # 50-token prompt crosses the 32-token attention chunk and the temperature floor
     _check(eng, hf, [list(range(20, 70)), [7, 8, 9]], n=5)
+
+
+def test_rope_cache_accepts_splitk_on_cpu():
+    """The split-K hand-off into K4 (ops/rotary.py) also works on the CPU reference path."""
+    import torch
+    from enterprise_inference_amd.ops import gemm
+    from enterprise_inference_amd.ops.rotary import RotaryCache, rope_qkv_cache
+    Hq, Hkv, D, M = 4, 2, 64, 3
+    N = (Hq + 2 * Hkv) * D
+    part = torch.randn(2, M, N)
+    bias = torch.randn(N).to(torch.bfloat16)
+    rot = RotaryCache(D, 128, 10000.0, None, torch.device("cpu"))
+    pos = torch.tensor([0, 5, 9], dtype=torch.int32)
+    slots = torch.tensor([0, 1, 2], dtype=torch.int32)
+    outs = []
+    for split in (True, False):
+        kc = torch.zeros(2, Hkv, 16, D, dtype=torch.bfloat16)
+        vc = torch.zeros(2, Hkv, D, 16, dtype=torch.bfloat16)
+        s = gemm.SplitK(part, 2, M, N, bias)
+        qkv = s if split else s.materialize()
+        q = rope_qkv_cache(qkv, pos, rot, slots, kc, vc, Hq, Hkv, D,
+                           bias=None)
+        outs.append((q, kc, vc))
+    for a, b in zip(*outs):
+        assert torch.equal(a, b)
