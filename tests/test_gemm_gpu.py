@@ -101,5 +101,5 @@ def test_rope_cache_from_splitk(M, bias):
         qkv = s if split else s.materialize()
         q = rope_qkv_cache(qkv, pos, rot, slots, kc, vc, Hq, Hkv, D, bias=b)
         outs.append((q, kc, vc))
-    for a, c in zip(outs[0], outs[1]):
-        assert torch.equal(a, c)
+    for a, c in zip(outs[0], outs[1]):   # same math; allow 1 bf16 ulp (summation contraction)
+        torch.testing.assert_close(a.float(), c.float(), rtol=2 ** -7, atol=1e-3)
