@@ -141,7 +141,7 @@ MULTISTREAM = textwrap.dedent('''
 ''')
 
 
-@pytest.mark.parametrize("world", [2, 4, 8])
+@pytest.mark.parametrize("world", [2, 4])
 def test_allreduce_kernel_multistream(tmp_path, world):
     """The K12 kernel with W 'ranks' inside ONE process: each rank's buffers are ordinary
     in-process allocations and each rank's kernel runs on its own HIP stream, concurrently
@@ -154,7 +154,7 @@ def test_allreduce_kernel_multistream(tmp_path, world):
     f.write_text(MULTISTREAM)
     env = dict(os.environ, EIA_ROOT=root, GPU_MAX_HW_QUEUES="8")
     r = subprocess.run([sys.executable, str(f), str(world)], env=env, capture_output=True,
-                       text=True, timeout=300)
+                       text=True, timeout=120)
     out = r.stdout + r.stderr
     assert r.returncode == 0, out[-3000:]
     assert "NO_SPIN_ERR BAD 0" in out, out[-3000:]
