@@ -237,39 +237,51 @@ paged_decode_kernel(const bf16_t* __restrict__ q, long q_stride,
       out[(long)b * out_stride + (long)hq * D + d] = f2bf(Ls > 0.f ? O / Ls : 0.f);
     } else {
       const long pi = ((long)b * Hq + hq) * P + p;
-      part_o[pi * D + d] = O;
-      if (d == 0) { part_ml[2 * pi] = M; part_ml[2 * pi + 1] = Ls; }
+      // agent-scope relaxed atomic stores = plain stores that are coherent across the XCDs'
+      // L2s (sc1), so the merging workgroup (possibly on another XCD) reads them without a
+      // cache-wide writeback/invalidate fence
+      __hip_atomic_store(part_o + pi * D + d, O, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (d == 0) {
+        __hip_atomic_store(part_ml + 2 * pi, M, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(part_ml + 2 * pi + 1, Ls, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
     }
   }
   if (P == 1 || part_cnt == nullptr) return;
   // Fused partition merge: the last of the P workgroups of this (b, kv head, q group) merges
-  // the partials (no separate reduce launch).  Agent-scope fences write back / invalidate the
-  // per-XCD L2s so partials written on another XCD are visible; the last arrival resets the
+  // the partials (no separate reduce launch).  No __threadfence(): an agent-scope fence
+  // writes back AND invalidates the whole XCD L2 on gfx950, which -- issued by ~1000
+  // workgroups -- measured 10x slower.  Instead every wave drains its (sc1) partial stores
+  // (s_waitcnt 0) before the barrier, the arrival counter is an agent-scope atomic, and the
+  // merger reads the partials with agent-scope atomic loads.  The last arrival resets the
   // counter, keeping the kernel replayable inside a HIP graph.
-  __threadfence();
+  __builtin_amdgcn_s_waitcnt(0);
   __syncthreads();
   int* cnt = part_cnt + ((long)b * Hkv + kvh) * NQG + qg;
-  if (threadIdx.x == 0) s_last = (atomicAdd(cnt, 1) == P - 1);
+  if (threadIdx.x == 0)
+    s_last = __hip_atomic_fetch_add(cnt, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == P - 1;
   __syncthreads();
   if (!s_last) return;
-  __threadfence();
+  auto ld = [](const float* p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  };
   for (int idx = threadIdx.x; idx < 16 * D; idx += blockDim.x) {
     const int cq = idx / D, d = idx % D;
     if (cq >= nq) continue;
     const long base = ((long)b * Hq + hq0 + cq) * P;
     float M = NEG_INF;
-    for (int pp = 0; pp < P; ++pp) M = fmaxf(M, __builtin_nontemporal_load(part_ml + 2 * (base + pp)));
+    for (int pp = 0; pp < P; ++pp) M = fmaxf(M, ld(part_ml + 2 * (base + pp)));
     float Ls = 0.f, O = 0.f;
     if (M != NEG_INF) {
       for (int pp = 0; pp < P; ++pp) {
-        const float f = exp2f(__builtin_nontemporal_load(part_ml + 2 * (base + pp)) - M);
-        Ls += __builtin_nontemporal_load(part_ml + 2 * (base + pp) + 1) * f;
-        O += __builtin_nontemporal_load(part_o + (base + pp) * D + d) * f;
+        const float f = exp2f(ld(part_ml + 2 * (base + pp)) - M);
+        Ls += ld(part_ml + 2 * (base + pp) + 1) * f;
+        O += ld(part_o + (base + pp) * D + d) * f;
       }
     }
     out[(long)b * out_stride + (long)(hq0 + cq) * D + d] = f2bf(Ls > 0.f ? O / Ls : 0.f);
   }
-  if (threadIdx.x == 0) *cnt = 0;
+  if (threadIdx.x == 0) __hip_atomic_store(cnt, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 template <int D>
