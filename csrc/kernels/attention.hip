@@ -164,8 +164,8 @@ paged_decode_kernel(const bf16_t* __restrict__ q, long q_stride,
                     bf16_t* __restrict__ out, long out_stride,
                     float* __restrict__ part_o, float* __restrict__ part_ml,
                     int* __restrict__ part_cnt,
-                    float scale_log2, int Hq, int Hkv, int bs, int P, int NQG,
-                    int sliding_window, int chunk_size) {
+                    float scale_log2, int Hq, int Hkv, int bs, int Pmax, int NQG,
+                    int sliding_window, int chunk_size, const int* __restrict__ p_dyn) {
   __shared__ int s_last;
   __shared__ float sm[4][16];
   __shared__ float sl[4][16];
@@ -174,6 +174,12 @@ paged_decode_kernel(const bf16_t* __restrict__ q, long q_stride,
   const int b = blockIdx.x;
   const int kvh = blockIdx.y / NQG, qg = blockIdx.y % NQG;
   const int p = blockIdx.z;
+  // partitions actually used this call: a HIP graph is captured with grid.z = Pmax and the
+  // host writes the step's P (from the batch's longest context) into device memory, so one
+  // graph serves short and long contexts; surplus workgroups exit at once (grid.z is the
+  // slowest dispatch dimension, so they trail the real work)
+  const int P = p_dyn != nullptr ? max(1, min(*p_dyn, Pmax)) : Pmax;
+  if (p >= P) return;
   const int G = Hq / Hkv;
   const int hq0 = kvh * G + qg * 16;
   const int nq = min(16, G - qg * 16);
@@ -236,7 +242,7 @@ paged_decode_kernel(const bf16_t* __restrict__ q, long q_stride,
     if (P == 1) {
       out[(long)b * out_stride + (long)hq * D + d] = f2bf(Ls > 0.f ? O / Ls : 0.f);
     } else {
-      const long pi = ((long)b * Hq + hq) * P + p;
+      const long pi = ((long)b * Hq + hq) * Pmax + p;
       // agent-scope relaxed atomic stores = plain stores that are coherent across the XCDs'
       // L2s (sc1), so the merging workgroup (possibly on another XCD) reads them without a
       // cache-wide writeback/invalidate fence
@@ -268,7 +274,7 @@ paged_decode_kernel(const bf16_t* __restrict__ q, long q_stride,
   for (int idx = threadIdx.x; idx < 16 * D; idx += blockDim.x) {
     const int cq = idx / D, d = idx % D;
     if (cq >= nq) continue;
-    const long base = ((long)b * Hq + hq0 + cq) * P;
+    const long base = ((long)b * Hq + hq0 + cq) * Pmax;
     float M = NEG_INF;
     for (int pp = 0; pp < P; ++pp) M = fmaxf(M, ld(part_ml + 2 * (base + pp)));
     float Ls = 0.f, O = 0.f;
@@ -287,9 +293,12 @@ paged_decode_kernel(const bf16_t* __restrict__ q, long q_stride,
 template <int D>
 __global__ void __launch_bounds__(256)
 paged_decode_reduce_kernel(const float* __restrict__ part_o, const float* __restrict__ part_ml,
-                           bf16_t* __restrict__ out, long out_stride, int Hq, int P) {
+                           bf16_t* __restrict__ out, long out_stride, int Hq, int Pmax,
+                           const int* __restrict__ p_dyn) {
+  const int P = p_dyn != nullptr ? max(1, min(*p_dyn, Pmax)) : Pmax;
+  if (P == 1) return;                     // the decode kernel wrote the output directly
   const int b = blockIdx.x, h = blockIdx.y;
-  const long base = ((long)b * Hq + h) * P;
+  const long base = ((long)b * Hq + h) * Pmax;
   float M = NEG_INF;
   for (int p = 0; p < P; ++p) M = fmaxf(M, part_ml[2 * (base + p)]);
   for (int d = threadIdx.x; d < D; d += blockDim.x) {
@@ -380,7 +389,8 @@ EIA_API int eia_paged_decode(const void* q, long q_stride, const void* k_cache, 
                              const int* block_tables, int bt_stride, const int* seq_lens,
                              void* out, long out_stride, float* part_o, float* part_ml,
                              int* part_cnt, float scale, int B, int Hq, int Hkv, int D, int bs, int P,
-                             int sliding_window, int chunk_size, hipStream_t st) {
+                             int sliding_window, int chunk_size, const int* p_dyn,
+                             hipStream_t st) {
   if (B < 0 || Hkv <= 0 || Hq % Hkv != 0 || bs % 16 != 0 || P < 1) return EIA_BAD_SHAPE;
   if (P > 1 && (part_o == nullptr || part_ml == nullptr)) return EIA_BAD_SHAPE;
   if (B == 0) return EIA_OK;
@@ -392,10 +402,10 @@ EIA_API int eia_paged_decode(const void* q, long q_stride, const void* k_cache, 
   hipLaunchKernelGGL((paged_decode_kernel<DD>), grid, block, 0, st, (const bf16_t*)q, q_stride, \
                      (const bf16_t*)k_cache, (const bf16_t*)v_cache, block_tables, bt_stride, \
                      seq_lens, (bf16_t*)out, out_stride, part_o, part_ml, part_cnt, sl2, Hq, Hkv, bs, \
-                     P, NQG, sliding_window, chunk_size);                                    \
+                     P, NQG, sliding_window, chunk_size, p_dyn);                             \
   if (P > 1 && part_cnt == nullptr)                                                         \
     hipLaunchKernelGGL((paged_decode_reduce_kernel<DD>), dim3(B, Hq), dim3(DD < 256 ? DD : 256), 0, st, \
-                       part_o, part_ml, (bf16_t*)out, out_stride, Hq, P);
+                       part_o, part_ml, (bf16_t*)out, out_stride, Hq, P, p_dyn);
   switch (D) {
     case 64: DEC(64) break;
     case 128: DEC(128) break;

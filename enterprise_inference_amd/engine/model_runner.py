@@ -80,6 +80,7 @@ class ModelRunner:
         self.kv_caches: List[Tuple[torch.Tensor, torch.Tensor]] = []
         self.num_blocks = 0
         self.graphs: Dict[int, torch.cuda.CUDAGraph] = {}
+        self.graph_P: Dict[int, int] = {}
         self.graph_pool = None
         self.vocab = m.vocab_size
         self.num_heads = m.num_attention_heads // pstate.tp_size()
@@ -92,7 +93,8 @@ class ModelRunner:
         self.max_work = T // qb + S + 1
         pin = self.is_gpu
         # graph (decode) region, fixed offsets
-        self.g_hdr = torch.zeros(4 * S, dtype=torch.int32, pin_memory=pin)      # ids|pos|slot|len
+        # ids|pos|slot|len|P (P: decode partitions of this step, read by K1 inside the graph)
+        self.g_hdr = torch.zeros(4 * S + 4, dtype=torch.int32, pin_memory=pin)
         self.g_bt = torch.zeros(S * mb, dtype=torch.int32, pin_memory=pin)
         # eager region: packed per step
         self.e_size = 3 * T + 2 * S * mb + 3 * S + 1 + 2 * self.max_work + S + 64
@@ -101,7 +103,7 @@ class ModelRunner:
         self.s_i32 = torch.zeros(S, dtype=torch.int32, pin_memory=pin)          # top_k
         self.s_i64 = torch.zeros(S, dtype=torch.int64, pin_memory=pin)          # seeds
         dev = self.device
-        self.d_g_hdr = torch.zeros(4 * S, dtype=torch.int32, device=dev)
+        self.d_g_hdr = torch.zeros(4 * S + 4, dtype=torch.int32, device=dev)
         self.d_g_bt = torch.zeros(S * mb, dtype=torch.int32, device=dev)
         self.d_e_buf = torch.zeros(self.e_size, dtype=torch.int32, device=dev)
         self.d_s_f32 = torch.zeros(3 * S, dtype=torch.float32, device=dev)
@@ -219,6 +221,8 @@ class ModelRunner:
             hdr[S + n:S + Bp] = 0
             hdr[2 * S + n:2 * S + Bp] = -1
             hdr[3 * S + n:3 * S + Bp] = 0
+        max_len = int(hdr[3 * S:3 * S + n].max()) if n else 1
+        hdr[4 * S] = min(self._decode_partitions(Bp, max_len), self.graph_P.get(Bp, 1))
         return {"kind": "graph", "Bp": Bp, "nd": n}
 
     def _upload_graph(self, Bp: int) -> None:
@@ -232,7 +236,7 @@ class ModelRunner:
             num_decode=Bp, num_prefill_tokens=0, slot_mapping=d[2 * S:2 * S + Bp],
             positions=d[S:S + Bp], decode_block_tables=self.d_g_bt[:Bp * self.maxb].view(Bp, self.maxb),
             decode_seq_lens=d[3 * S:3 * S + Bp], decode_partitions=P, decode_part_o=self.part_o,
-            decode_part_ml=self.part_ml, decode_part_cnt=self.part_cnt)
+            decode_part_ml=self.part_ml, decode_p_dyn=d[4 * S:4 * S + 1])
         return d[:Bp], md
 
     def _prepare_eager(self, bm: BlockManager, out: SchedulerOutput) -> dict:
@@ -311,7 +315,6 @@ class ModelRunner:
             decode_block_tables=d[o["dbt"]:o["dbt"] + nd * mb_d].view(nd, mb_d) if nd else None,
             decode_seq_lens=d[o["dlen"]:o["dlen"] + nd] if nd else None,
             decode_partitions=plan["P"], decode_part_o=self.part_o, decode_part_ml=self.part_ml,
-            decode_part_cnt=self.part_cnt,
             prefill_block_tables=d[o["pbt"]:o["pbt"] + npf * mb_p].view(npf, mb_p) if npf else None,
             prefill_seq_lens=d[o["plen"]:o["plen"] + npf] if npf else None,
             prefill_cu_q=d[o["cu"]:o["cu"] + npf + 1] if npf else None,
@@ -339,8 +342,8 @@ class ModelRunner:
         a = np.frombuffer(payload, dtype=np.int32)
         if plan["kind"] == "graph":
             S = self.max_num_seqs
-            self.g_hdr.numpy()[:] = a[:4 * S]
-            self.g_bt.numpy()[:len(a) - 4 * S] = a[4 * S:]
+            self.g_hdr.numpy()[:] = a[:4 * S + 4]
+            self.g_bt.numpy()[:len(a) - 4 * S - 4] = a[4 * S + 4:]
         else:
             self.e_buf.numpy()[:len(a)] = a
 
@@ -472,9 +475,10 @@ class ModelRunner:
         self.graph_pool = torch.cuda.graph_pool_handle()
         # dummy decode inputs: len 1, slot -1 (no cache write), block 0
         S = self.max_num_seqs
-        hdr = torch.zeros(4 * S, dtype=torch.int32)
+        hdr = torch.zeros(4 * S + 4, dtype=torch.int32)
         hdr[2 * S:3 * S] = -1
-        hdr[3 * S:] = 1
+        hdr[3 * S:4 * S] = 1
+        hdr[4 * S] = 1
         self.d_g_hdr.copy_(hdr)
         self.d_g_bt.zero_()
         stream = torch.cuda.Stream()
@@ -482,6 +486,7 @@ class ModelRunner:
         with torch.cuda.stream(stream):
             for Bp in sorted(buckets, reverse=True):
                 P = self._decode_partitions(Bp, self.cfg.scheduler.max_model_len)
+                self.graph_P[Bp] = P          # upper bound; the step's P is read on device
                 ids, md = self._graph_metadata(Bp, P)
                 for _ in range(2):       # warm-up (hipBLASLt heuristics, allocator)
                     h = self.model(ids, md, self.kv_caches)

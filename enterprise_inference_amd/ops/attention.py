@@ -37,12 +37,26 @@ def build_prefill_work(q_lens: Sequence[int], qblock: int) -> List[int]:
 
 
 def decode_partitions(batch: int, num_kv_heads: int, num_heads: int, max_len: int,
-                      target_wgs: int = 1024, max_parts: int = 16) -> int:
+                      cus: int = 256, max_parts: int = 8) -> int:
+    """Context partitions (flash-decoding split) for a decode batch.
+
+    Fitted to scripts/bench_attn.py on MI355X (graph-timed, Llama-8B heads): short contexts
+    never split (the partial write + merge costs more than it hides); grids of >= 4 workgroups
+    per CU do not split; small grids split up to one workgroup per CU (B=16: P=2, B=1: P=8);
+    mid-size grids split 2x, or 4x past 2048 tokens (B=65, ctx 4096: 213 us vs 249 us)."""
+    if max_len <= 512:
+        return 1
     g = num_heads // num_kv_heads
     wgs = max(1, batch * num_kv_heads * ((g + 15) // 16))
-    p = max(1, math.ceil(target_wgs / wgs))
-    p = min(p, max_parts, max(1, math.ceil(max_len / 256)))
-    return p
+    if wgs >= 4 * cus:
+        return 1
+    if wgs >= cus:
+        p = 2 if max_len <= 2048 else 4
+    else:
+        p = 2
+        while p < max_parts and wgs * p * 2 <= cus:
+            p *= 2
+    return max(1, min(p, max_parts, max_len // 128))
 
 
 @dataclasses.dataclass
@@ -58,6 +72,7 @@ class AttentionMetadata:
     decode_part_o: Optional[torch.Tensor] = None
     decode_part_ml: Optional[torch.Tensor] = None
     decode_part_cnt: Optional[torch.Tensor] = None      # zeroed int32 [Bd*Hkv*ceil(G/16)]
+    decode_p_dyn: Optional[torch.Tensor] = None         # device int32 [1]: partitions this step
     # prefill part
     prefill_block_tables: Optional[torch.Tensor] = None  # [Sp, maxb] int32
     prefill_seq_lens: Optional[torch.Tensor] = None      # [Sp] int32 (context + new)
@@ -77,12 +92,15 @@ def paged_decode(q: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tensor,
                  part_ml: Optional[torch.Tensor] = None,
                  out: Optional[torch.Tensor] = None, sliding_window: Optional[int] = None,
                  chunk_size: Optional[int] = None,
-                 part_cnt: Optional[torch.Tensor] = None) -> torch.Tensor:
+                 part_cnt: Optional[torch.Tensor] = None,
+                 p_dyn: Optional[torch.Tensor] = None) -> torch.Tensor:
     """q [B, Hq, D] -> out [B, Hq, D].
 
     With ``partitions > 1`` the context is split over grid.z; ``part_cnt`` (zeroed int32,
     >= B*Hkv*ceil(G/16) entries, left zeroed by the kernel) lets the last partition merge the
-    partials in-kernel, otherwise a separate reduce kernel runs."""
+    partials in-kernel, otherwise a separate reduce kernel runs.  ``p_dyn`` (device int32[1])
+    makes ``partitions`` an upper bound and reads the partitions actually used from device
+    memory (HIP graphs captured once per batch bucket)."""
     if not (use_hip(q, k_cache) and q.dtype == torch.bfloat16):
         r = ref.paged_attention_decode(q, k_cache, v_cache, block_tables, seq_lens, scale,
                                        sliding_window, chunk_size)
@@ -111,7 +129,8 @@ def paged_decode(q: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tensor,
         ptr(part_ml) if partitions > 1 else None,
         ptr(part_cnt) if (partitions > 1 and part_cnt is not None) else None,
         float(scale), B, Hq, Hkv, D, bs, partitions,
-        sliding_window or 0, chunk_size or 0, stream(q)), "paged_decode")
+        sliding_window or 0, chunk_size or 0,
+        ptr(p_dyn) if (partitions > 1 and p_dyn is not None) else None, stream(q)), "paged_decode")
     return o
 
 
@@ -153,13 +172,13 @@ def attention(q: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tensor,
         return paged_decode(q[:nd], k_cache, v_cache, md.decode_block_tables, md.decode_seq_lens,
                             scale, md.decode_partitions, md.decode_part_o, md.decode_part_ml,
                             sliding_window=sliding_window, chunk_size=chunk_size,
-                            part_cnt=md.decode_part_cnt)
+                            part_cnt=md.decode_part_cnt, p_dyn=md.decode_p_dyn)
     out = torch.empty_like(q)
     if nd:
         paged_decode(q[:nd], k_cache, v_cache, md.decode_block_tables, md.decode_seq_lens, scale,
                      md.decode_partitions, md.decode_part_o, md.decode_part_ml, out=out[:nd],
                      sliding_window=sliding_window, chunk_size=chunk_size,
-                     part_cnt=md.decode_part_cnt)
+                     part_cnt=md.decode_part_cnt, p_dyn=md.decode_p_dyn)
     paged_prefill(q[nd:], k_cache, v_cache, md.prefill_block_tables, md.prefill_seq_lens,
                   md.prefill_cu_q, md.prefill_work, md.prefill_n_work, scale, md.causal,
                   sliding_window, chunk_size, out=out[nd:])

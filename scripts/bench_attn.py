@@ -68,11 +68,20 @@ def main():
                     t = graph_time(lambda: attention.paged_decode(
                         q, k, v, bt, sl, a.d ** -0.5, P, po, pml, out=out, part_cnt=cnt))
                     res.append((round(t, 2), P, fused))
+            # graph-style: grid for Pmax=8, P chosen per call on device (model runner path)
+            Pm = 8
+            po = torch.empty(B * a.hq * Pm * a.d, device=dev)
+            pml = torch.empty(B * a.hq * Pm * 2, device=dev)
+            pd = torch.tensor([attention.decode_partitions(B, a.hkv, a.hq, L)], dtype=torch.int32,
+                              device=dev)
+            t = graph_time(lambda: attention.paged_decode(
+                q, k, v, bt, sl, a.d ** -0.5, Pm, po, pml, out=out, p_dyn=pd))
+            dyn = (round(t, 2), int(pd.item()))
             res.sort()
             auto = attention.decode_partitions(B, a.hkv, a.hq, L)
             print(json.dumps({"B": B, "ctx": L, "best_us": res[0][0], "best_P": res[0][1],
                               "fused": res[0][2], "TBps": round(kv_bytes / res[0][0] / 1e6, 2),
-                              "heuristic_P": auto, "all": res}), flush=True)
+                              "heuristic_P": auto, "dyn_us_P": dyn, "all": res}), flush=True)
 
 
 if __name__ == "__main__":

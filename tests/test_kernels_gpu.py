@@ -297,3 +297,24 @@ def test_penalties():
     sampling.apply_penalties(b, rows.cpu(), toks.cpu(), cnts.cpu(), rep.cpu(), fq.cpu(), pr.cpu())
     d.FORCE_TORCH = old
     _close(a, b, 1e-5, 0, "penalties")
+
+
+@pytest.mark.parametrize("p_use", [1, 3, 8])
+def test_paged_decode_dynamic_partitions(p_use):
+    """Graph-style call: grid sized for Pmax=8, partitions actually used read from device."""
+    from enterprise_inference_amd.ops import attention
+    B, Hq, Hkv, D, bs, Pmax = 7, 32, 8, 128, 128, 8
+    torch.manual_seed(p_use)
+    lens = [random.Random(i).randint(1, 1500) for i in range(B)]
+    nbt = sum(math.ceil(l / bs) for l in lens) + 3
+    k, v = _make_cache(nbt, Hkv, bs, D, fill=True)
+    bt = _random_tables(lens, bs, nbt).to(DEV)
+    sl = torch.tensor(lens, dtype=torch.int32, device=DEV)
+    q = torch.randn(B, Hq, D, device=DEV, dtype=BF)
+    po = torch.full((B * Hq * Pmax * D,), float("nan"), device=DEV)
+    pml = torch.full((B * Hq * Pmax * 2,), float("nan"), device=DEV)
+    pd = torch.tensor([p_use], dtype=torch.int32, device=DEV)
+    o = attention.paged_decode(q, k, v, bt, sl, D ** -0.5, Pmax, po, pml, p_dyn=pd)
+    r = ref.paged_attention_decode(q.cpu().float(), k.cpu().float(), v.cpu().float(), bt.cpu(),
+                                   sl.cpu(), D ** -0.5)
+    _close(o, r, 2e-2, 2e-2, f"decode p_dyn={p_use}")
