@@ -286,24 +286,40 @@ splitk_reduce_kernel(const float* __restrict__ part, int sk, int M, int N,
 }
 
 // residual[M][H] += sum_k part[k] ; out = rmsnorm(residual) * w   (one workgroup per row)
-template <int VPT>
-__global__ void __launch_bounds__(256)
-splitk_add_rmsnorm_kernel(const float* __restrict__ part, int sk, int M, int H,
+// The decode batch has only M ~ 65 rows, so each row must pull its SK x H fp32 partials
+// with all loads in flight at once: SK is a template parameter (loads unrolled, issued before
+// the first add; summed in slab order, bit-identical to a serial loop) and the workgroup is
+// 1024 threads, one 16-B vector per thread per 4096 columns.  A runtime-SK loop serialised
+// one HBM round trip per slab (10 us per call at SK = 8 in profiles/, vs ~2 us here).
+template <int VPT, int SK>
+__global__ void __launch_bounds__(1024)
+splitk_add_rmsnorm_kernel(const float* __restrict__ part, int sk_rt, int M, int H,
                           bf16_t* __restrict__ residual, const bf16_t* __restrict__ w, float eps,
                           bf16_t* __restrict__ out, long ldo) {
-  __shared__ float scratch[4];
+  __shared__ float scratch[16];
   const int row = blockIdx.x;
   const long total = (long)M * H;
+  const int sk = SK > 0 ? SK : sk_rt;
   float v[VPT][4];
   float ss = 0.f;
 #pragma unroll
   for (int i = 0; i < VPT; ++i) {
-    const int c = (threadIdx.x + i * 256) * 4;
+    const int c = (threadIdx.x + i * 1024) * 4;
     if (c < H) {
       const long off = (long)row * H + c;
-      f32x4 a = *reinterpret_cast<const f32x4*>(part + off);
-      for (int k = 1; k < sk; ++k) a += *reinterpret_cast<const f32x4*>(part + k * total + off);
-      bf16x4 rr = *reinterpret_cast<const bf16x4*>(residual + off);
+      f32x4 a;
+      if constexpr (SK > 0) {
+        f32x4 p[SK];
+#pragma unroll
+        for (int k = 0; k < SK; ++k) p[k] = *reinterpret_cast<const f32x4*>(part + k * total + off);
+        a = p[0];
+#pragma unroll
+        for (int k = 1; k < SK; ++k) a += p[k];
+      } else {
+        a = *reinterpret_cast<const f32x4*>(part + off);
+        for (int k = 1; k < sk; ++k) a += *reinterpret_cast<const f32x4*>(part + k * total + off);
+      }
+      const bf16x4 rr = *reinterpret_cast<const bf16x4*>(residual + off);
       bf16x4 nr;
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
@@ -318,9 +334,9 @@ splitk_add_rmsnorm_kernel(const float* __restrict__ part, int sk, int M, int H,
   const float inv = rsqrtf(tot / (float)H + eps);
 #pragma unroll
   for (int i = 0; i < VPT; ++i) {
-    const int c = (threadIdx.x + i * 256) * 4;
+    const int c = (threadIdx.x + i * 1024) * 4;
     if (c < H) {
-      bf16x4 ww = *reinterpret_cast<const bf16x4*>(w + c);
+      const bf16x4 ww = *reinterpret_cast<const bf16x4*>(w + c);
       bf16x4 o;
 #pragma unroll
       for (int j = 0; j < 4; ++j) o[j] = f2bf(v[i][j] * inv * bf2f(ww[j]));
@@ -465,17 +481,26 @@ EIA_API int eia_splitk_reduce(const float* part, int sk, int M, int N, const voi
 
 EIA_API int eia_splitk_add_rmsnorm(const float* part, int sk, int M, int H, void* residual,
                                    const void* w, float eps, void* out, long ldo, hipStream_t st) {
-  if (H % 4 != 0 || H > 4 * 256 * 16) return EIA_BAD_SHAPE;
-  const int vpt = (H / 4 + 255) / 256;
+  if (H % 4 != 0 || H > 4 * 1024 * 4 || sk < 1) return EIA_BAD_SHAPE;
+  const int vpt = (H / 4 + 1023) / 1024;
   bf16_t* res = static_cast<bf16_t*>(residual);
   const bf16_t* ww = static_cast<const bf16_t*>(w);
   bf16_t* o = static_cast<bf16_t*>(out);
-#define EIA_SKN(V)                                                                              \
-  hipLaunchKernelGGL(splitk_add_rmsnorm_kernel<V>, dim3(M), dim3(256), 0, st, part, sk, M, H, res, \
-                     ww, eps, o, ldo)
-  if (vpt <= 4) EIA_SKN(4);
-  else if (vpt <= 8) EIA_SKN(8);
-  else EIA_SKN(16);
+#define EIA_SKN(V, K)                                                                              \
+  hipLaunchKernelGGL((splitk_add_rmsnorm_kernel<V, K>), dim3(M), dim3(1024), 0, st, part, sk, M, H, \
+                     res, ww, eps, o, ldo)
+#define EIA_SKV(V)                          \
+  switch (sk) {                             \
+    case 1: EIA_SKN(V, 1); break;           \
+    case 2: EIA_SKN(V, 2); break;           \
+    case 4: EIA_SKN(V, 4); break;           \
+    case 8: EIA_SKN(V, 8); break;           \
+    default: EIA_SKN(V, 0); break;          \
+  }
+  if (vpt <= 1) { EIA_SKV(1) }
+  else if (vpt <= 2) { EIA_SKV(2) }
+  else { EIA_SKV(4) }
+#undef EIA_SKV
 #undef EIA_SKN
   EIA_LAUNCH_CHECK();
 }

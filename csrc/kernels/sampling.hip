@@ -162,6 +162,92 @@ EIA_API int eia_sample(const float* logits, long stride, int B, int V, const flo
   EIA_LAUNCH_CHECK();
 }
 
+// Split-row fast path for batches where no row uses top-k / top-p / min-p (greedy or plain
+// temperature sampling -- the serving default).  One 1024-thread workgroup per row leaves
+// most of the 256 CUs idle at decode batch sizes (B ~ 65 -> 65 workgroups, each running the
+// splitmix64 hash and two logs for 128k tokens); here every row is cut into C chunks so the
+// grid is B x C workgroups, each writing its chunk's (value, index) winner, and a second
+// kernel picks each row's winner.  Per-element math and tie-breaking (lowest index) are
+// identical to sample_kernel, so both paths return the same token for the same seed.
+#define SPLIT_THREADS 256
+
+__global__ void __launch_bounds__(SPLIT_THREADS)
+sample_split_kernel(const float* __restrict__ logits, long stride, int V, int chunk,
+                    const float* __restrict__ temperature, const uint64_t* __restrict__ seeds,
+                    float* __restrict__ part_v, int* __restrict__ part_i) {
+  __shared__ float sv[SPLIT_THREADS / 64];
+  __shared__ int si[SPLIT_THREADS / 64];
+  const int b = blockIdx.y, c = blockIdx.x, C = gridDim.x;
+  const float* row = logits + (long)b * stride;
+  const int lo = c * chunk, hi = min(V, lo + chunk);
+  const float T = temperature[b];
+  const bool greedy = !(T > 0.f);
+  const uint64_t seed = seeds[b];
+  ArgMax best{-INFINITY, 0x7fffffff};
+  for (int i = lo + threadIdx.x; i < hi; i += SPLIT_THREADS) {
+    const float l = row[i];
+    float v = l;
+    if (!greedy) {
+      const float u = rng_uniform(seed, (uint32_t)i);
+      v = l / T - logf(-logf(u));
+    }
+    best = argmax_combine(best, ArgMax{v, i});
+  }
+  best = block_argmax(best, sv, si);
+  if (threadIdx.x == 0) {
+    part_v[(long)b * C + c] = best.v;
+    part_i[(long)b * C + c] = best.i;
+  }
+}
+
+__global__ void __launch_bounds__(64)
+sample_merge_kernel(const float* __restrict__ part_v, const int* __restrict__ part_i, int C,
+                    int* __restrict__ out_tokens) {
+  const int b = blockIdx.x;
+  ArgMax best{-INFINITY, 0x7fffffff};
+  for (int c = threadIdx.x; c < C; c += 64)
+    best = argmax_combine(best, ArgMax{part_v[(long)b * C + c], part_i[(long)b * C + c]});
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    ArgMax y{__shfl_xor(best.v, o, 64), __shfl_xor(best.i, o, 64)};
+    best = argmax_combine(best, y);
+  }
+  if (threadIdx.x == 0) out_tokens[b] = best.i == 0x7fffffff ? 0 : best.i;
+}
+
+// part_v / part_i: >= B * ceil(V / chunk) entries each.
+EIA_API int eia_sample_split(const float* logits, long stride, int B, int V, int chunk,
+                             const float* temperature, const uint64_t* seeds, float* part_v,
+                             int* part_i, int* out_tokens, hipStream_t st) {
+  if (B < 0 || V <= 0 || chunk <= 0) return EIA_BAD_SHAPE;
+  if (B == 0) return EIA_OK;
+  const int C = (V + chunk - 1) / chunk;
+  if (C > 4096) return EIA_BAD_SHAPE;
+  hipLaunchKernelGGL(sample_split_kernel, dim3(C, B), dim3(SPLIT_THREADS), 0, st, logits, stride,
+                     V, chunk, temperature, seeds, part_v, part_i);
+  hipLaunchKernelGGL(sample_merge_kernel, dim3(B), dim3(64), 0, st, part_v, part_i, C, out_tokens);
+  EIA_LAUNCH_CHECK();
+}
+
+// Overlapped scheduling: the next step's input ids of sequences whose previous token is still
+// on the device.  ids[i] = tok[src[i]] where src[i] >= 0 (row of the previous step's sampler
+// output), else ids[i] is left as the host wrote it.  Captured inside the decode HIP graph.
+__global__ void fill_ids_kernel(int* __restrict__ ids, const int* __restrict__ src,
+                                const int* __restrict__ tok, int n) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) {
+    const int s = src[i];
+    if (s >= 0) ids[i] = tok[s];
+  }
+}
+
+EIA_API int eia_fill_ids(int* ids, const int* src, const int* tok, int n, hipStream_t st) {
+  if (n < 0) return EIA_BAD_SHAPE;
+  if (n == 0) return EIA_OK;
+  hipLaunchKernelGGL(fill_ids_kernel, dim3((n + 255) / 256), dim3(256), 0, st, ids, src, tok, n);
+  EIA_LAUNCH_CHECK();
+}
+
 // Sparse penalties: for each (row, token, count) triple in the list apply
 //   repetition (HF: divide positive / multiply negative), frequency, presence.
 // prompt tokens get count 0 and flag 1 (repetition only).

@@ -210,7 +210,8 @@ class SchedulerConfig:
     enable_chunked_prefill: bool = True
     # Decode batch-size bucket step for HIP-graph capture (VLLM_DECODE_BS_BUCKET_STEP).
     decode_bs_bucket_step: int = 16
-    delayed_sampling: bool = False
+    # overlapped scheduling: plan step k+1 while step k runs (VLLM_DELAYED_SAMPLING)
+    delayed_sampling: bool = True
 
 
 @dataclasses.dataclass

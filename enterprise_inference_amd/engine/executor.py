@@ -58,12 +58,18 @@ def setup_runner(cfg: EngineConfig) -> ModelRunner:
 
 
 class UniprocExecutor:
+    # steps can be launched ahead of reading their tokens back (engine overlapped scheduling)
+    supports_overlap = True
+
     def __init__(self, cfg: EngineConfig, runner: Optional[ModelRunner] = None):
         self.runner = runner or setup_runner(cfg)
         self.num_blocks = self.runner.num_blocks
 
     def execute(self, bm, sched) -> StepOutput:
         return self.runner.execute(bm, sched)
+
+    def launch(self, bm, sched, overlap: bool):
+        return self.runner.launch(bm, sched, overlap)
 
     def shutdown(self) -> None:
         pass
@@ -100,6 +106,8 @@ def _spawned_worker(cfg: EngineConfig, rank: int, world: int, port: int, ring_na
 
 class TPExecutor:
     """Driver side of tensor (and pipeline) parallelism: one process per rank of the replica."""
+
+    supports_overlap = False    # workers replay plans synchronously; tokens are read each step
 
     def __init__(self, cfg: EngineConfig, spawn: bool = True):
         tp = cfg.parallel.tensor_parallel_size * cfg.parallel.pipeline_parallel_size

@@ -118,6 +118,12 @@ class LLMEngine:
         from ..utils.profiling import StepProfiler, invariants_enabled
         self.profiler = StepProfiler()
         self._check_invariants = invariants_enabled()
+        # Overlapped scheduling (the reference's VLLM_DELAYED_SAMPLING knob,
+        # core/helm-charts/vllm/gaudi-values.yaml:54): step k+1 is scheduled and launched
+        # while step k's sampled tokens are still on the GPU; its input ids are read there.
+        self._overlap = bool(cfg.scheduler.delayed_sampling) and \
+            getattr(executor, "supports_overlap", False)
+        self._pending = None        # StepHandle of the launched, not yet processed step
 
     # ------------------------------------------------------------------ requests
     def add_request(self, request_id: str, prompt: Optional[str] = None,
@@ -166,13 +172,87 @@ class LLMEngine:
             self.requests.pop(rid, None)
 
     def has_unfinished_requests(self) -> bool:
-        return self.scheduler.num_unfinished() > 0
+        return self.scheduler.num_unfinished() > 0 or self._pending is not None
 
     def num_unfinished_requests(self) -> int:
         return len(self.requests)
 
     # ------------------------------------------------------------------ step
+    @staticmethod
+    def _needs_host_tokens(seq: Sequence) -> bool:
+        """Rows whose sampling needs the host (penalties over the output, logits processors,
+        guided decoding, logprobs): their step is read back before the next is planned."""
+        p = seq.params
+        return (p.needs_penalties or p.needs_logit_processing or p.logprobs is not None
+                or p.prompt_logprobs is not None or seq.guided_state is not None
+                or p.best_of > p.n)
+
     def step(self) -> List[RequestOutput]:
+        if not self._overlap:
+            return self._step_sync()
+        t0 = time.time()
+        sched = self.scheduler.schedule()
+        touched: Dict[str, _Request] = {}
+        for s in self.scheduler.finished_since_last:
+            r = self.requests.get(s.request_id)
+            if r:
+                touched[r.request_id] = r
+        self.scheduler.finished_since_last.clear()
+        deltas: Dict[int, tuple] = {}
+        prev, self._pending = self._pending, None
+        if sched.empty:
+            if prev is not None:
+                self._process(prev, touched, deltas)
+            return self._emit(touched, deltas)
+        sample_items = sched.decodes + [p for p in sched.prefills if p.samples]
+        overlap = not any(self._needs_host_tokens(it.seq) for it in sample_items)
+        handle = self.profiler.step(
+            lambda: self.executor.launch(self.scheduler.bm, sched, overlap))
+        for it in sample_items:
+            it.seq.num_pending += 1
+        if prev is not None:
+            self._process(prev, touched, deltas)    # the GPU is busy with `handle` meanwhile
+        self.scheduler.update_after_step(sched)
+        if self._check_invariants:
+            from ..utils.profiling import check_engine_invariants
+            check_engine_invariants(self)
+        self.stats.num_steps += 1
+        self.stats.num_preemptions = self.scheduler.num_preemptions
+        self.stats.num_prompt_tokens += sum(it.num_tokens for it in sched.prefills)
+        if overlap:
+            self._pending = handle
+        else:
+            self._process(handle, touched, deltas)
+        self.stats.step_time_s += time.time() - t0
+        return self._emit(touched, deltas)
+
+    def _process(self, handle, touched: Dict[str, "_Request"], deltas: Dict[int, tuple]) -> None:
+        """Apply a launched step's sampled tokens: append, detokenise, stop checks."""
+        res = handle.result()
+        now = time.time()
+        for r, it in enumerate(handle.items):
+            seq = it.seq
+            if seq.num_pending:
+                seq.num_pending -= 1
+            if seq.finished:
+                continue
+            tok = res.tokens[r]
+            lp = res.logprobs[r] if res.logprobs is not None else None
+            self._append_token(seq, tok, lp, now)
+            before = len(seq.output_text)
+            new_text = self.detok.step(seq)
+            self._check_stop(seq, tok, new_text)
+            new_text = seq.output_text[before:]
+            d = deltas.get(seq.seq_id)
+            if d is None:
+                deltas[seq.seq_id] = (new_text, [tok], [lp] if lp is not None else None)
+            else:   # two tokens of one sequence surfaced in one step() call
+                deltas[seq.seq_id] = (d[0] + new_text, d[1] + [tok],
+                                      (d[2] or []) + [lp] if lp is not None else d[2])
+            touched[seq.request_id] = self.requests[seq.request_id]
+            self.stats.num_generation_tokens += 1
+
+    def _step_sync(self) -> List[RequestOutput]:
         t0 = time.time()
         sched = self.scheduler.schedule()
         touched: Dict[str, _Request] = {}
@@ -236,7 +316,8 @@ class LLMEngine:
                 if hit is not None:
                     status = SeqStatus.FINISHED_STOPPED
                     seq.stop_reason = hit[0]
-        if status is None and (n_out >= p.max_tokens or seq.num_tokens >= self.cfg.scheduler.max_model_len):
+        if status is None and (n_out >= p.max_tokens or
+                               seq.num_real_tokens >= self.cfg.scheduler.max_model_len):
             status = SeqStatus.FINISHED_LENGTH
         if status is None and seq.guided_state is not None:
             seq.guided_state.advance(tok)

@@ -51,6 +51,27 @@ class StepOutput:
         self.prompt_logprobs = None
 
 
+class StepHandle:
+    """A launched step's sampled tokens.  With overlapped scheduling the tokens stay on the
+    device (feeding the next step's inputs) and are copied to pinned host memory behind an
+    event; ``result()`` waits for that copy only when the host needs the values."""
+
+    __slots__ = ("items", "_out", "_host", "_event")
+
+    def __init__(self, items, out: Optional[StepOutput] = None, host=None, event=None):
+        self.items = items
+        self._out = out
+        self._host = host
+        self._event = event
+
+    def result(self) -> StepOutput:
+        if self._out is None:
+            if self._event is not None:
+                self._event.synchronize()
+            self._out = StepOutput(self._host.tolist(), None)
+        return self._out
+
+
 class ModelRunner:
     def __init__(self, cfg: EngineConfig, device: Optional[torch.device] = None):
         self.cfg = cfg
@@ -92,23 +113,30 @@ class ModelRunner:
         qb = attn_ops.prefill_query_block(self.num_heads, self.num_kv_heads)
         self.max_work = T // qb + S + 1
         pin = self.is_gpu
-        # graph (decode) region, fixed offsets
-        # ids|pos|slot|len|P (P: decode partitions of this step, read by K1 inside the graph)
-        self.g_hdr = torch.zeros(4 * S + 4, dtype=torch.int32, pin_memory=pin)
-        self.g_bt = torch.zeros(S * mb, dtype=torch.int32, pin_memory=pin)
+        # graph (decode) header, fixed offsets:
+        #   ids[S] | pos[S] | slot[S] | len[S] | P (+3 pad) | src[S]
+        # P: decode partitions of this step (read by K1 inside the graph); src: row of the
+        # previous step's sampler output holding this row's input token (-1: host id)
+        self.hdr_len = 5 * S + 4
+        self.src_off = 4 * S + 4
         # eager region: packed per step
-        self.e_size = 3 * T + 2 * S * mb + 3 * S + 1 + 2 * self.max_work + S + 64
-        self.e_buf = torch.zeros(self.e_size, dtype=torch.int32, pin_memory=pin)
-        self.s_f32 = torch.zeros(3 * S, dtype=torch.float32, pin_memory=pin)    # temp|top_p|min_p
-        self.s_i32 = torch.zeros(S, dtype=torch.int32, pin_memory=pin)          # top_k
-        self.s_i64 = torch.zeros(S, dtype=torch.int64, pin_memory=pin)          # seeds
+        self.e_size = 3 * T + 2 * S * mb + 4 * S + 1 + 2 * self.max_work + S + 64
+        # Host staging is double-buffered: with overlapped scheduling step k+1 is prepared
+        # while step k's H2D copies may still be queued behind step k-1 on the stream.
+        self._pin = [self._pinned_set(pin) for _ in range(2)]
+        self._par = 0
+        self._use_pinned(0)
         dev = self.device
-        self.d_g_hdr = torch.zeros(4 * S + 4, dtype=torch.int32, device=dev)
+        self.d_g_hdr = torch.zeros(self.hdr_len, dtype=torch.int32, device=dev)
         self.d_g_bt = torch.zeros(S * mb, dtype=torch.int32, device=dev)
         self.d_e_buf = torch.zeros(self.e_size, dtype=torch.int32, device=dev)
         self.d_s_f32 = torch.zeros(3 * S, dtype=torch.float32, device=dev)
         self.d_s_i32 = torch.zeros(S, dtype=torch.int32, device=dev)
         self.d_s_i64 = torch.zeros(S, dtype=torch.int64, device=dev)
+        # sampled tokens of the last launched step (device) + their host copies
+        self.d_tok = torch.zeros(S, dtype=torch.int32, device=dev)
+        self.h_tok = [torch.zeros(S, dtype=torch.int32, pin_memory=pin) for _ in range(2)]
+        self.last_rows: Dict[int, int] = {}      # seq_id -> row of d_tok (last launched step)
         pmax = 16
         self.part_o = torch.empty(S * self.num_heads * pmax * self.head_dim, dtype=torch.float32,
                                   device=dev) if self.is_gpu else None
@@ -117,6 +145,41 @@ class ModelRunner:
         # arrival counters of the in-kernel partition merge (kernels leave them zeroed)
         self.part_cnt = torch.zeros(S * self.num_heads, dtype=torch.int32,
                                     device=dev) if self.is_gpu else None
+
+    def _pinned_set(self, pin: bool) -> Dict[str, torch.Tensor]:
+        S, mb = self.max_num_seqs, self.maxb
+        return {
+            "g_hdr": torch.zeros(self.hdr_len, dtype=torch.int32, pin_memory=pin),
+            "g_bt": torch.zeros(S * mb, dtype=torch.int32, pin_memory=pin),
+            "e_buf": torch.zeros(self.e_size, dtype=torch.int32, pin_memory=pin),
+            "s_f32": torch.zeros(3 * S, dtype=torch.float32, pin_memory=pin),   # temp|top_p|min_p
+            "s_i32": torch.zeros(S, dtype=torch.int32, pin_memory=pin),         # top_k
+            "s_i64": torch.zeros(S, dtype=torch.int64, pin_memory=pin),         # seeds
+        }
+
+    def _use_pinned(self, k: int) -> None:
+        for name, t in self._pin[k].items():
+            setattr(self, name, t)
+
+    def _flip_staging(self) -> None:
+        self._par ^= 1
+        self._use_pinned(self._par)
+
+    def _fill_decode_inputs(self, decodes: List[ScheduledSeq], ids: np.ndarray,
+                            src: np.ndarray) -> bool:
+        """Input ids of decode rows; rows whose token is still in flight read it on device."""
+        lr = self.last_rows
+        any_src = False
+        for i, d in enumerate(decodes):
+            s = d.seq
+            if d.start >= s.num_real_tokens:
+                ids[i] = 0
+                src[i] = lr[s.seq_id]
+                any_src = True
+            else:
+                ids[i] = s.token_at(d.start)
+                src[i] = -1
+        return any_src
 
     # ------------------------------------------------------------------ KV cache
     def kv_block_bytes(self) -> int:
@@ -210,7 +273,8 @@ class ModelRunner:
         S = self.max_num_seqs
         hdr = self.g_hdr.numpy()
         n = len(decodes)
-        hdr[0:n] = np.fromiter((d.seq.token_at(d.start) for d in decodes), dtype=np.int32, count=n)
+        so = self.src_off
+        self._fill_decode_inputs(decodes, hdr[0:n], hdr[so:so + n])
         seq_ids = np.fromiter((d.seq.seq_id for d in decodes), dtype=np.int64, count=n)
         starts = np.fromiter((d.start for d in decodes), dtype=np.int32, count=n)
         base = self.g_hdr.data_ptr()
@@ -221,6 +285,7 @@ class ModelRunner:
             hdr[S + n:S + Bp] = 0
             hdr[2 * S + n:2 * S + Bp] = -1
             hdr[3 * S + n:3 * S + Bp] = 0
+            hdr[so + n:so + Bp] = -1
         max_len = int(hdr[3 * S:3 * S + n].max()) if n else 1
         hdr[4 * S] = min(self._decode_partitions(Bp, max_len), self.graph_P.get(Bp, 1))
         return {"kind": "graph", "Bp": Bp, "nd": n}
@@ -239,11 +304,17 @@ class ModelRunner:
             decode_part_ml=self.part_ml, decode_p_dyn=d[4 * S:4 * S + 1])
         return d[:Bp], md
 
+    def _graph_forward(self, Bp: int, P: int) -> torch.Tensor:
+        """Body of a decode graph: in-flight input ids from d_tok, forward, logits."""
+        ids, md = self._graph_metadata(Bp, P)
+        sampling_ops.fill_ids(ids, self.d_g_hdr[self.src_off:self.src_off + Bp], self.d_tok)
+        h = self.model(ids, md, self.kv_caches)
+        return self.model.compute_logits(h)
+
     def _prepare_eager(self, bm: BlockManager, out: SchedulerOutput) -> dict:
         """Pack the step's metadata into the eager staging buffer; returns the plan."""
         buf = self.e_buf.numpy()
         base = self.e_buf.data_ptr()
-        items = out.decodes + out.prefills
         T = out.num_batched_tokens
         nd, npf = len(out.decodes), len(out.prefills)
         o = {}
@@ -257,8 +328,11 @@ class ModelRunner:
         take("ids", T)
         take("pos", T)
         take("slot", T)
-        p = o["ids"]
-        for it in items:
+        take("src", nd)
+        has_src = self._fill_decode_inputs(out.decodes, buf[o["ids"]:o["ids"] + nd],
+                                           buf[o["src"]:o["src"] + nd]) if nd else False
+        p = o["ids"] + nd
+        for it in out.prefills:
             s = it.seq
             if it.num_tokens == 1:
                 buf[p] = s.token_at(it.start)
@@ -303,7 +377,8 @@ class ModelRunner:
         max_len = max([it.start + it.num_tokens for it in out.decodes], default=1)
         P = self._decode_partitions(nd, max_len) if nd else 1
         return {"kind": "eager", "T": T, "nd": nd, "npf": npf, "mb_d": mb_d, "mb_p": mb_p,
-                "o": o, "n_work": len(work) // 2, "n_lidx": len(sample_rows), "P": P, "off": off}
+                "o": o, "n_work": len(work) // 2, "n_lidx": len(sample_rows), "P": P, "off": off,
+                "src": has_src}
 
     def _eager_inputs(self, plan: dict):
         d = self.d_e_buf
@@ -321,10 +396,14 @@ class ModelRunner:
             prefill_work=d[o["work"]:o["work"] + 2 * nw] if npf else None,
             prefill_n_work=nw)
         lidx = d[o["lidx"]:o["lidx"] + plan["n_lidx"]].long()
-        return d[o["ids"]:o["ids"] + T], md, lidx
+        ids = d[o["ids"]:o["ids"] + T]
+        if plan.get("src"):
+            sampling_ops.fill_ids(ids[:nd], d[o["src"]:o["src"] + nd], self.d_tok)
+        return ids, md, lidx
 
     def prepare(self, bm: BlockManager, out: SchedulerOutput) -> dict:
         """Host side of a step (driver only): fill the pinned staging buffers."""
+        self._flip_staging()
         nd = len(out.decodes)
         if not out.prefills and self.graphs and nd <= max(self.graphs):
             Bp = min(b for b in self.graphs if b >= nd)
@@ -341,9 +420,9 @@ class ModelRunner:
     def load_payload(self, plan: dict, payload: bytes) -> None:
         a = np.frombuffer(payload, dtype=np.int32)
         if plan["kind"] == "graph":
-            S = self.max_num_seqs
-            self.g_hdr.numpy()[:] = a[:4 * S + 4]
-            self.g_bt.numpy()[:len(a) - 4 * S - 4] = a[4 * S + 4:]
+            hl = self.hdr_len
+            self.g_hdr.numpy()[:] = a[:hl]
+            self.g_bt.numpy()[:len(a) - hl] = a[hl:]
         else:
             self.e_buf.numpy()[:len(a)] = a
 
@@ -409,13 +488,20 @@ class ModelRunner:
         S = self.max_num_seqs
         k = self.s_i32.numpy()
         sd = self.s_i64.numpy()
+        V = self.vocab
+        unfiltered = True
         for i, it in enumerate(items):
-            p = it.seq.params
+            seq = it.seq
+            p = seq.params
             f[i] = 0.0 if p.greedy else p.temperature
             f[S + i] = p.top_p
             f[2 * S + i] = p.min_p
             k[i] = p.top_k if p.top_k > 0 else 0
-            sd[i] = sampling_ops.row_seed(it.seq.seed, len(it.seq.output_token_ids))
+            if (0 < p.top_k < V) or p.top_p < 1.0 or p.min_p > 0.0:
+                unfiltered = False
+            # index of the token being sampled (in-flight samples included)
+            sd[i] = sampling_ops.row_seed(seq.seed, len(seq.output_token_ids) + seq.num_pending)
+        self._unfiltered = unfiltered
         if self.is_gpu:
             self.d_s_f32.copy_(self.s_f32, non_blocking=True)
             self.d_s_i32[:n].copy_(self.s_i32[:n], non_blocking=True)
@@ -425,12 +511,20 @@ class ModelRunner:
             F_, K_, SD = self.s_f32, self.s_i32, self.s_i64
         return F_[:n], K_[:n], F_[S:S + n], F_[2 * S:2 * S + n], SD[:n]
 
+    def _sample_tokens(self, logits: torch.Tensor, items: List[ScheduledSeq]) -> torch.Tensor:
+        """Sample into d_tok[:n] (device); also records which seq owns which row."""
+        temp, top_k, top_p, min_p, seeds = self._sampling_tensors(items)
+        n = len(items)
+        toks = sampling_ops.sample(logits, temp, top_k, top_p, min_p, seeds, out=self.d_tok[:n],
+                                   unfiltered=self._unfiltered)
+        self.last_rows = {it.seq.seq_id: r for r, it in enumerate(items)}
+        return toks
+
     def sample(self, logits: torch.Tensor, items: List[ScheduledSeq]) -> StepOutput:
         from .logits_process import apply_logits_processors
 
         logits = apply_logits_processors(logits, items)
-        temp, top_k, top_p, min_p, seeds = self._sampling_tensors(items)
-        toks = sampling_ops.sample(logits, temp, top_k, top_p, min_p, seeds)
+        toks = self._sample_tokens(logits, items)
         lp = None
         want = [it.seq.params.logprobs for it in items]
         if any(w is not None for w in want):
@@ -456,6 +550,29 @@ class ModelRunner:
 
     # ------------------------------------------------------------------ execute
     @torch.no_grad()
+    def launch(self, bm: BlockManager, out: SchedulerOutput, overlap: bool) -> StepHandle:
+        """Enqueue a step.  ``overlap``: leave the sampled tokens on the device (the next step
+        reads them there) and copy them to pinned memory behind an event instead of
+        synchronising; the caller guarantees no row needs host-side logits processing."""
+        sample_items = out.decodes + [p for p in out.prefills if p.samples]
+        plan = self.prepare(bm, out)
+        logits = self.run(plan)
+        if not sample_items:
+            self.last_rows = {}
+            return StepHandle([], StepOutput([], None))
+        if not overlap:
+            return StepHandle(sample_items, self.sample(logits, sample_items))
+        toks = self._sample_tokens(logits, sample_items)
+        host = self.h_tok[self._par][:len(sample_items)]
+        if self.is_gpu:
+            host.copy_(toks, non_blocking=True)
+            ev = torch.cuda.Event()
+            ev.record()
+            return StepHandle(sample_items, host=host, event=ev)
+        host.copy_(toks)
+        return StepHandle(sample_items, host=host)
+
+    @torch.no_grad()
     def execute(self, bm: BlockManager, out: SchedulerOutput) -> StepOutput:
         sample_items = out.decodes + [p for p in out.prefills if p.samples]
         plan = self.prepare(bm, out)
@@ -475,10 +592,11 @@ class ModelRunner:
         self.graph_pool = torch.cuda.graph_pool_handle()
         # dummy decode inputs: len 1, slot -1 (no cache write), block 0
         S = self.max_num_seqs
-        hdr = torch.zeros(4 * S + 4, dtype=torch.int32)
+        hdr = torch.zeros(self.hdr_len, dtype=torch.int32)
         hdr[2 * S:3 * S] = -1
         hdr[3 * S:4 * S] = 1
         hdr[4 * S] = 1
+        hdr[self.src_off:] = -1
         self.d_g_hdr.copy_(hdr)
         self.d_g_bt.zero_()
         stream = torch.cuda.Stream()
@@ -487,14 +605,11 @@ class ModelRunner:
             for Bp in sorted(buckets, reverse=True):
                 P = self._decode_partitions(Bp, self.cfg.scheduler.max_model_len)
                 self.graph_P[Bp] = P          # upper bound; the step's P is read on device
-                ids, md = self._graph_metadata(Bp, P)
                 for _ in range(2):       # warm-up (hipBLASLt heuristics, allocator)
-                    h = self.model(ids, md, self.kv_caches)
-                    self.model.compute_logits(h)
+                    self._graph_forward(Bp, P)
                 g = torch.cuda.CUDAGraph()
                 with torch.cuda.graph(g, pool=self.graph_pool, stream=stream):
-                    h = self.model(ids, md, self.kv_caches)
-                    logits = self.model.compute_logits(h)
+                    logits = self._graph_forward(Bp, P)
                 self.graphs[Bp] = g
                 self.graph_logits[Bp] = logits
         torch.cuda.current_stream().wait_stream(stream)

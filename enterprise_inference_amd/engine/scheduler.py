@@ -114,6 +114,10 @@ class Scheduler:
         i = 0
         while i < len(self.running) and budget > 0:
             seq = self.running[i]
+            if seq.num_pending and (len(seq.output_token_ids) + seq.num_pending >= seq.params.max_tokens
+                                    or seq.num_tokens >= self.cfg.max_model_len):
+                i += 1        # its final token is in flight: nothing left to compute
+                continue
             remaining = seq.num_tokens - seq.num_computed_tokens
             n = min(remaining, budget)
             if n < remaining and not self.cfg.enable_chunked_prefill and remaining > 1:

@@ -40,7 +40,8 @@ class Sequence:
                  "first_scheduled_time", "first_token_time", "last_token_time", "finish_time",
                  "stop_reason", "output_logprobs", "cumulative_logprob", "prompt_logprobs",
                  "detok_offset", "output_text", "prefix_offset", "read_offset", "lora",
-                 "num_preemptions", "seed", "guided_state", "token_times", "priority")
+                 "num_preemptions", "seed", "guided_state", "token_times", "priority",
+                 "num_pending")
 
     def __init__(self, request_id: str, prompt_token_ids: List[int], params: SamplingParams,
                  index: int = 0, arrival_time: Optional[float] = None, seed: int = 0,
@@ -73,9 +74,17 @@ class Sequence:
         self.guided_state = None
         self.token_times: List[float] = []
         self.priority = priority
+        # tokens sampled by a launched, not yet read-back step (overlapped scheduling): they
+        # count toward num_tokens so the next step can be planned before the values are known
+        self.num_pending = 0
 
     @property
     def num_tokens(self) -> int:
+        return len(self.prompt_token_ids) + len(self.output_token_ids) + self.num_pending
+
+    @property
+    def num_real_tokens(self) -> int:
+        """Tokens whose ids are known on the host (excludes in-flight samples)."""
         return len(self.prompt_token_ids) + len(self.output_token_ids)
 
     @property
@@ -87,8 +96,12 @@ class Sequence:
         return self.prompt_token_ids + self.output_token_ids
 
     def token_at(self, i: int) -> int:
+        """Token id at position i; 0 for an in-flight sample (its id is filled in on device)."""
         n = len(self.prompt_token_ids)
-        return self.prompt_token_ids[i] if i < n else self.output_token_ids[i - n]
+        if i < n:
+            return self.prompt_token_ids[i]
+        j = i - n
+        return self.output_token_ids[j] if j < len(self.output_token_ids) else 0
 
     @property
     def is_prefill(self) -> bool:

@@ -146,7 +146,7 @@ def engine_config_from_args(args: argparse.Namespace):
         max_num_prefill_seqs=args.max_num_prefill_seqs or 64, max_model_len=max_len,
         enable_chunked_prefill=bool(args.enable_chunked_prefill),
         decode_bs_bucket_step=int(os.environ.get("VLLM_DECODE_BS_BUCKET_STEP", 16)),
-        delayed_sampling=_truthy(os.environ.get("VLLM_DELAYED_SAMPLING", "false")))
+        delayed_sampling=_truthy(os.environ.get("VLLM_DELAYED_SAMPLING", "true")))
     cache = CacheConfig(block_size=args.block_size,
                         gpu_memory_utilization=args.gpu_memory_utilization,
                         cpu_kvcache_space_gb=float(os.environ.get("VLLM_CPU_KVCACHE_SPACE", 4)),

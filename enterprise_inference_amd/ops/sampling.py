@@ -72,10 +72,16 @@ def sample_reference(logits: torch.Tensor, temperature: torch.Tensor, top_k: tor
     return torch.where(t > 0, sampled, greedy)
 
 
+SPLIT_CHUNK = 4096     # tokens per workgroup of the split-row sampler
+
+
 def sample(logits: torch.Tensor, temperature: torch.Tensor, top_k: torch.Tensor,
            top_p: torch.Tensor, min_p: torch.Tensor, seeds: torch.Tensor,
-           out: Optional[torch.Tensor] = None) -> torch.Tensor:
-    """logits fp32 [B, V]; per-row params on the same device. Returns int32 [B]."""
+           out: Optional[torch.Tensor] = None, unfiltered: bool = False) -> torch.Tensor:
+    """logits fp32 [B, V]; per-row params on the same device. Returns int32 [B].
+
+    ``unfiltered`` (caller-asserted: no row uses top-k / top-p / min-p) selects the split-row
+    kernel, which spreads each row over V/4096 workgroups; same result as the full kernel."""
     if not use_hip(logits):
         r = sample_reference(logits, temperature, top_k, top_p, min_p, seeds)
         if out is not None:
@@ -88,6 +94,13 @@ def sample(logits: torch.Tensor, temperature: torch.Tensor, top_k: torch.Tensor,
                   (min_p, torch.float32), (seeds, torch.int64)):
         require(t.dtype == dt and t.is_cuda and t.numel() >= B, f"sample: param {dt}")
     o = torch.empty(B, dtype=torch.int32, device=logits.device) if out is None else out
+    if unfiltered:
+        C = (V + SPLIT_CHUNK - 1) // SPLIT_CHUNK
+        ws = torch.empty(2 * B * C, dtype=torch.int32, device=logits.device)
+        check(lib().eia_sample_split(ptr(logits), logits.stride(0), B, V, SPLIT_CHUNK,
+                                     ptr(temperature), ptr(seeds), ptr(ws), ws.data_ptr() + 4 * B * C,
+                                     ptr(o), stream(logits)), "sample_split")
+        return o
     check(lib().eia_sample(ptr(logits), logits.stride(0), B, V, ptr(temperature), ptr(top_k),
                            ptr(top_p), ptr(min_p), ptr(seeds), ptr(o), stream(logits)), "sample")
     return o
@@ -113,3 +126,21 @@ def apply_penalties(logits: torch.Tensor, rows: torch.Tensor, toks: torch.Tensor
                                     ptr(counts), n, ptr(rep), ptr(freq), ptr(pres),
                                     stream(logits)), "apply_penalties")
     return logits
+
+
+def fill_ids(ids: torch.Tensor, src: torch.Tensor, tok: torch.Tensor) -> torch.Tensor:
+    """ids[i] = tok[src[i]] where src[i] >= 0 (in place; int32).  Feeds a step the tokens the
+    previous, still in-flight step sampled on the device (overlapped scheduling)."""
+    n = ids.numel()
+    if n == 0:
+        return ids
+    if not use_hip(ids):
+        m = src >= 0
+        if bool(m.any()):
+            ids[m] = tok[src[m].long()].to(ids.dtype)
+        return ids
+    require(ids.dtype == torch.int32 and src.dtype == torch.int32 and tok.dtype == torch.int32,
+            "fill_ids: int32 tensors")
+    require(src.numel() >= n and ids.is_contiguous(), "fill_ids: shapes")
+    check(lib().eia_fill_ids(ptr(ids), ptr(src), ptr(tok), n, stream(ids)), "fill_ids")
+    return ids

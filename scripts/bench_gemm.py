@@ -78,6 +78,7 @@ def main():
     ap.add_argument("--shapes", nargs="+", default=list(SHAPES))
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--tune", action="store_true")
+    ap.add_argument("--sweep", action="store_true", help="time every candidate (no table write)")
     ap.add_argument("--out", default=None, help="also write the tuning table here")
     a = ap.parse_args()
     tuned = {}
@@ -96,7 +97,13 @@ def main():
             else:
                 base = lambda i: F.linear(x, ws[i % pool])
             tb = graph_time(base, a.iters)
-            cands = candidates(M, N, K, swiglu) if a.tune else [gemm.choose(M, N, K, swiglu)]
+            cands = candidates(M, N, K, swiglu) if (a.tune or a.sweep) else \
+                [c for c in [gemm.choose(M, N, K, swiglu)] if c[0] >= 0]
+            if not cands:
+                print(json.dumps({"shape": name, "M": M, "hipblaslt_us": round(tb, 2),
+                                  "hipblaslt_TBps": round(wbytes / tb / 1e6, 2),
+                                  "note": "tuned table routes this shape to hipBLASLt"}), flush=True)
+                continue
             results = []
             for cfg, sk in cands:
                 if swiglu:

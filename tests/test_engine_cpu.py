@@ -42,8 +42,8 @@ def test_parity_with_transformers(arch):
     eng.executor.runner.model.load_weights(hf.state_dict().items())
     cap = []
     r = eng.executor.runner
-    orig = r.sample
-    r.sample = lambda logits, items: (cap.append(logits.clone()), orig(logits, items))[1]
+    orig = r._sample_tokens      # every sampling path (sync and overlapped) goes through it
+    r._sample_tokens = lambda logits, items: (cap.append(logits.clone()), orig(logits, items))[1]
     prompts = [[5, 6, 7, 8, 9] * 10, [3, 4, 5], list(range(10, 100))]
     eng.generate(prompt_token_ids=prompts, params=SamplingParams(max_tokens=1, temperature=0))
     with torch.no_grad():
@@ -124,3 +124,54 @@ def test_logprobs_and_penalties_run():
     assert len(c.logprobs) == 4
     assert all(tok in lp for tok, lp in zip(c.token_ids, c.logprobs))
     assert all(len(lp) >= 3 for lp in c.logprobs)
+
+
+def _mixed_requests():
+    sp = [SamplingParams(max_tokens=12, temperature=0, ignore_eos=True),
+          SamplingParams(max_tokens=9, temperature=0.9, seed=7, ignore_eos=True),
+          SamplingParams(max_tokens=15, temperature=1.1, top_k=20, seed=3, ignore_eos=True),
+          SamplingParams(max_tokens=6, temperature=0.7, seed=11, n=2, ignore_eos=True),
+          SamplingParams(max_tokens=10, temperature=0.8, seed=5, ignore_eos=True,
+                         repetition_penalty=1.2, presence_penalty=0.3)]
+    prompts = [list(range(10 + 3 * i, 40 + 5 * i)) for i in range(len(sp))]
+    return prompts, sp
+
+
+@pytest.mark.parametrize("nblocks,prefix", [(64, True), (12, False)])
+def test_overlapped_scheduling_matches_sync(nblocks, prefix):
+    """Overlapped scheduling (step k+1 planned before step k's tokens are read back, inputs
+    taken from the device) produces exactly the tokens of the synchronous engine, including
+    under preemption and with penalty rows that force a read-back."""
+    d = tiny_config()
+    prompts, sp = _mixed_requests()
+    outs = {}
+    for overlap in (False, True):
+        eng = _engine(d, nblocks=nblocks, prefix=prefix, mbt=48)
+        eng._overlap = overlap
+        outs[overlap] = eng.generate(prompt_token_ids=prompts, params=sp)
+        assert eng._pending is None and not eng.has_unfinished_requests()
+        assert eng.scheduler.bm.check_invariants() == ""
+    for a, b in zip(outs[False], outs[True]):
+        assert [c.token_ids for c in a.outputs] == [c.token_ids for c in b.outputs]
+        assert [c.finish_reason for c in a.outputs] == [c.finish_reason for c in b.outputs]
+
+
+def test_overlapped_scheduling_stops_and_streams():
+    d = tiny_config()
+    eng = _engine(d)
+    assert eng._overlap
+    p = [5, 6, 7, 8, 9]
+    ref = eng.generate(prompt_token_ids=[p], params=SamplingParams(max_tokens=8, temperature=0))[0]
+    stop_tok = ref.outputs[0].token_ids[3]
+    eng.add_request("s", prompt_token_ids=p,
+                    params=SamplingParams(max_tokens=8, temperature=0, stop_token_ids=[stop_tok]))
+    streamed = []
+    final = None
+    while eng.has_unfinished_requests():
+        for o in eng.step():
+            streamed += o.outputs[0].new_token_ids
+            if o.finished:
+                final = o
+    assert final.outputs[0].finish_reason == "stop"
+    assert final.outputs[0].token_ids == ref.outputs[0].token_ids[:4]
+    assert streamed == final.outputs[0].token_ids       # no token lost or duplicated

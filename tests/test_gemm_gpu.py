@@ -60,8 +60,9 @@ def test_swiglu_gemm(M, I, K):
             _check(gemm.swiglu_gemm(x, w, cfg=cfg), ref, f"swiglu M={M} I={I} cfg={cfg}")
 
 
-@pytest.mark.parametrize("M,H", [(1, 4096), (65, 4096), (128, 8192)])
-def test_splitk_add_rmsnorm(M, H):
+@pytest.mark.parametrize("M,H,sk", [(1, 4096, 4), (65, 4096, 4), (128, 8192, 4), (65, 4096, 2),
+                                    (65, 4096, 8), (7, 5120, 16)])
+def test_splitk_add_rmsnorm(M, H, sk):
     from enterprise_inference_amd.ops import gemm
     from enterprise_inference_amd.ops import reference as ref
     K = 4096
@@ -69,7 +70,7 @@ def test_splitk_add_rmsnorm(M, H):
     w = (torch.randn(H, K, device=DEV) * K ** -0.5).to(BF)
     res = torch.randn(M, H, device=DEV, dtype=BF)
     nw = (torch.rand(H, device=DEV) + 0.5).to(BF)
-    s = gemm.skinny(x, w, defer_reduce=True, cfg=2, sk=4)
+    s = gemm.skinny(x, w, defer_reduce=True, cfg=2, sk=sk)   # sk 16: generic (non-unrolled) path
     assert isinstance(s, gemm.SplitK) and s.sk > 1
     y = _ref(x, w)
     r_ref = (y + res.float()).to(BF)
@@ -97,7 +98,7 @@ def test_rope_cache_from_splitk(M, bias):
     for split in (False, True):
         kc = torch.zeros(4, Hkv, bs, D, device=DEV, dtype=BF)
         vc = torch.zeros(4, Hkv, D, bs, device=DEV, dtype=BF)
-        s = gemm.skinny(x, w, defer_reduce=True, cfg=2, sk=4)
+        s = gemm.skinny(x, w, defer_reduce=True, cfg=2, sk=sk)   # sk 16: generic (non-unrolled) path
         qkv = s if split else s.materialize()
         q = rope_qkv_cache(qkv, pos, rot, slots, kc, vc, Hq, Hkv, D, bias=b)
         outs.append((q, kc, vc))

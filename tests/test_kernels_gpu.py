@@ -318,3 +318,34 @@ def test_paged_decode_dynamic_partitions(p_use):
     r = ref.paged_attention_decode(q.cpu().float(), k.cpu().float(), v.cpu().float(), bt.cpu(),
                                    sl.cpu(), D ** -0.5)
     _close(o, r, 2e-2, 2e-2, f"decode p_dyn={p_use}")
+
+
+@pytest.mark.parametrize("B,V", [(1, 1000), (65, 128256), (9, 32000), (300, 4097)])
+def test_sample_split_matches_full_kernel(B, V):
+    """Split-row sampler (no top-k/top-p/min-p rows) == single-workgroup kernel == CPU oracle."""
+    from enterprise_inference_amd.ops import sampling
+    torch.manual_seed(B)
+    logits = torch.randn(B, V, device=DEV) * 4
+    logits[0, 7] = float("-inf")
+    temp = torch.rand(B, device=DEV) * 1.5
+    temp[::3] = 0.0                                   # greedy rows mixed in
+    zk = torch.zeros(B, dtype=torch.int32, device=DEV)
+    ones = torch.ones(B, device=DEV)
+    zp = torch.zeros(B, device=DEV)
+    seeds = torch.tensor([sampling.row_seed(99 + i, i) for i in range(B)], dtype=torch.int64,
+                         device=DEV)
+    full = sampling.sample(logits, temp, zk, ones, zp, seeds)
+    split = sampling.sample(logits, temp, zk, ones, zp, seeds, unfiltered=True)
+    assert split.cpu().tolist() == full.cpu().tolist()
+    ref = sampling.sample_reference(logits.cpu(), temp.cpu(), zk.cpu(), ones.cpu(), zp.cpu(),
+                                    seeds.cpu())
+    assert split.cpu().tolist() == ref.tolist()
+
+
+def test_fill_ids():
+    from enterprise_inference_amd.ops import sampling
+    ids = torch.tensor([5, 6, 7, 8, 9], dtype=torch.int32, device=DEV)
+    src = torch.tensor([-1, 2, -1, 0, 3], dtype=torch.int32, device=DEV)
+    tok = torch.tensor([100, 101, 102, 103], dtype=torch.int32, device=DEV)
+    sampling.fill_ids(ids, src, tok)
+    assert ids.cpu().tolist() == [5, 102, 7, 100, 103]
