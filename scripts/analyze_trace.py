@@ -30,7 +30,8 @@ def short(name: str) -> str:
     if name.startswith(("Cijk_", "Custom_Cijk")):
         m = re.search(r"MT(\d+x\d+x\d+)", name)
         return f"hipBLASLt MT{m.group(1) if m else '?'}"
-    return re.sub(r"\(.*", "", name).replace("void ", "")[:60]
+    name = name.replace("void ", "").replace("(anonymous namespace)::", "")
+    return re.sub(r"\(.*", "", name)[:60]
 
 
 def main() -> int:

@@ -34,7 +34,7 @@ for s in $STEPS; do
       python3 scripts/analyze_trace.py "$OUT" --tail ${TRACE_TAIL:-1.0} > gpurun_out/prof_trace.md 2>&1 || true
       find "$OUT" -name '*kernel_trace.csv' -delete
       head -12 gpurun_out/prof_trace.md ;;
-    gemm) run gemm 600 python scripts/bench_gemm.py --m 1 16 32 65 96 128 \
+    gemm) run gemm 900 python scripts/bench_gemm.py --sweep --m ${GEMM_M:-65} \
             --shapes qkv_8b o_8b gate_up_8b down_8b lm_head_8b ;;
     attn) run attn 300 python scripts/bench_attn.py ;;
     *) echo "unknown step $s"; exit 2 ;;

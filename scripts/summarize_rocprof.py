@@ -13,8 +13,8 @@ def short(name: str) -> str:
     m = re.search(r"MT(\d+x\d+x\d+)", name)
     if name.startswith(("Cijk_", "Custom_Cijk")):
         return f"hipBLASLt GEMM MT{m.group(1) if m else '?'}"
+    name = name.replace("void ", "").replace("(anonymous namespace)::", "")
     name = re.sub(r"\(.*", "", name)
-    name = name.replace("void ", "")
     return name[:70]
 
 
