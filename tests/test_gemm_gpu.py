@@ -98,7 +98,7 @@ def test_rope_cache_from_splitk(M, bias):
     for split in (False, True):
         kc = torch.zeros(4, Hkv, bs, D, device=DEV, dtype=BF)
         vc = torch.zeros(4, Hkv, D, bs, device=DEV, dtype=BF)
-        s = gemm.skinny(x, w, defer_reduce=True, cfg=2, sk=sk)   # sk 16: generic (non-unrolled) path
+        s = gemm.skinny(x, w, defer_reduce=True, cfg=2, sk=4)
         qkv = s if split else s.materialize()
         q = rope_qkv_cache(qkv, pos, rot, slots, kc, vc, Hq, Hkv, D, bias=b)
         outs.append((q, kc, vc))
