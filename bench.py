@@ -146,6 +146,12 @@ def main() -> int:
     for w in range(args.warmup):
         one_round(f"warm{w}")
     _sync_and_barrier(torch, dist, bgroup)
+    prof = None
+    if os.environ.get("EIA_BENCH_CPROFILE"):      # host-side profile of the timed rounds
+        import cProfile
+        prof = cProfile.Profile()
+        prof.enable()
+    engine.phase_times.clear()
     t0 = time.time()
     tot_tokens, all_ttft, all_tpot = 0, [], []
     for s in range(args.steps):
@@ -158,6 +164,15 @@ def main() -> int:
                   f"ttft p50 {1000 * statistics.median(tt):.1f} ms", file=sys.stderr)
     _sync_and_barrier(torch, dist, bgroup)
     elapsed = time.time() - t0
+    if prof is not None:
+        import pstats
+        prof.disable()
+        with open(os.environ["EIA_BENCH_CPROFILE"], "w") as f:
+            pstats.Stats(prof, stream=f).sort_stats("tottime").print_stats(45)
+    if args.verbose and engine.phase_times:
+        n = max(1, engine.stats.num_steps)
+        print("[rank %d] host ms/step: %s" % (rank, {k: round(1e3 * v / n, 3) for k, v in
+                                                     engine.phase_times.items()}), file=sys.stderr)
     if tp > 1:
         ex.shutdown()
     local_stats = {"tokens": tot_tokens, "elapsed": elapsed, "ttft": all_ttft, "tpot": all_tpot,

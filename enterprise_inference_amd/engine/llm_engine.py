@@ -124,6 +124,7 @@ class LLMEngine:
         self._overlap = bool(cfg.scheduler.delayed_sampling) and \
             getattr(executor, "supports_overlap", False)
         self._pending = None        # StepHandle of the launched, not yet processed step
+        self.phase_times: Dict[str, float] = {}   # host seconds per step phase (overlap path)
 
     # ------------------------------------------------------------------ requests
     def add_request(self, request_id: str, prompt: Optional[str] = None,
@@ -204,14 +205,18 @@ class LLMEngine:
             if prev is not None:
                 self._process(prev, touched, deltas)
             return self._emit(touched, deltas)
+        pt = self.phase_times
+        t1 = time.time()
         sample_items = sched.decodes + [p for p in sched.prefills if p.samples]
         overlap = not any(self._needs_host_tokens(it.seq) for it in sample_items)
         handle = self.profiler.step(
             lambda: self.executor.launch(self.scheduler.bm, sched, overlap))
+        t2 = time.time()
         for it in sample_items:
             it.seq.num_pending += 1
         if prev is not None:
             self._process(prev, touched, deltas)    # the GPU is busy with `handle` meanwhile
+        t3 = time.time()
         self.scheduler.update_after_step(sched)
         if self._check_invariants:
             from ..utils.profiling import check_engine_invariants
@@ -223,13 +228,21 @@ class LLMEngine:
             self._pending = handle
         else:
             self._process(handle, touched, deltas)
-        self.stats.step_time_s += time.time() - t0
-        return self._emit(touched, deltas)
+        t4 = time.time()
+        outs = self._emit(touched, deltas)
+        t5 = time.time()
+        for k, v in (("schedule", t1 - t0), ("launch", t2 - t1), ("process", t3 - t2),
+                     ("update", t4 - t3), ("emit", t5 - t4)):
+            pt[k] = pt.get(k, 0.0) + v
+        self.stats.step_time_s += t5 - t0
+        return outs
 
     def _process(self, handle, touched: Dict[str, "_Request"], deltas: Dict[int, tuple]) -> None:
         """Apply a launched step's sampled tokens: append, detokenise, stop checks."""
+        tw = time.time()
         res = handle.result()
         now = time.time()
+        self.phase_times["wait"] = self.phase_times.get("wait", 0.0) + now - tw
         for r, it in enumerate(handle.items):
             seq = it.seq
             if seq.num_pending:
