@@ -53,9 +53,22 @@ EIA_DEV void load_unit(KVFrag<D>& f, const bf16_t* __restrict__ kc, const bf16_t
   const int tv = tb + 8 * g;
   const int lastb = (L - 1) / bs;   // tokens past L may lie in unallocated table slots: clamp
   const long hk = (long)bs * D;
-  const bf16_t* kp0 = kc + ((long)bt[min(tk0 / bs, lastb)] * Hkv + kvh) * hk + (long)(tk0 % bs) * D + 8 * g;
-  const bf16_t* kp1 = kc + ((long)bt[min(tk1 / bs, lastb)] * Hkv + kvh) * hk + (long)(tk1 % bs) * D + 8 * g;
-  const bf16_t* vp = vc + ((long)bt[min(tv / bs, lastb)] * Hkv + kvh) * hk + (tv % bs);
+  const bf16_t *kp0, *kp1, *vp;
+  if (bs >= 32) {
+    // The 32-token unit lies inside one block (tb < L, 32 | bs): ONE wave-uniform table read,
+    // a scalar load counted by lgkmcnt.  A per-lane (vector) read would sit in the in-order
+    // vmcnt queue behind the previous unit's K/V loads and serialise the prefetch pipeline.
+    const int blk = bt[__builtin_amdgcn_readfirstlane(tb / bs)];
+    const long base = ((long)blk * Hkv + kvh) * hk;
+    const int o = tb % bs;
+    kp0 = kc + base + (long)(o + tk0 - tb) * D + 8 * g;
+    kp1 = kp0 + 4 * D;
+    vp = vc + base + (o + 8 * g);
+  } else {
+    kp0 = kc + ((long)bt[min(tk0 / bs, lastb)] * Hkv + kvh) * hk + (long)(tk0 % bs) * D + 8 * g;
+    kp1 = kc + ((long)bt[min(tk1 / bs, lastb)] * Hkv + kvh) * hk + (long)(tk1 % bs) * D + 8 * g;
+    vp = vc + ((long)bt[min(tv / bs, lastb)] * Hkv + kvh) * hk + (tv % bs);
+  }
 #pragma unroll
   for (int s = 0; s < D / 32; ++s) {
     f.k0[s] = *reinterpret_cast<const bf16x8*>(kp0 + 32 * s);

@@ -31,9 +31,7 @@
 
 namespace {
 
-constexpr int KC = 256;             // K chunk per pipeline stage
 constexpr int XPAD = 8;             // LDS row padding (elements)
-constexpr int XLD = KC + XPAD;      // LDS row stride (elements)
 // k permutation inside a 128-deep super-step: lane group g, MFMA step s, element j covers
 // k = KLANE*g + KSTEP*s + j.  KLANE = 8 / KSTEP = 32 makes each W load instruction read one
 // contiguous 64-B run per row (4 lanes x 16 B; the 4 steps walk the row), i.e. 16 half cache
@@ -65,13 +63,17 @@ EIA_DEV bf16x8 ld_w(const bf16_t* p) {
 // through row_idx (nullptr = identity) and outputs land in sorted order; experts with
 // more than 16*MT rows loop over row chunks (weights re-streamed per chunk).
 // S: W pipeline stages (register sets); S-1 chunks of weights stay in flight.
-template <int MT, int NT, int WAVES, int S, bool GROUPED>
-__global__ void __launch_bounds__(WAVES * 64)
+// KC: K chunk per pipeline stage -- 256, or 128 (half the LDS and registers per stage, so a
+// deeper weight pipeline and two 4-wave workgroups per CU fit: more HBM bytes in flight).
+template <int MT, int NT, int WAVES, int S, bool GROUPED, int KC>
+__global__ void __launch_bounds__(WAVES * 64, (KC == 128 && WAVES == 4) ? 2 : 1)
 gemm_skinny_kernel(const bf16_t* __restrict__ X, long ldx, const bf16_t* __restrict__ W, long ldw,
                    const bf16_t* __restrict__ bias, void* __restrict__ out, long ldo, int M, int N,
                    int krange, int mode, int inter, const int* __restrict__ offs,
                    const int* __restrict__ row_idx, long w_estride) {
   extern __shared__ __align__(16) bf16_t xs[];   // [2][MT*16][XLD]
+  constexpr int XLD = KC + XPAD;     // LDS row stride (elements)
+  constexpr int NST = KC / 32;       // 32-deep MFMA steps per chunk
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
   const int r = lane & 15, g = lane >> 4;
@@ -137,11 +139,11 @@ gemm_skinny_kernel(const bf16_t* __restrict__ X, long ldx, const bf16_t* __restr
     };
     // W fragments of one chunk: [tile][superstep*4 + s]; lane (r, g) covers
     // k = 128*superstep + 32g + 8s + j of the chunk
-    auto load_w = [&](int c, bf16x8 (&w)[NT][8]) {
+    auto load_w = [&](int c, bf16x8 (&w)[NT][NST]) {
 #pragma unroll
       for (int t = 0; t < NT; ++t)
 #pragma unroll
-        for (int ss = 0; ss < 2; ++ss)
+        for (int ss = 0; ss < KC / 128; ++ss)
 #pragma unroll
           for (int s = 0; s < 4; ++s) w[t][ss * 4 + s] = ld_w(wp[t] + c * KC + 128 * ss + KSTEP * s);
     };
@@ -155,7 +157,7 @@ gemm_skinny_kernel(const bf16_t* __restrict__ X, long ldx, const bf16_t* __restr
     // X fragments are read from LDS one MFMA step ahead (two named sets); the sched_barriers
     // stop hipcc from hoisting all 8 steps' ds_reads (MT*32 VGPRs) to the top, which left no
     // registers for deeper weight pipelines.
-    auto compute = [&](int buf, const bf16x8 (&w)[NT][8]) {
+    auto compute = [&](int buf, const bf16x8 (&w)[NT][NST]) {
       const bf16_t* xb = xs + (buf * MT * 16 + r) * XLD + KLANE * g;
       auto ldx = [&](int st, bf16x8 (&xf)[MT]) {
 #pragma unroll
@@ -172,12 +174,12 @@ gemm_skinny_kernel(const bf16_t* __restrict__ X, long ldx, const bf16_t* __restr
       bf16x8 xa[MT], xc[MT];
       ldx(0, xa);
 #pragma unroll
-      for (int st = 0; st < 8; st += 2) {
+      for (int st = 0; st < NST; st += 2) {
         ldx(st + 1, xc);
         __builtin_amdgcn_sched_barrier(0);
         mma(st, xa);
         __builtin_amdgcn_sched_barrier(0);
-        if (st + 2 < 8) ldx(st + 2, xa);
+        if (st + 2 < NST) ldx(st + 2, xa);
         __builtin_amdgcn_sched_barrier(0);
         mma(st + 1, xc);
         __builtin_amdgcn_sched_barrier(0);
@@ -192,7 +194,7 @@ gemm_skinny_kernel(const bf16_t* __restrict__ X, long ldx, const bf16_t* __restr
     // W(c+1) (needed next phase anyway) and leaves W(c+2..c+S-1) in flight.  Loads are
     // unconditional (chunk index clamped) and full groups of S phases have no early exit, so
     // the vmcnt accounting stays exact; the <S leftover phases run once as a guarded tail.
-    bf16x8 w[S][NT][8];
+    bf16x8 w[S][NT][NST];
     {
       bf16x8 xr[XPT];
       load_x(0, xr);
@@ -201,7 +203,7 @@ gemm_skinny_kernel(const bf16_t* __restrict__ X, long ldx, const bf16_t* __restr
       store_x(0, xr);
     }
     __syncthreads();
-    auto phase = [&](int cc, bf16x8 (&wcur)[NT][8], bf16x8 (&wnext)[NT][8]) {
+    auto phase = [&](int cc, bf16x8 (&wcur)[NT][NST], bf16x8 (&wnext)[NT][NST]) {
       bf16x8 xr[XPT];
       load_x(min(cc + 1, last), xr);
       load_w(min(cc + S - 1, last), wnext);
@@ -345,19 +347,19 @@ splitk_add_rmsnorm_kernel(const float* __restrict__ part, int sk_rt, int M, int 
   }
 }
 
-template <int MT, int NT, int WAVES, int S, bool GROUPED>
+template <int MT, int NT, int WAVES, int S, bool GROUPED, int KC>
 int launch_cfg(const bf16_t* X, long ldx, const bf16_t* W, long ldw, const bf16_t* bias, void* out,
                long ldo, int M, int N, int K, int sk, int mode, int experts, const int* offs,
                const int* row_idx, long w_estride, hipStream_t st) {
-  const size_t lds = 2ull * MT * 16 * XLD * sizeof(bf16_t);
+  const size_t lds = 2ull * MT * 16 * (KC + XPAD) * sizeof(bf16_t);
   static bool attr_set = false;   // > 64 KiB of dynamic LDS must be opted into
   if (!attr_set) {
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(gemm_skinny_kernel<MT, NT, WAVES, S, GROUPED>),
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(gemm_skinny_kernel<MT, NT, WAVES, S, GROUPED, KC>),
                         hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     attr_set = true;
   }
   dim3 grid(mode == MODE_SWIGLU ? (N / 2) / (WAVES * 16) : N / (WAVES * NT * 16), sk, experts);
-  hipLaunchKernelGGL((gemm_skinny_kernel<MT, NT, WAVES, S, GROUPED>), grid, dim3(WAVES * 64), lds, st,
+  hipLaunchKernelGGL((gemm_skinny_kernel<MT, NT, WAVES, S, GROUPED, KC>), grid, dim3(WAVES * 64), lds, st,
                      X, ldx, W, ldw, bias, out, ldo, M, N, K / sk, mode, N / 2, offs, row_idx,
                      w_estride);
   return (int)hipGetLastError();
@@ -367,31 +369,45 @@ template <int MT, bool GROUPED>
 int launch_mt(int cfg, const bf16_t* X, long ldx, const bf16_t* W, long ldw, const bf16_t* bias,
               void* out, long ldo, int M, int N, int K, int sk, int mode, int experts,
               const int* offs, const int* row_idx, long w_estride, hipStream_t st) {
-#define EIA_CFG(NT_, W_, S_) \
-  return launch_cfg<MT, NT_, W_, S_, GROUPED>(X, ldx, W, ldw, bias, out, ldo, M, N, K, sk, mode, \
-                                              experts, offs, row_idx, w_estride, st)
-  // cfg = (NT - 1) | ((WAVES / 2 - 1) << 1) | ((S - 2) << 2); grouped (MoE) uses S = 2
+#define EIA_CFG(NT_, W_, S_, KC_)                                                             \
+  return launch_cfg<MT, NT_, W_, S_, GROUPED, KC_>(X, ldx, W, ldw, bias, out, ldo, M, N, K, sk, \
+                                                   mode, experts, offs, row_idx, w_estride, st)
+  // cfg = (NT - 1) | ((WAVES / 2 - 1) << 1) | ((S - 2) << 2) | (KC == 128 ? 16 : 0);
+  // grouped (MoE) uses S = 2, KC = 256
   if constexpr (GROUPED) {
     switch (cfg & 3) {
-      case 0: EIA_CFG(1, 2, 2);
-      case 1: EIA_CFG(2, 2, 2);
-      case 2: EIA_CFG(1, 4, 2);
-      default: EIA_CFG(2, 4, 2);
+      case 0: EIA_CFG(1, 2, 2, 256);
+      case 1: EIA_CFG(2, 2, 2, 256);
+      case 2: EIA_CFG(1, 4, 2, 256);
+      default: EIA_CFG(2, 4, 2, 256);
     }
   } else {
     switch (cfg) {
-      case 0: EIA_CFG(1, 2, 2);
-      case 1: EIA_CFG(2, 2, 2);
-      case 2: EIA_CFG(1, 4, 2);
-      case 3: EIA_CFG(2, 4, 2);
-      case 4: EIA_CFG(1, 2, 3);
-      case 5: EIA_CFG(2, 2, 3);
-      case 6: EIA_CFG(1, 4, 3);
-      case 7: EIA_CFG(2, 4, 3);
-      case 8: EIA_CFG(1, 2, 4);
-      case 9: EIA_CFG(2, 2, 4);
-      case 10: EIA_CFG(1, 4, 4);
-      default: EIA_CFG(2, 4, 4);
+      case 0: EIA_CFG(1, 2, 2, 256);
+      case 1: EIA_CFG(2, 2, 2, 256);
+      case 2: EIA_CFG(1, 4, 2, 256);
+      case 3: EIA_CFG(2, 4, 2, 256);
+      case 4: EIA_CFG(1, 2, 3, 256);
+      case 5: EIA_CFG(2, 2, 3, 256);
+      case 6: EIA_CFG(1, 4, 3, 256);
+      case 7: EIA_CFG(2, 4, 3, 256);
+      case 8: EIA_CFG(1, 2, 4, 256);
+      case 9: EIA_CFG(2, 2, 4, 256);
+      case 10: EIA_CFG(1, 4, 4, 256);
+      case 11: EIA_CFG(2, 4, 4, 256);
+      case 16: EIA_CFG(1, 2, 2, 128);
+      case 17: EIA_CFG(2, 2, 2, 128);
+      case 18: EIA_CFG(1, 4, 2, 128);
+      case 19: EIA_CFG(2, 4, 2, 128);
+      case 20: EIA_CFG(1, 2, 3, 128);
+      case 21: EIA_CFG(2, 2, 3, 128);
+      case 22: EIA_CFG(1, 4, 3, 128);
+      case 23: EIA_CFG(2, 4, 3, 128);
+      case 24: EIA_CFG(1, 2, 4, 128);
+      case 25: EIA_CFG(2, 2, 4, 128);
+      case 26: EIA_CFG(1, 4, 4, 128);
+      case 27: EIA_CFG(2, 4, 4, 128);
+      default: return EIA_BAD_SHAPE;
     }
   }
 #undef EIA_CFG
@@ -420,11 +436,12 @@ int dispatch_mt(int mt, int cfg, const bf16_t* x, long ldx, const bf16_t* w, lon
 // (MT, cfg) pairs whose kernels spill to scratch on gfx950 (hipcc -Rpass-analysis=
 // kernel-resource-usage; 512 VGPR+AGPR budget at 1 wave/SIMD): rejected -- a spilling weight
 // pipeline is slow, and MT=5 cfg=5 also produced wrong results on MI355X.
-constexpr unsigned kSpillCfg[9] = {0x0, 0x200, 0xa00, 0xa20, 0xa20, 0xba0, 0xba2, 0xfb3, 0xfbb};
+constexpr unsigned kSpillCfg[9] = {0x0, 0x8000200, 0x8000a00, 0x8800a20, 0x8800a20, 0x8800ba0, 0xc880ba3, 0xec80fb3, 0xec80fbb};
 
 int check_shape(int N, int K, int sk, int mode, int cfg) {
   const int nt = (cfg & 1) ? 2 : 1, waves = (cfg & 2) ? 4 : 2;
-  if (sk < 1 || K % (sk * KC) != 0 || cfg < 0 || cfg > 11) return EIA_BAD_SHAPE;
+  const int kc = (cfg & 16) ? 128 : 256;
+  if (sk < 1 || cfg < 0 || (cfg & ~16) > 11 || K % (sk * kc) != 0) return EIA_BAD_SHAPE;
   if (mode == MODE_SWIGLU) {
     if (nt != 2 || sk != 1 || N % 2 != 0 || (N / 2) % (waves * 16) != 0) return EIA_BAD_SHAPE;
   } else if (N % (waves * nt * 16) != 0) {
@@ -440,7 +457,7 @@ int check_shape(int N, int K, int sk, int mode, int cfg) {
 // mode 1: out fp32 partial slabs [sk][M][N] (reduce with eia_splitk_reduce / _add_rmsnorm)
 // mode 2: SwiGLU: W = merged [gate; up] (N = 2I rows), out bf16 [M][ldo] = silu(gate) * up
 // cfg: bit0 -> two 16-row W tiles per wave (else one), bit1 -> 4 waves per workgroup (else 2),
-// bits 2-3 -> W pipeline stages - 2 (2..4)
+// bits 2-3 -> W pipeline stages - 2 (2..4), bit 4 -> 128-deep K chunks (else 256)
 EIA_API int eia_gemm_skinny(const void* X, long ldx, const void* W, long ldw, const void* bias,
                             void* out, long ldo, int M, int N, int K, int sk, int mode, int cfg,
                             hipStream_t st) {
@@ -461,7 +478,7 @@ EIA_API int eia_gemm_skinny(const void* X, long ldx, const void* W, long ldw, co
 EIA_API int eia_moe_gemm(const void* X, long ldx, const void* W, long ldw, const void* bias,
                          void* out, long ldo, int N, int K, int experts, const int* offs,
                          const int* row_idx, int mt_hint, int mode, int cfg, hipStream_t st) {
-  if (experts < 1 || mode == MODE_F32_SPLIT) return EIA_BAD_SHAPE;
+  if (experts < 1 || mode == MODE_F32_SPLIT || (cfg & 16)) return EIA_BAD_SHAPE;
   if (int rc = check_shape(N, K, 1, mode, cfg)) return rc;
   if ((ldx % 8) || (ldw % 8) || (ldo % 4)) return EIA_BAD_SHAPE;
   const int mt = mt_hint < 1 ? 1 : (mt_hint > 8 ? 8 : mt_hint);

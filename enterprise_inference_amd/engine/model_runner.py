@@ -51,6 +51,9 @@ class StepOutput:
         self.prompt_logprobs = None
 
 
+_TOKEN_WAIT = __import__("os").environ.get("EIA_TOKEN_WAIT", "event")
+
+
 class StepHandle:
     """A launched step's sampled tokens.  With overlapped scheduling the tokens stay on the
     device (feeding the next step's inputs) and are copied to pinned host memory behind an
@@ -66,8 +69,14 @@ class StepHandle:
 
     def result(self) -> StepOutput:
         if self._out is None:
-            if self._event is not None:
-                self._event.synchronize()
+            ev = self._event
+            if ev is not None:
+                if _TOKEN_WAIT in ("event", "blocking"):
+                    ev.synchronize()
+                else:                       # poll: "spin" or "yield"
+                    while not ev.query():
+                        if _TOKEN_WAIT == "yield":
+                            time.sleep(0)
             self._out = StepOutput(self._host.tolist(), None)
         return self._out
 
@@ -566,7 +575,7 @@ class ModelRunner:
         host = self.h_tok[self._par][:len(sample_items)]
         if self.is_gpu:
             host.copy_(toks, non_blocking=True)
-            ev = torch.cuda.Event()
+            ev = torch.cuda.Event(blocking=_TOKEN_WAIT == "blocking")
             ev.record()
             return StepHandle(sample_items, host=host, event=ev)
         host.copy_(toks)

@@ -29,7 +29,12 @@ TUNING_FILE = os.environ.get("EIA_GEMM_TUNING",
 
 MODE_BF16, MODE_SPLIT, MODE_SWIGLU = 0, 1, 2
 # kernel configs: bit0 -> 2 W tiles (32 rows) per wave, bit1 -> 4 waves per workgroup
-CFGS = tuple(range(12))   # bit0 NT=2, bit1 WAVES=4, bits2-3 pipeline stages-2
+# bit0 NT=2, bit1 WAVES=4, bits2-3 pipeline stages-2, bit4 128-deep K chunks (else 256)
+CFGS = tuple(range(12)) + tuple(range(16, 28))
+
+
+def cfg_kc(cfg: int) -> int:
+    return 128 if cfg & 16 else KC
 
 
 def cfg_rows(cfg: int) -> int:
@@ -58,11 +63,11 @@ _TUNED = _load_tuning()
 
 
 # (M-tile bucket -> cfgs whose kernel spills registers; mirrors kSpillCfg in gemm_skinny.hip)
-SPILL_CFGS = {1: (9,), 2: (9, 11), 3: (5, 9, 11), 4: (5, 9, 11), 5: (5, 7, 8, 9, 11), 6: (1, 5, 7, 8, 9, 11), 7: (0, 1, 4, 5, 7, 8, 9, 10, 11), 8: (0, 1, 3, 4, 5, 7, 8, 9, 10, 11)}
+SPILL_CFGS = {1: (9, 27), 2: (9, 11, 27), 3: (5, 9, 11, 23, 27), 4: (5, 9, 11, 23, 27), 5: (5, 7, 8, 9, 11, 23, 27), 6: (0, 1, 5, 7, 8, 9, 11, 19, 23, 26, 27), 7: (0, 1, 4, 5, 7, 8, 9, 10, 11, 19, 22, 23, 25, 26, 27), 8: (0, 1, 3, 4, 5, 7, 8, 9, 10, 11, 19, 22, 23, 25, 26, 27)}
 
 
 def valid(N: int, K: int, swiglu: bool, cfg: int, sk: int, M: Optional[int] = None) -> bool:
-    if K % (sk * KC):
+    if K % (sk * cfg_kc(cfg)):
         return False
     if M is not None and cfg in SPILL_CFGS.get(m_bucket(M), ()):
         return False
@@ -76,7 +81,7 @@ def heuristic_splitk(N: int, K: int, cfg: int, swiglu: bool = False) -> int:
     if swiglu:
         return 1
     tiles = N // cfg_rows(cfg)
-    nk = K // KC
+    nk = K // cfg_kc(cfg)
     best = 1
     for sk in range(1, nk + 1):
         if nk % sk:
@@ -108,7 +113,7 @@ def skinny_ok(x: torch.Tensor, w: torch.Tensor, swiglu: bool = False) -> bool:
         return False
     M, K = x.shape
     N = w.shape[0]
-    if M < 1 or M > MAX_M or K % KC or w.shape[1] != K:
+    if M < 1 or M > MAX_M or K % 128 or w.shape[1] != K:
         return False
     if x.stride(1) != 1 or w.stride(1) != 1 or x.stride(0) % 8 or w.stride(0) % 8:
         return False

@@ -70,6 +70,14 @@ def main() -> int:
     for lo, hi in buckets:
         g = [x for x in gaps if lo <= x < hi]
         print(f"  gaps {lo / 1e3:>6.0f}-{hi / 1e3:<8.0f}us: n={len(g):6d} total {sum(g) / 1e6:8.2f} ms")
+    where = collections.Counter()
+    for x, y in zip(rows, rows[1:]):
+        if y[0] - x[1] > 200e3:
+            where[(short(x[2])[:40], short(y[2])[:40])] += 1
+    if where:
+        print("\nidle gaps > 200 us, by (kernel before -> kernel after):")
+        for (x, y), n in where.most_common(6):
+            print(f"  {n:5d}  {x} -> {y}")
     print("\n| kernel | calls | total ms | % busy | avg us |\n|---|---:|---:|---:|---:|")
     for n, t in per.most_common(25):
         print(f"| {n} | {cnt[n]} | {t / 1e6:.2f} | {100 * t / busy:.1f} | {t / cnt[n] / 1e3:.1f} |")

@@ -57,8 +57,8 @@ def graph_time(fn, iters, rounds=3):
 
 def candidates(M, N, K, swiglu):
     out = []
-    nk = K // gemm.KC
     for cfg in gemm.CFGS:
+        nk = K // gemm.cfg_kc(cfg)
         for sk in range(1, nk + 1):
             if nk % sk or not gemm.valid(N, K, swiglu, cfg, sk, M=M):
                 continue
