@@ -37,6 +37,9 @@ for s in $STEPS; do
     gemm) run gemm 900 python scripts/bench_gemm.py --sweep --m ${GEMM_M:-65} \
             --shapes qkv_8b o_8b gate_up_8b down_8b lm_head_8b ;;
     attn) run attn 300 python scripts/bench_attn.py ;;
+    tune) run tune 1100 python scripts/bench_gemm.py --tune --m ${GEMM_M:-65} \
+            --shapes ${GEMM_SHAPES:-qkv_8b o_8b gate_up_8b down_8b lm_head_8b} --out gpurun_out/gemm_tuning.json ;;
+    probe) run probe 300 python scripts/probe_overlap.py ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac
 done
