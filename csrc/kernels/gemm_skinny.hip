@@ -186,41 +186,44 @@ gemm_skinny_kernel(const bf16_t* __restrict__ X, long ldx, const bf16_t* __restr
       }
     };
 
-    // Pipeline: S W register sets (S-1 chunks of weights in flight while one is multiplied;
-    // indices are compile-time after unrolling -- no runtime-indexed register arrays, guide
-    // rule 20).  Each phase issues X(c+1) then W(c+S-1) -- pinned ahead of the MFMAs with
-    // sched_barrier, since hipcc otherwise sinks the X loads behind the compute and waits
-    // vmcnt(0) on them -- so the in-order vmcnt wait for X before its ds_write only drains
-    // W(c+1) (needed next phase anyway) and leaves W(c+2..c+S-1) in flight.  Loads are
+    // Pipeline: S register sets for W and for X (indices compile-time after unrolling -- no
+    // runtime-indexed register arrays, guide rule 20).  Phase c issues X(c+S-1) and then
+    // W(c+S-1), multiplies chunk c, and writes X(c+1) to LDS.  vmcnt retires in issue order,
+    // so the wait for X(c+1) before its ds_write drains only what was issued before it
+    // (X(c+1) left S-2 phases ago, just ahead of W(c+1)): W(c+1..c+S-1) stay in flight and the
+    // weight stream runs S-1 chunks deep.  (Issuing X only one chunk ahead would drain every
+    // older W load at that wait and cap the depth at one chunk for any S.)  Loads are
     // unconditional (chunk index clamped) and full groups of S phases have no early exit, so
     // the vmcnt accounting stays exact; the <S leftover phases run once as a guarded tail.
     bf16x8 w[S][NT][NST];
-    {
-      bf16x8 xr[XPT];
-      load_x(0, xr);
+    bf16x8 xr[S][XPT];
 #pragma unroll
-      for (int s = 0; s < S - 1; ++s) load_w(min(s, last), w[s]);
-      store_x(0, xr);
+    for (int s = 0; s < S - 1; ++s) {
+      load_x(min(s, last), xr[s]);
+      load_w(min(s, last), w[s]);
     }
+    store_x(0, xr[0]);
     __syncthreads();
-    auto phase = [&](int cc, bf16x8 (&wcur)[NT][NST], bf16x8 (&wnext)[NT][NST]) {
-      bf16x8 xr[XPT];
-      load_x(min(cc + 1, last), xr);
+    auto phase = [&](int cc, bf16x8 (&wcur)[NT][NST], bf16x8 (&wnext)[NT][NST],
+                     bf16x8 (&xnext)[XPT], const bf16x8 (&xstore)[XPT]) {
+      load_x(min(cc + S - 1, last), xnext);
       load_w(min(cc + S - 1, last), wnext);
       __builtin_amdgcn_sched_barrier(0);
       compute(cc & 1, wcur);
       __builtin_amdgcn_sched_barrier(0);
-      store_x((cc + 1) & 1, xr);
+      store_x((cc + 1) & 1, xstore);
       __syncthreads();
     };
     int c = 0;
     for (; c + S <= nchunks; c += S) {
 #pragma unroll
-      for (int s = 0; s < S; ++s) phase(c + s, w[s], w[(s + S - 1) % S]);
+      for (int s = 0; s < S; ++s)
+        phase(c + s, w[s], w[(s + S - 1) % S], xr[(s + S - 1) % S], xr[(s + 1) % S]);
     }
 #pragma unroll
     for (int s = 0; s < S - 1; ++s)
-      if (c + s < nchunks) phase(c + s, w[s], w[(s + S - 1) % S]);
+      if (c + s < nchunks)
+        phase(c + s, w[s], w[(s + S - 1) % S], xr[(s + S - 1) % S], xr[(s + 1) % S]);
 
     // epilogue: lane (r, g) holds rows n = tile_base + 4g + i, column m = 16*mt + r
     const long orow0 = mbase + m0;
@@ -436,7 +439,7 @@ int dispatch_mt(int mt, int cfg, const bf16_t* x, long ldx, const bf16_t* w, lon
 // (MT, cfg) pairs whose kernels spill to scratch on gfx950 (hipcc -Rpass-analysis=
 // kernel-resource-usage; 512 VGPR+AGPR budget at 1 wave/SIMD): rejected -- a spilling weight
 // pipeline is slow, and MT=5 cfg=5 also produced wrong results on MI355X.
-constexpr unsigned kSpillCfg[9] = {0x0, 0x8000200, 0x8000a00, 0x8800a20, 0x8800a20, 0x8800ba0, 0xc880ba3, 0xec80fb3, 0xec80fbb};
+constexpr unsigned kSpillCfg[9] = {0x0, 0x8000a00, 0x8000a20, 0x8800ba0, 0xc800bb0, 0xe800fb0, 0xee80fb3, 0xfe80ff3, 0xff80ffb};
 
 int check_shape(int N, int K, int sk, int mode, int cfg) {
   const int nt = (cfg & 1) ? 2 : 1, waves = (cfg & 2) ? 4 : 2;

@@ -63,7 +63,7 @@ _TUNED = _load_tuning()
 
 
 # (M-tile bucket -> cfgs whose kernel spills registers; mirrors kSpillCfg in gemm_skinny.hip)
-SPILL_CFGS = {1: (9, 27), 2: (9, 11, 27), 3: (5, 9, 11, 23, 27), 4: (5, 9, 11, 23, 27), 5: (5, 7, 8, 9, 11, 23, 27), 6: (0, 1, 5, 7, 8, 9, 11, 19, 23, 26, 27), 7: (0, 1, 4, 5, 7, 8, 9, 10, 11, 19, 22, 23, 25, 26, 27), 8: (0, 1, 3, 4, 5, 7, 8, 9, 10, 11, 19, 22, 23, 25, 26, 27)}
+SPILL_CFGS = {1: (9, 11, 27), 2: (5, 9, 11, 27), 3: (5, 7, 8, 9, 11, 23, 27), 4: (4, 5, 7, 8, 9, 11, 23, 26, 27), 5: (4, 5, 7, 8, 9, 10, 11, 23, 25, 26, 27), 6: (0, 1, 4, 5, 7, 8, 9, 10, 11, 19, 21, 22, 23, 25, 26, 27), 7: (0, 1, 4, 5, 6, 7, 8, 9, 10, 11, 19, 21, 22, 23, 24, 25, 26, 27), 8: (0, 1, 3, 4, 5, 6, 7, 8, 9, 10, 11, 19, 20, 21, 22, 23, 24, 25, 26, 27)}
 
 
 def valid(N: int, K: int, swiglu: bool, cfg: int, sk: int, M: Optional[int] = None) -> bool:
