@@ -65,8 +65,12 @@ EIA_DEV bf16x8 ld_w(const bf16_t* p) {
 // S: W pipeline stages (register sets); S-1 chunks of weights stay in flight.
 // KC: K chunk per pipeline stage -- 256, or 128 (half the LDS and registers per stage, so a
 // deeper weight pipeline and two 4-wave workgroups per CU fit: more HBM bytes in flight).
-template <int MT, int NT, int WAVES, int S, bool GROUPED, int KC>
-__global__ void __launch_bounds__(WAVES * 64, (KC == 128 && WAVES == 4) ? 2 : 1)
+// LOADER: one extra wave stages the X chunks into LDS (one chunk ahead) while the WAVES
+// compute waves only stream W: their in-order vmcnt queue then holds nothing but weight
+// loads, so the weight pipeline stays S-1 chunks deep without X lookahead registers.
+template <int MT, int NT, int WAVES, int S, bool GROUPED, int KC, bool LOADER>
+__global__ void __launch_bounds__(WAVES * 64 + (LOADER ? 64 : 0),
+                                  ((KC == 128 && WAVES == 4) || LOADER) ? 2 : 1)
 gemm_skinny_kernel(const bf16_t* __restrict__ X, long ldx, const bf16_t* __restrict__ W, long ldw,
                    const bf16_t* __restrict__ bias, void* __restrict__ out, long ldo, int M, int N,
                    int krange, int mode, int inter, const int* __restrict__ offs,
@@ -105,8 +109,11 @@ gemm_skinny_kernel(const bf16_t* __restrict__ X, long ldx, const bf16_t* __restr
   }
 
   constexpr int XV = MT * 16 * (KC / 8);                // 16-B vectors per X chunk
-  constexpr int XPT = XV / (WAVES * 64);                // per thread
-  static_assert(XV % (WAVES * 64) == 0, "X chunk split");
+  constexpr int XTHREADS = LOADER ? 64 : WAVES * 64;    // threads that stage X
+  constexpr int XPT = XV / XTHREADS;                    // per staging thread
+  static_assert(XV % XTHREADS == 0, "X chunk split");
+  const int xt = LOADER ? lane : (int)threadIdx.x;      // index among the staging threads
+  const bool is_loader = LOADER && wave == WAVES;
 
   for (int m0 = 0; m0 < Mtot; m0 += MT * 16) {
     const int Mc = min(MT * 16, Mtot - m0);
@@ -119,12 +126,12 @@ gemm_skinny_kernel(const bf16_t* __restrict__ X, long ldx, const bf16_t* __restr
     };
     int xrows[XPT];   // 32-bit: 64-bit row offsets cost 2*XPT live VGPRs
 #pragma unroll
-    for (int j = 0; j < XPT; ++j) xrows[j] = xrow_of((threadIdx.x + j * WAVES * 64) / (KC / 8));
+    for (int j = 0; j < XPT; ++j) xrows[j] = xrow_of((xt + j * XTHREADS) / (KC / 8));
 
     auto load_x = [&](int c, bf16x8 (&xr)[XPT]) {
 #pragma unroll
       for (int j = 0; j < XPT; ++j) {
-        const int v = threadIdx.x + j * WAVES * 64;
+        const int v = xt + j * XTHREADS;
         const int col = (v % (KC / 8)) * 8;
         xr[j] = *reinterpret_cast<const bf16x8*>(X + (long)xrows[j] * ldx + k0 + c * KC + col);
       }
@@ -132,7 +139,7 @@ gemm_skinny_kernel(const bf16_t* __restrict__ X, long ldx, const bf16_t* __restr
     auto store_x = [&](int buf, const bf16x8 (&xr)[XPT]) {
 #pragma unroll
       for (int j = 0; j < XPT; ++j) {
-        const int v = threadIdx.x + j * WAVES * 64;
+        const int v = xt + j * XTHREADS;
         const int row = v / (KC / 8), col = (v % (KC / 8)) * 8;
         *reinterpret_cast<bf16x8*>(xs + (buf * MT * 16 + row) * XLD + col) = xr[j];
       }
@@ -195,35 +202,79 @@ gemm_skinny_kernel(const bf16_t* __restrict__ X, long ldx, const bf16_t* __restr
     // older W load at that wait and cap the depth at one chunk for any S.)  Loads are
     // unconditional (chunk index clamped) and full groups of S phases have no early exit, so
     // the vmcnt accounting stays exact; the <S leftover phases run once as a guarded tail.
-    bf16x8 w[S][NT][NST];
-    bf16x8 xr[S][XPT];
+    if constexpr (LOADER) {
+      // Both roles pass the same 1 + nchunks barriers.  Phase c: the compute waves multiply
+      // LDS buffer c&1 while the loader writes X(c+1) into buffer (c+1)&1 (last read in phase
+      // c-1, before the previous barrier) and fetches X(c+2) into registers.
+      if (is_loader) {
+        bf16x8 xr[2][XPT];
+        load_x(0, xr[0]);
+        load_x(min(1, last), xr[1]);
+        store_x(0, xr[0]);
+        __syncthreads();
+        auto step = [&](int cc, const bf16x8 (&xstore)[XPT], bf16x8 (&xload)[XPT]) {
+          store_x((cc + 1) & 1, xstore);
+          load_x(min(cc + 2, last), xload);
+          __syncthreads();
+        };
+        int cc = 0;
+        for (; cc + 2 <= nchunks; cc += 2) {
+          step(cc, xr[1], xr[0]);
+          step(cc + 1, xr[0], xr[1]);
+        }
+        if (cc < nchunks) step(cc, xr[1], xr[0]);
+        continue;                                 // the loader has no epilogue
+      }
+      bf16x8 w[S][NT][NST];
 #pragma unroll
-    for (int s = 0; s < S - 1; ++s) {
-      load_x(min(s, last), xr[s]);
-      load_w(min(s, last), w[s]);
-    }
-    store_x(0, xr[0]);
-    __syncthreads();
-    auto phase = [&](int cc, bf16x8 (&wcur)[NT][NST], bf16x8 (&wnext)[NT][NST],
-                     bf16x8 (&xnext)[XPT], const bf16x8 (&xstore)[XPT]) {
-      load_x(min(cc + S - 1, last), xnext);
-      load_w(min(cc + S - 1, last), wnext);
-      __builtin_amdgcn_sched_barrier(0);
-      compute(cc & 1, wcur);
-      __builtin_amdgcn_sched_barrier(0);
-      store_x((cc + 1) & 1, xstore);
+      for (int s = 0; s < S - 1; ++s) load_w(min(s, last), w[s]);
       __syncthreads();
-    };
-    int c = 0;
-    for (; c + S <= nchunks; c += S) {
+      auto phase = [&](int cc, bf16x8 (&wcur)[NT][NST], bf16x8 (&wnext)[NT][NST]) {
+        load_w(min(cc + S - 1, last), wnext);
+        __builtin_amdgcn_sched_barrier(0);
+        compute(cc & 1, wcur);
+        __builtin_amdgcn_sched_barrier(0);
+        __syncthreads();
+      };
+      int c = 0;
+      for (; c + S <= nchunks; c += S) {
 #pragma unroll
-      for (int s = 0; s < S; ++s)
-        phase(c + s, w[s], w[(s + S - 1) % S], xr[(s + S - 1) % S], xr[(s + 1) % S]);
+        for (int s = 0; s < S; ++s) phase(c + s, w[s], w[(s + S - 1) % S]);
+      }
+#pragma unroll
+      for (int s = 0; s < S - 1; ++s)
+        if (c + s < nchunks) phase(c + s, w[s], w[(s + S - 1) % S]);
+    } else {
+      bf16x8 w[S][NT][NST];
+      bf16x8 xr[S][XPT];
+  #pragma unroll
+      for (int s = 0; s < S - 1; ++s) {
+        load_x(min(s, last), xr[s]);
+        load_w(min(s, last), w[s]);
+      }
+      store_x(0, xr[0]);
+      __syncthreads();
+      auto phase = [&](int cc, bf16x8 (&wcur)[NT][NST], bf16x8 (&wnext)[NT][NST],
+                       bf16x8 (&xnext)[XPT], const bf16x8 (&xstore)[XPT]) {
+        load_x(min(cc + S - 1, last), xnext);
+        load_w(min(cc + S - 1, last), wnext);
+        __builtin_amdgcn_sched_barrier(0);
+        compute(cc & 1, wcur);
+        __builtin_amdgcn_sched_barrier(0);
+        store_x((cc + 1) & 1, xstore);
+        __syncthreads();
+      };
+      int c = 0;
+      for (; c + S <= nchunks; c += S) {
+  #pragma unroll
+        for (int s = 0; s < S; ++s)
+          phase(c + s, w[s], w[(s + S - 1) % S], xr[(s + S - 1) % S], xr[(s + 1) % S]);
+      }
+  #pragma unroll
+      for (int s = 0; s < S - 1; ++s)
+        if (c + s < nchunks)
+          phase(c + s, w[s], w[(s + S - 1) % S], xr[(s + S - 1) % S], xr[(s + 1) % S]);
     }
-#pragma unroll
-    for (int s = 0; s < S - 1; ++s)
-      if (c + s < nchunks)
-        phase(c + s, w[s], w[(s + S - 1) % S], xr[(s + S - 1) % S], xr[(s + 1) % S]);
 
     // epilogue: lane (r, g) holds rows n = tile_base + 4g + i, column m = 16*mt + r
     const long orow0 = mbase + m0;
@@ -350,19 +401,19 @@ splitk_add_rmsnorm_kernel(const float* __restrict__ part, int sk_rt, int M, int 
   }
 }
 
-template <int MT, int NT, int WAVES, int S, bool GROUPED, int KC>
+template <int MT, int NT, int WAVES, int S, bool GROUPED, int KC, bool LOADER = false>
 int launch_cfg(const bf16_t* X, long ldx, const bf16_t* W, long ldw, const bf16_t* bias, void* out,
                long ldo, int M, int N, int K, int sk, int mode, int experts, const int* offs,
                const int* row_idx, long w_estride, hipStream_t st) {
   const size_t lds = 2ull * MT * 16 * (KC + XPAD) * sizeof(bf16_t);
   static bool attr_set = false;   // > 64 KiB of dynamic LDS must be opted into
   if (!attr_set) {
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(gemm_skinny_kernel<MT, NT, WAVES, S, GROUPED, KC>),
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(gemm_skinny_kernel<MT, NT, WAVES, S, GROUPED, KC, LOADER>),
                         hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     attr_set = true;
   }
   dim3 grid(mode == MODE_SWIGLU ? (N / 2) / (WAVES * 16) : N / (WAVES * NT * 16), sk, experts);
-  hipLaunchKernelGGL((gemm_skinny_kernel<MT, NT, WAVES, S, GROUPED, KC>), grid, dim3(WAVES * 64), lds, st,
+  hipLaunchKernelGGL((gemm_skinny_kernel<MT, NT, WAVES, S, GROUPED, KC, LOADER>), grid, dim3(WAVES * 64 + (LOADER ? 64 : 0)), lds, st,
                      X, ldx, W, ldw, bias, out, ldo, M, N, K / sk, mode, N / 2, offs, row_idx,
                      w_estride);
   return (int)hipGetLastError();
@@ -410,6 +461,16 @@ int launch_mt(int cfg, const bf16_t* X, long ldx, const bf16_t* W, long ldw, con
       case 25: EIA_CFG(2, 2, 4, 128);
       case 26: EIA_CFG(1, 4, 4, 128);
       case 27: EIA_CFG(2, 4, 4, 128);
+      default: break;
+    }
+    // bit 5: wave-specialised X loader (4 compute waves, 128-deep chunks)
+    switch (cfg) {
+      case 50: return launch_cfg<MT, 1, 4, 2, GROUPED, 128, true>(X, ldx, W, ldw, bias, out, ldo, M, N, K, sk, mode, experts, offs, row_idx, w_estride, st);
+      case 51: return launch_cfg<MT, 2, 4, 2, GROUPED, 128, true>(X, ldx, W, ldw, bias, out, ldo, M, N, K, sk, mode, experts, offs, row_idx, w_estride, st);
+      case 54: return launch_cfg<MT, 1, 4, 3, GROUPED, 128, true>(X, ldx, W, ldw, bias, out, ldo, M, N, K, sk, mode, experts, offs, row_idx, w_estride, st);
+      case 55: return launch_cfg<MT, 2, 4, 3, GROUPED, 128, true>(X, ldx, W, ldw, bias, out, ldo, M, N, K, sk, mode, experts, offs, row_idx, w_estride, st);
+      case 58: return launch_cfg<MT, 1, 4, 4, GROUPED, 128, true>(X, ldx, W, ldw, bias, out, ldo, M, N, K, sk, mode, experts, offs, row_idx, w_estride, st);
+      case 59: return launch_cfg<MT, 2, 4, 4, GROUPED, 128, true>(X, ldx, W, ldw, bias, out, ldo, M, N, K, sk, mode, experts, offs, row_idx, w_estride, st);
       default: return EIA_BAD_SHAPE;
     }
   }
@@ -439,12 +500,13 @@ int dispatch_mt(int mt, int cfg, const bf16_t* x, long ldx, const bf16_t* w, lon
 // (MT, cfg) pairs whose kernels spill to scratch on gfx950 (hipcc -Rpass-analysis=
 // kernel-resource-usage; 512 VGPR+AGPR budget at 1 wave/SIMD): rejected -- a spilling weight
 // pipeline is slow, and MT=5 cfg=5 also produced wrong results on MI355X.
-constexpr unsigned kSpillCfg[9] = {0x0, 0x8000a00, 0x8000a20, 0x8800ba0, 0xc800bb0, 0xe800fb0, 0xee80fb3, 0xfe80ff3, 0xff80ffb};
+constexpr unsigned long long kSpillCfg[9] = {0x0ull, 0x8000a00ull, 0x8000a20ull, 0x8800ba0ull, 0x80000000e800bb0ull, 0x44400000ec00fb2ull, 0x80000000ee80fb2ull, 0x88000000fe80ff3ull, 0xccc00000ff80ffbull};
 
 int check_shape(int N, int K, int sk, int mode, int cfg) {
   const int nt = (cfg & 1) ? 2 : 1, waves = (cfg & 2) ? 4 : 2;
   const int kc = (cfg & 16) ? 128 : 256;
-  if (sk < 1 || cfg < 0 || (cfg & ~16) > 11 || K % (sk * kc) != 0) return EIA_BAD_SHAPE;
+  if (sk < 1 || cfg < 0 || (cfg & ~(16 | 32)) > 11 || K % (sk * kc) != 0) return EIA_BAD_SHAPE;
+  if ((cfg & 32) && !((cfg & 16) && (cfg & 2))) return EIA_BAD_SHAPE;   // loader: 4 waves, KC 128
   if (mode == MODE_SWIGLU) {
     if (nt != 2 || sk != 1 || N % 2 != 0 || (N / 2) % (waves * 16) != 0) return EIA_BAD_SHAPE;
   } else if (N % (waves * nt * 16) != 0) {
@@ -460,13 +522,14 @@ int check_shape(int N, int K, int sk, int mode, int cfg) {
 // mode 1: out fp32 partial slabs [sk][M][N] (reduce with eia_splitk_reduce / _add_rmsnorm)
 // mode 2: SwiGLU: W = merged [gate; up] (N = 2I rows), out bf16 [M][ldo] = silu(gate) * up
 // cfg: bit0 -> two 16-row W tiles per wave (else one), bit1 -> 4 waves per workgroup (else 2),
-// bits 2-3 -> W pipeline stages - 2 (2..4), bit 4 -> 128-deep K chunks (else 256)
+// bits 2-3 -> W pipeline stages - 2 (2..4), bit 4 -> 128-deep K chunks (else 256),
+// bit 5 -> extra X-loader wave (with bits 1 and 4)
 EIA_API int eia_gemm_skinny(const void* X, long ldx, const void* W, long ldw, const void* bias,
                             void* out, long ldo, int M, int N, int K, int sk, int mode, int cfg,
                             hipStream_t st) {
   if (M < 1 || M > 128) return EIA_BAD_SHAPE;
   if (int rc = check_shape(N, K, sk, mode, cfg)) return rc;
-  if ((kSpillCfg[(M + 15) / 16] >> cfg) & 1u) return EIA_BAD_SHAPE;
+  if ((kSpillCfg[(M + 15) / 16] >> cfg) & 1ull) return EIA_BAD_SHAPE;
   if ((ldx % 8) || (ldw % 8) || (ldo % 4)) return EIA_BAD_SHAPE;
   return dispatch_mt<false>((M + 15) / 16, cfg, static_cast<const bf16_t*>(X), ldx,
                             static_cast<const bf16_t*>(W), ldw, static_cast<const bf16_t*>(bias),
@@ -481,7 +544,7 @@ EIA_API int eia_gemm_skinny(const void* X, long ldx, const void* W, long ldw, co
 EIA_API int eia_moe_gemm(const void* X, long ldx, const void* W, long ldw, const void* bias,
                          void* out, long ldo, int N, int K, int experts, const int* offs,
                          const int* row_idx, int mt_hint, int mode, int cfg, hipStream_t st) {
-  if (experts < 1 || mode == MODE_F32_SPLIT || (cfg & 16)) return EIA_BAD_SHAPE;
+  if (experts < 1 || mode == MODE_F32_SPLIT || (cfg & 48)) return EIA_BAD_SHAPE;
   if (int rc = check_shape(N, K, 1, mode, cfg)) return rc;
   if ((ldx % 8) || (ldw % 8) || (ldo % 4)) return EIA_BAD_SHAPE;
   const int mt = mt_hint < 1 ? 1 : (mt_hint > 8 ? 8 : mt_hint);

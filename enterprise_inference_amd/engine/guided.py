@@ -23,7 +23,9 @@ try:
 except ImportError:  # pragma: no cover - regex ships in the image
     _re = None
 
-_WS = r"[ \t\n]*"
+# Whitespace between JSON tokens is capped: with an unbounded run a weakly-conditioned model
+# can spend its whole max_tokens budget on indentation and never close the document.
+_WS = r"[ \t\n]{0,2}"
 _STR = r'"(?:[^"\\\x00-\x1f]|\\["\\/bfnrt]|\\u[0-9a-fA-F]{4})*"'
 _NUM = r"-?(?:0|[1-9][0-9]*)(?:\.[0-9]+)?(?:[eE][+-]?[0-9]+)?"
 _INT = r"-?(?:0|[1-9][0-9]*)"

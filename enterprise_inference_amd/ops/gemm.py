@@ -30,7 +30,8 @@ TUNING_FILE = os.environ.get("EIA_GEMM_TUNING",
 MODE_BF16, MODE_SPLIT, MODE_SWIGLU = 0, 1, 2
 # kernel configs: bit0 -> 2 W tiles (32 rows) per wave, bit1 -> 4 waves per workgroup
 # bit0 NT=2, bit1 WAVES=4, bits2-3 pipeline stages-2, bit4 128-deep K chunks (else 256)
-CFGS = tuple(range(12)) + tuple(range(16, 28))
+# bit5: an extra wave stages X into LDS (4 compute waves, KC 128): 50, 51, 54, 55, 58, 59
+CFGS = tuple(range(12)) + tuple(range(16, 28)) + (50, 51, 54, 55, 58, 59)
 
 
 def cfg_kc(cfg: int) -> int:
@@ -63,7 +64,7 @@ _TUNED = _load_tuning()
 
 
 # (M-tile bucket -> cfgs whose kernel spills registers; mirrors kSpillCfg in gemm_skinny.hip)
-SPILL_CFGS = {1: (9, 11, 27), 2: (5, 9, 11, 27), 3: (5, 7, 8, 9, 11, 23, 27), 4: (4, 5, 7, 8, 9, 11, 23, 26, 27), 5: (4, 5, 7, 8, 9, 10, 11, 23, 25, 26, 27), 6: (0, 1, 4, 5, 7, 8, 9, 10, 11, 19, 21, 22, 23, 25, 26, 27), 7: (0, 1, 4, 5, 6, 7, 8, 9, 10, 11, 19, 21, 22, 23, 24, 25, 26, 27), 8: (0, 1, 3, 4, 5, 6, 7, 8, 9, 10, 11, 19, 20, 21, 22, 23, 24, 25, 26, 27)}
+SPILL_CFGS = {1: (9, 11, 27), 2: (5, 9, 11, 27), 3: (5, 7, 8, 9, 11, 23, 27), 4: (4, 5, 7, 8, 9, 11, 23, 25, 26, 27, 59), 5: (1, 4, 5, 7, 8, 9, 10, 11, 22, 23, 25, 26, 27, 50, 54, 58), 6: (1, 4, 5, 7, 8, 9, 10, 11, 19, 21, 22, 23, 25, 26, 27, 59), 7: (0, 1, 4, 5, 6, 7, 8, 9, 10, 11, 19, 21, 22, 23, 24, 25, 26, 27, 55, 59), 8: (0, 1, 3, 4, 5, 6, 7, 8, 9, 10, 11, 19, 20, 21, 22, 23, 24, 25, 26, 27, 50, 51, 54, 55, 58, 59)}
 
 
 def valid(N: int, K: int, swiglu: bool, cfg: int, sk: int, M: Optional[int] = None) -> bool:

@@ -11,7 +11,7 @@ import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 SRC = os.path.join(ROOT, "csrc", "kernels", "gemm_skinny.hip")
-PAT = re.compile(r"gemm_skinny_kernelILi(\d+)ELi(\d+)ELi(\d+)ELi(\d+)ELb([01])ELi(\d+)E")
+PAT = re.compile(r"gemm_skinny_kernelILi(\d+)ELi(\d+)ELi(\d+)ELi(\d+)ELb([01])ELi(\d+)ELb([01])E")
 
 
 def main() -> int:
@@ -37,20 +37,22 @@ def main() -> int:
         if m and int(m.group(2)) > 0:
             spill.add(cur)
     masks = [0] * 9
-    for mt, nt, waves, st, grouped, kc in spill:
+    for mt, nt, waves, st, grouped, kc, loader in spill:
         if grouped:
             continue
-        cfg = (nt - 1) | ((waves // 2 - 1) << 1) | ((st - 2) << 2) | (16 if kc == 128 else 0)
+        cfg = (nt - 1) | ((waves // 2 - 1) << 1) | ((st - 2) << 2) | (16 if kc == 128 else 0) \
+            | (32 if loader else 0)
         masks[mt] |= 1 << cfg
-    cpp = "constexpr unsigned kSpillCfg[9] = {" + ", ".join(hex(m) for m in masks) + "};"
+    cpp = "constexpr unsigned long long kSpillCfg[9] = {" + ", ".join(
+        hex(m) + "ull" for m in masks) + "};"
     py = "SPILL_CFGS = {" + ", ".join(
-        f"{mt}: {tuple(c for c in range(32) if masks[mt] >> c & 1)}" for mt in range(1, 9)) + "}"
+        f"{mt}: {tuple(c for c in range(64) if masks[mt] >> c & 1)}" for mt in range(1, 9)) + "}"
     print(f"{len(seen)} instantiations, {len(spill)} spill")
     print(cpp)
     print(py)
     if "--write" in sys.argv:
         s = open(SRC).read()
-        s = re.sub(r"constexpr unsigned kSpillCfg\[9\] = \{[^}]*\};", cpp, s)
+        s = re.sub(r"constexpr unsigned (long long )?kSpillCfg\[9\] = \{[^}]*\};", cpp, s)
         open(SRC, "w").write(s)
         p = os.path.join(ROOT, "enterprise_inference_amd", "ops", "gemm.py")
         s = open(p).read()
