@@ -27,6 +27,8 @@
 //    matching up rows [I + n0, ...) of the merged gate_up weight, so the
 //    epilogue writes silu(g) * u directly ([M, I]); the 2I-wide intermediate
 //    never reaches HBM.
+#include <cstdlib>
+
 #include "eia_common.h"
 
 namespace {
@@ -68,13 +70,17 @@ EIA_DEV bf16x8 ld_w(const bf16_t* p) {
 // LOADER: one extra wave stages the X chunks into LDS (one chunk ahead) while the WAVES
 // compute waves only stream W: their in-order vmcnt queue then holds nothing but weight
 // loads, so the weight pipeline stays S-1 chunks deep without X lookahead registers.
-template <int MT, int NT, int WAVES, int S, bool GROUPED, int KC, bool LOADER>
+// PACKED: W is stored tile-major (pack_weight): for each 16-row tile and 128-deep K block,
+// the four 64-lane fragment loads are consecutive 1 KiB runs, so a wave streams its tile's
+// whole K range as one contiguous region (8 full cache lines per load instruction instead of
+// 64-B pieces of 16 rows 8 KiB apart).
+template <int MT, int NT, int WAVES, int S, bool GROUPED, int KC, bool LOADER, bool PACKED>
 __global__ void __launch_bounds__(WAVES * 64 + (LOADER ? 64 : 0),
                                   ((KC == 128 && WAVES == 4) || LOADER) ? 2 : 1)
 gemm_skinny_kernel(const bf16_t* __restrict__ X, long ldx, const bf16_t* __restrict__ W, long ldw,
                    const bf16_t* __restrict__ bias, void* __restrict__ out, long ldo, int M, int N,
                    int krange, int mode, int inter, const int* __restrict__ offs,
-                   const int* __restrict__ row_idx, long w_estride) {
+                   const int* __restrict__ row_idx, long w_estride, int rot_mul) {
   extern __shared__ __align__(16) bf16_t xs[];   // [2][MT*16][XLD]
   constexpr int XLD = KC + XPAD;     // LDS row stride (elements)
   constexpr int NST = KC / 32;       // 32-deep MFMA steps per chunk
@@ -84,6 +90,10 @@ gemm_skinny_kernel(const bf16_t* __restrict__ X, long ldx, const bf16_t* __restr
   const int k0 = blockIdx.y * krange;
   const int nchunks = krange / KC;
   const int last = nchunks - 1;
+  // Workgroups start their K walk at staggered chunks (rot_mul != 0) so the concurrent
+  // streams do not all hit the same HBM channel window at the same K offset.
+  const int rot = (int)(((unsigned)blockIdx.x * (unsigned)rot_mul) % (unsigned)nchunks);
+  auto rc = [&](int c) { const int t = c + rot; return t >= nchunks ? t - nchunks : t; };
 
   int mbase = 0, Mtot = M;
   if constexpr (GROUPED) {
@@ -98,14 +108,22 @@ gemm_skinny_kernel(const bf16_t* __restrict__ X, long ldx, const bf16_t* __restr
   // rows of W owned by this wave's tiles
   const bf16_t* wp[NT];
   int nbase;
+  // element offset of row `row0 + r` (row0 a multiple of 16) at k0 for this lane
+  auto wrow = [&](int row0) -> long {
+    if constexpr (PACKED) return (long)row0 * ldw + (long)(k0 / 128) * 2048 + lane * 8;
+    return (long)(row0 + r) * ldw + k0 + KLANE * g;
+  };
+  // strides (elements) between a lane's fragments: MFMA step s, 128-deep super-step
+  constexpr int WS_STEP = PACKED ? 512 : KSTEP;
+  constexpr int WS_SUPER = PACKED ? 2048 : 128;
   if (NT == 2 && mode == MODE_SWIGLU) {
     nbase = blockIdx.x * (WAVES * 16) + wave * 16;      // output column block
-    wp[0] = W + (long)(nbase + r) * ldw + k0 + KLANE * g;
-    wp[NT - 1] = W + (long)(inter + nbase + r) * ldw + k0 + KLANE * g;
+    wp[0] = W + wrow(nbase);
+    wp[NT - 1] = W + wrow(inter + nbase);
   } else {
     nbase = blockIdx.x * (WAVES * NT * 16) + wave * (NT * 16);
 #pragma unroll
-    for (int t = 0; t < NT; ++t) wp[t] = W + (long)(nbase + 16 * t + r) * ldw + k0 + KLANE * g;
+    for (int t = 0; t < NT; ++t) wp[t] = W + wrow(nbase + 16 * t);
   }
 
   constexpr int XV = MT * 16 * (KC / 8);                // 16-B vectors per X chunk
@@ -133,7 +151,7 @@ gemm_skinny_kernel(const bf16_t* __restrict__ X, long ldx, const bf16_t* __restr
       for (int j = 0; j < XPT; ++j) {
         const int v = xt + j * XTHREADS;
         const int col = (v % (KC / 8)) * 8;
-        xr[j] = *reinterpret_cast<const bf16x8*>(X + (long)xrows[j] * ldx + k0 + c * KC + col);
+        xr[j] = *reinterpret_cast<const bf16x8*>(X + (long)xrows[j] * ldx + k0 + rc(c) * KC + col);
       }
     };
     auto store_x = [&](int buf, const bf16x8 (&xr)[XPT]) {
@@ -152,7 +170,7 @@ gemm_skinny_kernel(const bf16_t* __restrict__ X, long ldx, const bf16_t* __restr
 #pragma unroll
         for (int ss = 0; ss < KC / 128; ++ss)
 #pragma unroll
-          for (int s = 0; s < 4; ++s) w[t][ss * 4 + s] = ld_w(wp[t] + c * KC + 128 * ss + KSTEP * s);
+          for (int s = 0; s < 4; ++s) w[t][ss * 4 + s] = ld_w(wp[t] + (rc(c) * (KC / 128) + ss) * WS_SUPER + WS_STEP * s);
     };
 
     f32x4 acc[NT][MT];
@@ -401,21 +419,29 @@ splitk_add_rmsnorm_kernel(const float* __restrict__ part, int sk_rt, int M, int 
   }
 }
 
-template <int MT, int NT, int WAVES, int S, bool GROUPED, int KC, bool LOADER = false>
+template <int MT, int NT, int WAVES, int S, bool GROUPED, int KC, bool LOADER = false,
+          bool PACKED = false>
 int launch_cfg(const bf16_t* X, long ldx, const bf16_t* W, long ldw, const bf16_t* bias, void* out,
                long ldo, int M, int N, int K, int sk, int mode, int experts, const int* offs,
                const int* row_idx, long w_estride, hipStream_t st) {
   const size_t lds = 2ull * MT * 16 * (KC + XPAD) * sizeof(bf16_t);
   static bool attr_set = false;   // > 64 KiB of dynamic LDS must be opted into
   if (!attr_set) {
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(gemm_skinny_kernel<MT, NT, WAVES, S, GROUPED, KC, LOADER>),
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(gemm_skinny_kernel<MT, NT, WAVES, S, GROUPED, KC, LOADER, PACKED>),
                         hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     attr_set = true;
   }
+  // staggered K walk: measured +5-7% on the long single-split streams (gate_up, LM head),
+  // neutral to slightly negative on the short split-K ones.  EIA_GEMM_ROT overrides.
+  static const int rot_env = [] {
+    const char* e = getenv("EIA_GEMM_ROT");
+    return e != nullptr ? atoi(e) : -1;
+  }();
+  const int rot_mul = rot_env >= 0 ? rot_env : (sk == 1 ? 3 : 0);
   dim3 grid(mode == MODE_SWIGLU ? (N / 2) / (WAVES * 16) : N / (WAVES * NT * 16), sk, experts);
-  hipLaunchKernelGGL((gemm_skinny_kernel<MT, NT, WAVES, S, GROUPED, KC, LOADER>), grid, dim3(WAVES * 64 + (LOADER ? 64 : 0)), lds, st,
+  hipLaunchKernelGGL((gemm_skinny_kernel<MT, NT, WAVES, S, GROUPED, KC, LOADER, PACKED>), grid, dim3(WAVES * 64 + (LOADER ? 64 : 0)), lds, st,
                      X, ldx, W, ldw, bias, out, ldo, M, N, K / sk, mode, N / 2, offs, row_idx,
-                     w_estride);
+                     w_estride, GROUPED ? 0 : rot_mul);
   return (int)hipGetLastError();
 }
 
@@ -463,6 +489,26 @@ int launch_mt(int cfg, const bf16_t* X, long ldx, const bf16_t* W, long ldw, con
       case 27: EIA_CFG(2, 4, 4, 128);
       default: break;
     }
+#define EIA_CFGP(NT_, W_, S_, KC_, L_)                                                      \
+  return launch_cfg<MT, NT_, W_, S_, GROUPED, KC_, L_, true>(X, ldx, W, ldw, bias, out, ldo, M, \
+                                                            N, K, sk, mode, experts, offs,     \
+                                                            row_idx, w_estride, st)
+    // bit 6: tile-packed weights, for the configurations the decode tables use
+    switch (cfg) {
+      case 64 + 1: EIA_CFGP(2, 2, 2, 256, false);
+      case 64 + 2: EIA_CFGP(1, 4, 2, 256, false);
+      case 64 + 3: EIA_CFGP(2, 4, 2, 256, false);
+      case 64 + 7: EIA_CFGP(2, 4, 3, 256, false);
+      case 64 + 17: EIA_CFGP(2, 2, 2, 128, false);
+      case 64 + 18: EIA_CFGP(1, 4, 2, 128, false);
+      case 64 + 19: EIA_CFGP(2, 4, 2, 128, false);
+      case 64 + 22: EIA_CFGP(1, 4, 3, 128, false);
+      case 64 + 23: EIA_CFGP(2, 4, 3, 128, false);
+      case 64 + 51: EIA_CFGP(2, 4, 2, 128, true);
+      case 64 + 55: EIA_CFGP(2, 4, 3, 128, true);
+      default: break;
+    }
+#undef EIA_CFGP
     // bit 5: wave-specialised X loader (4 compute waves, 128-deep chunks)
     switch (cfg) {
       case 50: return launch_cfg<MT, 1, 4, 2, GROUPED, 128, true>(X, ldx, W, ldw, bias, out, ldo, M, N, K, sk, mode, experts, offs, row_idx, w_estride, st);
@@ -505,7 +551,7 @@ constexpr unsigned long long kSpillCfg[9] = {0x0ull, 0x8000a00ull, 0x8000a20ull,
 int check_shape(int N, int K, int sk, int mode, int cfg) {
   const int nt = (cfg & 1) ? 2 : 1, waves = (cfg & 2) ? 4 : 2;
   const int kc = (cfg & 16) ? 128 : 256;
-  if (sk < 1 || cfg < 0 || (cfg & ~(16 | 32)) > 11 || K % (sk * kc) != 0) return EIA_BAD_SHAPE;
+  if (sk < 1 || cfg < 0 || (cfg & ~(16 | 32 | 64)) > 11 || K % (sk * kc) != 0) return EIA_BAD_SHAPE;
   if ((cfg & 32) && !((cfg & 16) && (cfg & 2))) return EIA_BAD_SHAPE;   // loader: 4 waves, KC 128
   if (mode == MODE_SWIGLU) {
     if (nt != 2 || sk != 1 || N % 2 != 0 || (N / 2) % (waves * 16) != 0) return EIA_BAD_SHAPE;
@@ -523,14 +569,14 @@ int check_shape(int N, int K, int sk, int mode, int cfg) {
 // mode 2: SwiGLU: W = merged [gate; up] (N = 2I rows), out bf16 [M][ldo] = silu(gate) * up
 // cfg: bit0 -> two 16-row W tiles per wave (else one), bit1 -> 4 waves per workgroup (else 2),
 // bits 2-3 -> W pipeline stages - 2 (2..4), bit 4 -> 128-deep K chunks (else 256),
-// bit 5 -> extra X-loader wave (with bits 1 and 4)
+// bit 5 -> extra X-loader wave (with bits 1 and 4), bit 6 -> tile-packed W (ldw must be K)
 EIA_API int eia_gemm_skinny(const void* X, long ldx, const void* W, long ldw, const void* bias,
                             void* out, long ldo, int M, int N, int K, int sk, int mode, int cfg,
                             hipStream_t st) {
   if (M < 1 || M > 128) return EIA_BAD_SHAPE;
   if (int rc = check_shape(N, K, sk, mode, cfg)) return rc;
-  if ((kSpillCfg[(M + 15) / 16] >> cfg) & 1ull) return EIA_BAD_SHAPE;
-  if ((ldx % 8) || (ldw % 8) || (ldo % 4)) return EIA_BAD_SHAPE;
+  if ((kSpillCfg[(M + 15) / 16] >> (cfg & 63)) & 1ull) return EIA_BAD_SHAPE;
+  if ((ldx % 8) || (ldw % 8) || (ldo % 4) || ((cfg & 64) && ldw != K)) return EIA_BAD_SHAPE;
   return dispatch_mt<false>((M + 15) / 16, cfg, static_cast<const bf16_t*>(X), ldx,
                             static_cast<const bf16_t*>(W), ldw, static_cast<const bf16_t*>(bias),
                             out, ldo, M, N, K, sk, mode, 1, nullptr, nullptr, 0, st);
@@ -544,7 +590,7 @@ EIA_API int eia_gemm_skinny(const void* X, long ldx, const void* W, long ldw, co
 EIA_API int eia_moe_gemm(const void* X, long ldx, const void* W, long ldw, const void* bias,
                          void* out, long ldo, int N, int K, int experts, const int* offs,
                          const int* row_idx, int mt_hint, int mode, int cfg, hipStream_t st) {
-  if (experts < 1 || mode == MODE_F32_SPLIT || (cfg & 48)) return EIA_BAD_SHAPE;
+  if (experts < 1 || mode == MODE_F32_SPLIT || (cfg & 112)) return EIA_BAD_SHAPE;
   if (int rc = check_shape(N, K, 1, mode, cfg)) return rc;
   if ((ldx % 8) || (ldw % 8) || (ldo % 4)) return EIA_BAD_SHAPE;
   const int mt = mt_hint < 1 ? 1 : (mt_hint > 8 ? 8 : mt_hint);

@@ -32,6 +32,8 @@ MODE_BF16, MODE_SPLIT, MODE_SWIGLU = 0, 1, 2
 # bit0 NT=2, bit1 WAVES=4, bits2-3 pipeline stages-2, bit4 128-deep K chunks (else 256)
 # bit5: an extra wave stages X into LDS (4 compute waves, KC 128): 50, 51, 54, 55, 58, 59
 CFGS = tuple(range(12)) + tuple(range(16, 28)) + (50, 51, 54, 55, 58, 59)
+# bit6: tile-packed weights (pack_weight) for the layouts the decode tables use
+PACKED_CFGS = tuple(64 + c for c in (1, 2, 3, 7, 17, 18, 19, 22, 23, 51, 55))
 
 
 def cfg_kc(cfg: int) -> int:
@@ -70,11 +72,30 @@ SPILL_CFGS = {1: (9, 11, 27), 2: (5, 9, 11, 27), 3: (5, 7, 8, 9, 11, 23, 27), 4:
 def valid(N: int, K: int, swiglu: bool, cfg: int, sk: int, M: Optional[int] = None) -> bool:
     if K % (sk * cfg_kc(cfg)):
         return False
-    if M is not None and cfg in SPILL_CFGS.get(m_bucket(M), ()):
+    if M is not None and (cfg & 63) in SPILL_CFGS.get(m_bucket(M), ()):
         return False
     if swiglu:
         return sk == 1 and (cfg & 1) == 1 and (N // 2) % ((4 if cfg & 2 else 2) * 16) == 0
     return N % cfg_rows(cfg) == 0
+
+
+def pack_weight(w: torch.Tensor) -> torch.Tensor:
+    """[N, K] row-major -> the tile-packed layout of cfg bit 6 (same shape and dtype).
+
+    For each 16-row tile and 128-deep K block the kernel's four fragment loads per lane
+    (MFMA step s, lane = r + 16 g, k = 32 s + 8 g + j) become consecutive 1 KiB runs:
+    packed[tile, kb, s, g, r, j] = w[16 tile + r, 128 kb + 32 s + 8 g + j]."""
+    N, K = w.shape
+    assert N % 16 == 0 and K % 128 == 0, (N, K)
+    return w.reshape(N // 16, 16, K // 128, 4, 4, 8).permute(0, 2, 3, 4, 1, 5).contiguous() \
+        .view(N, K)
+
+
+def unpack_weight(p: torch.Tensor) -> torch.Tensor:
+    """Inverse of pack_weight."""
+    N, K = p.shape
+    return p.reshape(N // 16, K // 128, 4, 4, 16, 8).permute(0, 4, 1, 2, 3, 5).contiguous() \
+        .view(N, K)
 
 
 def heuristic_splitk(N: int, K: int, cfg: int, swiglu: bool = False) -> int:

@@ -80,6 +80,8 @@ def main():
     ap.add_argument("--tune", action="store_true")
     ap.add_argument("--sweep", action="store_true", help="time every candidate (no table write)")
     ap.add_argument("--out", default=None, help="also write the tuning table here")
+    ap.add_argument("--packed", action="store_true",
+                    help="sweep the tile-packed-weight configurations (cfg bit 6)")
     a = ap.parse_args()
     tuned = {}
     if a.tune and os.path.exists(gemm.TUNING_FILE):
@@ -89,6 +91,7 @@ def main():
         wbytes = N * K * 2
         pool = max(2, int(600e6 // wbytes) + 1)
         ws = [(torch.randn(N, K, device="cuda") * 0.02).to(torch.bfloat16) for _ in range(pool)]
+        wps = [gemm.pack_weight(w) for w in ws] if a.packed else ws
         for M in a.m:
             x = torch.randn(M, K, device="cuda", dtype=torch.bfloat16)
             if swiglu:
@@ -99,6 +102,10 @@ def main():
             tb = graph_time(base, a.iters)
             cands = candidates(M, N, K, swiglu) if (a.tune or a.sweep) else \
                 [c for c in [gemm.choose(M, N, K, swiglu)] if c[0] >= 0]
+            if a.packed:
+                cands = [(c, sk) for c in gemm.PACKED_CFGS for sk in {s for _, s in cands}
+                         if gemm.valid(N, K, swiglu, c, sk, M=M)
+                         and (N // gemm.cfg_rows(c)) * sk <= 4096]
             if not cands:
                 print(json.dumps({"shape": name, "M": M, "hipblaslt_us": round(tb, 2),
                                   "hipblaslt_TBps": round(wbytes / tb / 1e6, 2),
@@ -107,9 +114,11 @@ def main():
             results = []
             for cfg, sk in cands:
                 if swiglu:
-                    f = lambda i, cfg=cfg: gemm.swiglu_gemm(x, ws[i % pool], cfg=cfg)
+                    f = lambda i, cfg=cfg: gemm.swiglu_gemm(
+                        x, (wps if cfg & 64 else ws)[i % pool], cfg=cfg)
                 else:
-                    f = lambda i, cfg=cfg, sk=sk: gemm.skinny(x, ws[i % pool], cfg=cfg, sk=sk)
+                    f = lambda i, cfg=cfg, sk=sk: gemm.skinny(
+                        x, (wps if cfg & 64 else ws)[i % pool], cfg=cfg, sk=sk)
                 results.append((graph_time(f, a.iters), cfg, sk))
             results.sort()
             to, cfg, sk = results[0]
@@ -123,7 +132,7 @@ def main():
                 key = f"{gemm.m_bucket(M)},{N},{K},{int(swiglu)}"
                 # cfg -1 = "use hipBLASLt" (the skinny kernel lost on this shape)
                 tuned[key] = [cfg, sk] if to < tb * 1.02 else [-1, 1]
-        del ws
+        del ws, wps
         torch.cuda.empty_cache()
     if a.tune:
         with open(gemm.TUNING_FILE, "w") as f:

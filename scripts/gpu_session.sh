@@ -39,6 +39,13 @@ for s in $STEPS; do
     attn) run attn 300 python scripts/bench_attn.py ;;
     tune) run tune 1100 python scripts/bench_gemm.py --tune --m ${GEMM_M:-65} \
             --shapes ${GEMM_SHAPES:-qkv_8b o_8b gate_up_8b down_8b lm_head_8b} --out gpurun_out/gemm_tuning.json ;;
+    rot)  # staggered K-walk start (EIA_GEMM_ROT) on the tuned configs
+      for r in ${ROTS:-0 1 3 7}; do
+        EIA_GEMM_ROT=$r run rot_$r 300 python scripts/bench_gemm.py --m ${GEMM_M:-65} \
+          --shapes qkv_8b o_8b gate_up_8b down_8b lm_head_8b
+      done ;;
+    packed) run packed 900 python scripts/bench_gemm.py --packed --sweep --m ${GEMM_M:-65} \
+            --shapes ${GEMM_SHAPES:-qkv_8b o_8b gate_up_8b down_8b lm_head_8b} ;;
     probe) run probe 300 python scripts/probe_overlap.py ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac

@@ -11,7 +11,7 @@ import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 SRC = os.path.join(ROOT, "csrc", "kernels", "gemm_skinny.hip")
-PAT = re.compile(r"gemm_skinny_kernelILi(\d+)ELi(\d+)ELi(\d+)ELi(\d+)ELb([01])ELi(\d+)ELb([01])E")
+PAT = re.compile(r"gemm_skinny_kernelILi(\d+)ELi(\d+)ELi(\d+)ELi(\d+)ELb([01])ELi(\d+)ELb([01])ELb([01])E")
 
 
 def main() -> int:
@@ -37,7 +37,8 @@ def main() -> int:
         if m and int(m.group(2)) > 0:
             spill.add(cur)
     masks = [0] * 9
-    for mt, nt, waves, st, grouped, kc, loader in spill:
+    # packed-weight variants (cfg bit 6) share their base configuration's bit
+    for mt, nt, waves, st, grouped, kc, loader, _packed in spill:
         if grouped:
             continue
         cfg = (nt - 1) | ((waves // 2 - 1) << 1) | ((st - 2) << 2) | (16 if kc == 128 else 0) \

@@ -38,6 +38,31 @@ def test_skinny_linear(M, N, K):
             _check(out, _ref(x, w, b), f"M={M} N={N} K={K} cfg={cfg} sk={sk}")
 
 
+@pytest.mark.parametrize("M", [1, 16, 65, 100])
+@pytest.mark.parametrize("N,K", [(6144, 4096), (4096, 14336), (1280, 8192)])
+def test_skinny_packed_weights(M, N, K):
+    """cfg bit 6: the same GEMM reading the tile-packed weight layout."""
+    from enterprise_inference_amd.ops import gemm
+    torch.manual_seed(M + N)
+    x = torch.randn(M, K, device=DEV, dtype=BF)
+    w = (torch.randn(N, K, device=DEV) * K ** -0.5).to(BF)
+    wp = gemm.pack_weight(w)
+    ref = _ref(x, w)
+    ran = 0
+    for cfg in gemm.PACKED_CFGS:
+        for sk in sorted({1, gemm.heuristic_splitk(N, K, cfg)}):
+            if not gemm.valid(N, K, False, cfg, sk, M=M):
+                continue
+            _check(gemm.skinny(x, wp, cfg=cfg, sk=sk), ref, f"packed M={M} N={N} K={K} cfg={cfg} sk={sk}")
+            ran += 1
+    assert ran > 0
+    I = N // 2
+    y = F.silu(ref[:, :I]) * ref[:, I:]
+    for cfg in (64 + 1, 64 + 3, 64 + 7):
+        if gemm.valid(N, K, True, cfg, 1, M=M):
+            _check(gemm.swiglu_gemm(x, wp, cfg=cfg), y, f"packed swiglu M={M} cfg={cfg}")
+
+
 @pytest.mark.parametrize("M", [1, 17, 65, 128])
 def test_skinny_strided_input(M):
     from enterprise_inference_amd.ops import gemm

@@ -1,0 +1,25 @@
+"""Tile-packed weight layout of the skinny GEMM (cfg bit 6): pure index math, CPU."""
+import torch
+
+from enterprise_inference_amd.ops import gemm
+
+
+def test_pack_roundtrip_and_fragment_order():
+    N, K = 48, 384
+    w = torch.arange(N * K, dtype=torch.int64).view(N, K)
+    p = gemm.pack_weight(w)
+    assert p.shape == w.shape
+    assert torch.equal(gemm.unpack_weight(p), w)
+    flat = p.reshape(-1)
+    # the kernel's lane (r, g) fragment for MFMA step s of 128-block kb in tile t sits at
+    # t*16*K + kb*2048 + s*512 + (16 g + r)*8 .. +8, and holds w[16t + r, 128kb + 32s + 8g + j]
+    for t, kb, s, g, r in [(0, 0, 0, 0, 0), (1, 2, 3, 1, 7), (2, 1, 2, 3, 15)]:
+        off = t * 16 * K + kb * 2048 + s * 512 + (16 * g + r) * 8
+        k = 128 * kb + 32 * s + 8 * g
+        assert torch.equal(flat[off:off + 8], w[16 * t + r, k:k + 8])
+
+
+def test_packed_cfgs_share_base_validity():
+    for c in gemm.PACKED_CFGS:
+        assert c & 64 and (c & 63) in gemm.CFGS
+        assert gemm.cfg_rows(c) == gemm.cfg_rows(c & 63) and gemm.cfg_kc(c) == gemm.cfg_kc(c & 63)
