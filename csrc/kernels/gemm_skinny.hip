@@ -59,6 +59,58 @@ EIA_DEV bf16x8 ld_w(const bf16_t* p) {
 #endif
 }
 
+// Epilogue: lane (r, g) holds rows n = nbase + 16t + 4g + i, column m = 16*mt + r.
+// mode SWIGLU (NT == 2): tile 0 = gate, tile 1 = up; F32_SPLIT: fp32 slab blockIdx.y.
+template <int MT, int NT>
+EIA_DEV void store_tile(const f32x4 (&acc)[NT][MT], int mode, void* __restrict__ out, long ldo,
+                        int M, int N, int Mc, long orow0, int nbase, int r, int g,
+                        const bf16_t* __restrict__ bias) {
+  if (NT == 2 && mode == MODE_SWIGLU) {
+    bf16_t* o = reinterpret_cast<bf16_t*>(out);
+    const int n = nbase + 4 * g;
+#pragma unroll
+    for (int m = 0; m < MT; ++m) {
+      const int row = m * 16 + r;
+      if (row < Mc) {
+        bf16x4 v;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) v[i] = f2bf(silu(acc[0][m][i]) * acc[NT - 1][m][i]);
+        *reinterpret_cast<bf16x4*>(o + (orow0 + row) * ldo + n) = v;
+      }
+    }
+    return;
+  }
+#pragma unroll
+  for (int t = 0; t < NT; ++t) {
+    const int n = nbase + 16 * t + 4 * g;
+    if (mode == MODE_F32_SPLIT) {
+      float* o = reinterpret_cast<float*>(out) + (long)blockIdx.y * M * N;
+#pragma unroll
+      for (int m = 0; m < MT; ++m) {
+        const int row = m * 16 + r;
+        if (row < Mc) *reinterpret_cast<f32x4*>(o + (orow0 + row) * N + n) = acc[t][m];
+      }
+    } else {
+      bf16_t* o = reinterpret_cast<bf16_t*>(out);
+      float b[4] = {0.f, 0.f, 0.f, 0.f};
+      if (bias != nullptr) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) b[i] = bf2f(bias[n + i]);
+      }
+#pragma unroll
+      for (int m = 0; m < MT; ++m) {
+        const int row = m * 16 + r;
+        if (row < Mc) {
+          bf16x4 v;
+#pragma unroll
+          for (int i = 0; i < 4; ++i) v[i] = f2bf(acc[t][m][i] + b[i]);
+          *reinterpret_cast<bf16x4*>(o + (orow0 + row) * ldo + n) = v;
+        }
+      }
+    }
+  }
+}
+
 // MT: 16-column tiles of X (M <= 16*MT per pass); NT: 16-row W tiles per wave; WAVES per
 // workgroup.  GROUPED (MoE, K9): blockIdx.z = expert e, W += e * w_estride, the expert's
 // rows are [offs[e], offs[e+1]) of the expert-sorted token list, X rows are gathered
@@ -294,53 +346,143 @@ gemm_skinny_kernel(const bf16_t* __restrict__ X, long ldx, const bf16_t* __restr
           phase(c + s, w[s], w[(s + S - 1) % S], xr[(s + S - 1) % S], xr[(s + 1) % S]);
     }
 
-    // epilogue: lane (r, g) holds rows n = tile_base + 4g + i, column m = 16*mt + r
-    const long orow0 = mbase + m0;
-    if (NT == 2 && mode == MODE_SWIGLU) {
-      bf16_t* o = reinterpret_cast<bf16_t*>(out);
-      const int n = nbase + 4 * g;
-#pragma unroll
-      for (int m = 0; m < MT; ++m) {
-        const int row = m * 16 + r;
-        if (row < Mc) {
-          bf16x4 v;
-#pragma unroll
-          for (int i = 0; i < 4; ++i) v[i] = f2bf(silu(acc[0][m][i]) * acc[NT - 1][m][i]);
-          *reinterpret_cast<bf16x4*>(o + (orow0 + row) * ldo + n) = v;
-        }
-      }
-      continue;
-    }
-#pragma unroll
-    for (int t = 0; t < NT; ++t) {
-      const int n = nbase + 16 * t + 4 * g;
-      if (mode == MODE_F32_SPLIT) {
-        float* o = reinterpret_cast<float*>(out) + (long)blockIdx.y * M * N;
-#pragma unroll
-        for (int m = 0; m < MT; ++m) {
-          const int row = m * 16 + r;
-          if (row < Mc) *reinterpret_cast<f32x4*>(o + (orow0 + row) * N + n) = acc[t][m];
-        }
-      } else {
-        bf16_t* o = reinterpret_cast<bf16_t*>(out);
-        float b[4] = {0.f, 0.f, 0.f, 0.f};
-        if (bias != nullptr) {
-#pragma unroll
-          for (int i = 0; i < 4; ++i) b[i] = bf2f(bias[n + i]);
-        }
-#pragma unroll
-        for (int m = 0; m < MT; ++m) {
-          const int row = m * 16 + r;
-          if (row < Mc) {
-            bf16x4 v;
-#pragma unroll
-            for (int i = 0; i < 4; ++i) v[i] = f2bf(acc[t][m][i] + b[i]);
-            *reinterpret_cast<bf16x4*>(o + (orow0 + row) * ldo + n) = v;
-          }
-        }
-      }
-    }
+    store_tile<MT, NT>(acc, mode, out, ldo, M, N, Mc, mbase + m0, nbase, r, g, bias);
   }
+}
+
+// ---------------------------------------------------------------------------------------
+// LDS-DMA variant (cfg bit 7): W and X chunks travel HBM/L2 -> LDS by global_load_lds_dwordx4
+// (no VGPR staging), into a D-slot ring, so D-1 chunks per wave stay in flight whatever the
+// register budget.  Measured motivation (scripts/probe_gemm_floor.py): the register-staged
+// kernel streams ~11 B/clk per workgroup at any grid size -- latency-bound with one chunk in
+// flight.  Each lane's DMA source is the 16-B MFMA fragment it will later read, so every slot
+// is fragment-ordered ([tile][step][lane][16 B]) and the ds_read_b128s are conflict-free.
+// The DMAs are inline asm (untracked by hipcc's waitcnt pass): completion is counted here with
+// explicit vmcnt waits, and barriers are raw s_barrier (a __syncthreads() would drain vmcnt).
+// Phase c: wait until this wave's chunk-c DMAs landed, barrier (every wave's X part of chunk c
+// landed AND every wave finished chunk c-1), DMA chunk c+D-1 into slot (c-1)%D, multiply
+// chunk c.  4 waves; wave w DMAs X step w of every m-tile and its own W tiles.
+EIA_DEV void glds16(const void* gsrc, unsigned lds_addr) {
+  unsigned keep;
+  asm volatile(
+      "s_mov_b32 %0, m0\n\t"
+      "s_mov_b32 m0, %2\n\t"
+      "s_nop 0\n\t"
+      "global_load_lds_dwordx4 %1, off\n\t"
+      "s_mov_b32 m0, %0"
+      : "=&s"(keep)
+      : "v"(gsrc), "s"(__builtin_amdgcn_readfirstlane(lds_addr))
+      : "memory");
+}
+
+template <int N>
+EIA_DEV void wait_vmcnt() {
+  static_assert(N >= 0 && N < 64, "vmcnt range");
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+EIA_DEV void raw_barrier() { asm volatile("s_barrier" ::: "memory"); }
+
+template <int MT, int NT, int D>
+constexpr int glds_lds_bytes() { return D * (MT + 4 * NT) * 4096; }
+
+template <int MT, int NT, int D, bool PACKED>
+__global__ void __launch_bounds__(256, 1)
+gemm_glds_kernel(const bf16_t* __restrict__ X, long ldx, const bf16_t* __restrict__ W, long ldw,
+                 const bf16_t* __restrict__ bias, void* __restrict__ out, long ldo, int M, int N,
+                 int krange, int mode, int inter, int rot_mul) {
+  extern __shared__ __align__(16) bf16_t lds[];
+  constexpr int KC = 128;
+  constexpr int XSLOT = MT * 4 * 1024;             // bytes per X slot: [m][step][lane][16 B]
+  constexpr int WSLOT = NT * 4 * 1024;             // bytes per wave per W slot: [t][step][lane]
+  constexpr int PER_PHASE = MT + 4 * NT;           // DMAs per wave per chunk
+  const int lane = threadIdx.x & 63;
+  const int wave = threadIdx.x >> 6;
+  const int r = lane & 15, g = lane >> 4;
+  const int k0 = blockIdx.y * krange;
+  const int nchunks = krange / KC;
+  const int last = nchunks - 1;
+  const int rot = (int)(((unsigned)blockIdx.x * (unsigned)rot_mul) % (unsigned)nchunks);
+  auto rc = [&](int c) { const int t = c + rot; return t >= nchunks ? t - nchunks : t; };
+
+  const unsigned lds0 = (unsigned)(uintptr_t)lds;                  // LDS byte address
+  const unsigned xbase = __builtin_amdgcn_readfirstlane(lds0);
+  const unsigned wbase = __builtin_amdgcn_readfirstlane(lds0 + D * XSLOT + wave * D * WSLOT);
+
+  // this lane's W fragment sources (tile t, step 0, chunk 0)
+  const bf16_t* wp[NT];
+  int nbase;
+  auto wrow = [&](int row0) -> long {
+    if constexpr (PACKED) return (long)row0 * ldw + (long)(k0 / 128) * 2048 + lane * 8;
+    return (long)(row0 + r) * ldw + k0 + KLANE * g;
+  };
+  constexpr int WS_STEP = PACKED ? 512 : KSTEP;
+  constexpr int WS_CHUNK = PACKED ? 2048 : 128;
+  if (NT == 2 && mode == MODE_SWIGLU) {
+    nbase = blockIdx.x * (4 * 16) + wave * 16;
+    wp[0] = W + wrow(nbase);
+    wp[NT - 1] = W + wrow(inter + nbase);
+  } else {
+    nbase = blockIdx.x * (4 * NT * 16) + wave * (NT * 16);
+#pragma unroll
+    for (int t = 0; t < NT; ++t) wp[t] = W + wrow(nbase + 16 * t);
+  }
+  // this lane's X fragment sources: rows 16m + r (clamped to M-1), step = wave
+  const bf16_t* xp[MT];
+#pragma unroll
+  for (int m = 0; m < MT; ++m) {
+    const int row = min(16 * m + r, M - 1);
+    xp[m] = X + (long)row * ldx + k0 + KLANE * g + KSTEP * wave;
+  }
+
+  auto issue = [&](int c) {                // DMA chunk c (clamped) into slot c % D
+    const int cc = rc(min(c, last));
+    const int slot = c % D;
+#pragma unroll
+    for (int m = 0; m < MT; ++m)
+      glds16(xp[m] + cc * KC, xbase + slot * XSLOT + (m * 4 + wave) * 1024);
+#pragma unroll
+    for (int t = 0; t < NT; ++t)
+#pragma unroll
+      for (int s = 0; s < 4; ++s)
+        glds16(wp[t] + cc * WS_CHUNK + s * WS_STEP, wbase + slot * WSLOT + (t * 4 + s) * 1024);
+  };
+
+  f32x4 acc[NT][MT];
+#pragma unroll
+  for (int t = 0; t < NT; ++t)
+#pragma unroll
+    for (int m = 0; m < MT; ++m) acc[t][m] = (f32x4){0.f, 0.f, 0.f, 0.f};
+
+  const char* lb = reinterpret_cast<const char*>(lds);
+  auto compute = [&](int slot) {
+    const char* xs = lb + slot * XSLOT + lane * 16;
+    const char* ws = lb + D * XSLOT + (wave * D + slot) * WSLOT + lane * 16;
+#pragma unroll
+    for (int st = 0; st < 4; ++st) {
+      bf16x8 wf[NT], xf[MT];
+#pragma unroll
+      for (int t = 0; t < NT; ++t) wf[t] = *reinterpret_cast<const bf16x8*>(ws + (t * 4 + st) * 1024);
+#pragma unroll
+      for (int m = 0; m < MT; ++m) xf[m] = *reinterpret_cast<const bf16x8*>(xs + (m * 4 + st) * 1024);
+#pragma unroll
+      for (int m = 0; m < MT; ++m)
+#pragma unroll
+        for (int t = 0; t < NT; ++t)
+          acc[t][m] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[t], xf[m], acc[t][m], 0, 0, 0);
+    }
+  };
+
+#pragma unroll
+  for (int c = 0; c < D - 1; ++c) issue(c);
+  for (int c = 0; c < nchunks; ++c) {
+    wait_vmcnt<(D - 2) * PER_PHASE>();     // this wave's chunk-c DMAs have landed
+    raw_barrier();                         // ... and every wave's; chunk c-1 fully consumed
+    issue(c + D - 1);
+    compute(c % D);
+  }
+  wait_vmcnt<0>();                         // no DMA may land after the workgroup exits
+  store_tile<MT, NT>(acc, mode, out, ldo, M, N, M, 0, nbase, r, g, bias);
 }
 
 // Sum SK fp32 slabs [SK][M][N] (+bias) -> bf16 out[M][ldo].  One thread per 4 columns.
@@ -445,6 +587,26 @@ int launch_cfg(const bf16_t* X, long ldx, const bf16_t* W, long ldw, const bf16_
   return (int)hipGetLastError();
 }
 
+template <int MT, int NT, int D, bool PACKED>
+int launch_glds(const bf16_t* X, long ldx, const bf16_t* W, long ldw, const bf16_t* bias, void* out,
+                long ldo, int M, int N, int K, int sk, int mode, int rot_mul, hipStream_t st) {
+  if constexpr (glds_lds_bytes<MT, NT, D>() > 160 * 1024) {
+    return EIA_BAD_SHAPE;
+  } else {
+    constexpr size_t lds = glds_lds_bytes<MT, NT, D>();
+    static bool attr_set = false;
+    if (!attr_set) {
+      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(gemm_glds_kernel<MT, NT, D, PACKED>),
+                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+      attr_set = true;
+    }
+    dim3 grid(mode == MODE_SWIGLU ? (N / 2) / 64 : N / (64 * NT), sk);
+    hipLaunchKernelGGL((gemm_glds_kernel<MT, NT, D, PACKED>), grid, dim3(256), lds, st, X, ldx, W,
+                       ldw, bias, out, ldo, M, N, K / sk, mode, N / 2, rot_mul);
+    return (int)hipGetLastError();
+  }
+}
+
 template <int MT, bool GROUPED>
 int launch_mt(int cfg, const bf16_t* X, long ldx, const bf16_t* W, long ldw, const bf16_t* bias,
               void* out, long ldo, int M, int N, int K, int sk, int mode, int experts,
@@ -462,6 +624,31 @@ int launch_mt(int cfg, const bf16_t* X, long ldx, const bf16_t* W, long ldw, con
       default: EIA_CFG(2, 4, 2, 256);
     }
   } else {
+    if (cfg & 128) {   // LDS-DMA ring: cfg = 128|16|2 | (NT-1) | (D-2)<<2 | packed<<6
+      static const int rot_env = [] {
+        const char* e = getenv("EIA_GEMM_ROT");
+        return e != nullptr ? atoi(e) : -1;
+      }();
+      const int rot = rot_env >= 0 ? rot_env : (sk == 1 ? 3 : 0);
+#define EIA_GL(NT_, D_, P_) \
+  return launch_glds<MT, NT_, D_, P_>(X, ldx, W, ldw, bias, out, ldo, M, N, K, sk, mode, rot, st)
+      switch (cfg & ~(128 | 16 | 2)) {
+        case 0: EIA_GL(1, 2, false);
+        case 1: EIA_GL(2, 2, false);
+        case 4: EIA_GL(1, 3, false);
+        case 5: EIA_GL(2, 3, false);
+        case 8: EIA_GL(1, 4, false);
+        case 9: EIA_GL(2, 4, false);
+        case 64: EIA_GL(1, 2, true);
+        case 65: EIA_GL(2, 2, true);
+        case 68: EIA_GL(1, 3, true);
+        case 69: EIA_GL(2, 3, true);
+        case 72: EIA_GL(1, 4, true);
+        case 73: EIA_GL(2, 4, true);
+        default: return EIA_BAD_SHAPE;
+      }
+#undef EIA_GL
+    }
     switch (cfg) {
       case 0: EIA_CFG(1, 2, 2, 256);
       case 1: EIA_CFG(2, 2, 2, 256);
@@ -551,8 +738,10 @@ constexpr unsigned long long kSpillCfg[9] = {0x0ull, 0x8000a00ull, 0x8000a20ull,
 int check_shape(int N, int K, int sk, int mode, int cfg) {
   const int nt = (cfg & 1) ? 2 : 1, waves = (cfg & 2) ? 4 : 2;
   const int kc = (cfg & 16) ? 128 : 256;
-  if (sk < 1 || cfg < 0 || (cfg & ~(16 | 32 | 64)) > 11 || K % (sk * kc) != 0) return EIA_BAD_SHAPE;
+  if (sk < 1 || cfg < 0 || (cfg & ~(16 | 32 | 64 | 128)) > 11 || K % (sk * kc) != 0) return EIA_BAD_SHAPE;
   if ((cfg & 32) && !((cfg & 16) && (cfg & 2))) return EIA_BAD_SHAPE;   // loader: 4 waves, KC 128
+  if ((cfg & 128) && ((cfg & 32) || !(cfg & 16) || !(cfg & 2) || ((cfg >> 2) & 3) == 3))
+    return EIA_BAD_SHAPE;                                                // LDS-DMA ring
   if (mode == MODE_SWIGLU) {
     if (nt != 2 || sk != 1 || N % 2 != 0 || (N / 2) % (waves * 16) != 0) return EIA_BAD_SHAPE;
   } else if (N % (waves * nt * 16) != 0) {
@@ -569,13 +758,17 @@ int check_shape(int N, int K, int sk, int mode, int cfg) {
 // mode 2: SwiGLU: W = merged [gate; up] (N = 2I rows), out bf16 [M][ldo] = silu(gate) * up
 // cfg: bit0 -> two 16-row W tiles per wave (else one), bit1 -> 4 waves per workgroup (else 2),
 // bits 2-3 -> W pipeline stages - 2 (2..4), bit 4 -> 128-deep K chunks (else 256),
-// bit 5 -> extra X-loader wave (with bits 1 and 4), bit 6 -> tile-packed W (ldw must be K)
+// bit 5 -> extra X-loader wave (with bits 1 and 4), bit 6 -> tile-packed W (ldw must be K),
+// bit 7 -> LDS-DMA ring kernel (with bits 1 and 4; bits 2-3 = ring depth - 2)
 EIA_API int eia_gemm_skinny(const void* X, long ldx, const void* W, long ldw, const void* bias,
                             void* out, long ldo, int M, int N, int K, int sk, int mode, int cfg,
                             hipStream_t st) {
   if (M < 1 || M > 128) return EIA_BAD_SHAPE;
   if (int rc = check_shape(N, K, sk, mode, cfg)) return rc;
-  if ((kSpillCfg[(M + 15) / 16] >> (cfg & 63)) & 1ull) return EIA_BAD_SHAPE;
+  if (!(cfg & 128) && ((kSpillCfg[(M + 15) / 16] >> (cfg & 63)) & 1ull)) return EIA_BAD_SHAPE;
+  if ((cfg & 128) && (long)(((cfg >> 2) & 3) + 2) * ((M + 15) / 16 + 4 * ((cfg & 1) + 1)) * 4096 >
+                         160 * 1024)
+    return EIA_BAD_SHAPE;
   if ((ldx % 8) || (ldw % 8) || (ldo % 4) || ((cfg & 64) && ldw != K)) return EIA_BAD_SHAPE;
   return dispatch_mt<false>((M + 15) / 16, cfg, static_cast<const bf16_t*>(X), ldx,
                             static_cast<const bf16_t*>(W), ldw, static_cast<const bf16_t*>(bias),
@@ -590,7 +783,7 @@ EIA_API int eia_gemm_skinny(const void* X, long ldx, const void* W, long ldw, co
 EIA_API int eia_moe_gemm(const void* X, long ldx, const void* W, long ldw, const void* bias,
                          void* out, long ldo, int N, int K, int experts, const int* offs,
                          const int* row_idx, int mt_hint, int mode, int cfg, hipStream_t st) {
-  if (experts < 1 || mode == MODE_F32_SPLIT || (cfg & 112)) return EIA_BAD_SHAPE;
+  if (experts < 1 || mode == MODE_F32_SPLIT || (cfg & 240)) return EIA_BAD_SHAPE;
   if (int rc = check_shape(N, K, 1, mode, cfg)) return rc;
   if ((ldx % 8) || (ldw % 8) || (ldo % 4)) return EIA_BAD_SHAPE;
   const int mt = mt_hint < 1 ? 1 : (mt_hint > 8 ? 8 : mt_hint);

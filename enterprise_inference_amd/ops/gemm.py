@@ -31,9 +31,17 @@ MODE_BF16, MODE_SPLIT, MODE_SWIGLU = 0, 1, 2
 # kernel configs: bit0 -> 2 W tiles (32 rows) per wave, bit1 -> 4 waves per workgroup
 # bit0 NT=2, bit1 WAVES=4, bits2-3 pipeline stages-2, bit4 128-deep K chunks (else 256)
 # bit5: an extra wave stages X into LDS (4 compute waves, KC 128): 50, 51, 54, 55, 58, 59
-CFGS = tuple(range(12)) + tuple(range(16, 28)) + (50, 51, 54, 55, 58, 59)
+CFGS = tuple(range(12)) + tuple(range(16, 28)) + (50, 51, 54, 55, 58, 59) + \
+    (146, 147, 150, 151, 154, 155)
 # bit6: tile-packed weights (pack_weight) for the layouts the decode tables use
-PACKED_CFGS = tuple(64 + c for c in (1, 2, 3, 7, 17, 18, 19, 22, 23, 51, 55))
+PACKED_CFGS = tuple(64 + c for c in (1, 2, 3, 7, 17, 18, 19, 22, 23, 51, 55, 146, 147, 150, 151, 154, 155))
+# bit7: LDS-DMA ring kernel, 4 waves, KC 128: 146 | (NT-1) | (depth-2) << 2 (+64 packed)
+GLDS_CFGS = (146, 147, 150, 151, 154, 155)
+GLDS_PACKED_CFGS = tuple(c + 64 for c in GLDS_CFGS)
+
+
+def glds_lds_bytes(cfg: int, M: int) -> int:
+    return (((cfg >> 2) & 3) + 2) * ((M + 15) // 16 + 4 * ((cfg & 1) + 1)) * 4096
 
 
 def cfg_kc(cfg: int) -> int:
@@ -72,7 +80,10 @@ SPILL_CFGS = {1: (9, 11, 27), 2: (5, 9, 11, 27), 3: (5, 7, 8, 9, 11, 23, 27), 4:
 def valid(N: int, K: int, swiglu: bool, cfg: int, sk: int, M: Optional[int] = None) -> bool:
     if K % (sk * cfg_kc(cfg)):
         return False
-    if M is not None and (cfg & 63) in SPILL_CFGS.get(m_bucket(M), ()):
+    if cfg & 128:
+        if M is not None and glds_lds_bytes(cfg, M) > 160 * 1024:
+            return False
+    elif M is not None and (cfg & 63) in SPILL_CFGS.get(m_bucket(M), ()):
         return False
     if swiglu:
         return sk == 1 and (cfg & 1) == 1 and (N // 2) % ((4 if cfg & 2 else 2) * 16) == 0
