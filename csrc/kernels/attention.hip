@@ -13,6 +13,8 @@
 //     (4 consecutive tokens each) per 16-row d-tile -- no LDS transpose at all.
 // Decode splits a sequence's context into P partitions (grid.z) so that small
 // batches still fill 256 CUs; a reduce kernel merges (m, l, O) partials.
+#include <cstdlib>
+
 #include "eia_common.h"
 
 #define NEG_INF (-INFINITY)
@@ -142,34 +144,36 @@ EIA_DEV void attn_unit(WaveAcc<D>& acc, const bf16x8 (&qf)[D / 32],
   compute_unit<D>(acc, qf, f, tb, L, scale_log2, q_abs, kv_lo);
 }
 
-// Units ub+w, ub+w+4, ... (< ue) of one wave with the next unit's K/V in flight while the
+// Units ub+w, ub+w+NW, ... (< ue) of one wave with the next unit's K/V in flight while the
 // current one is multiplied (two named fragment sets; the prefetch index is clamped instead
 // of predicated so the vmcnt accounting stays static).
 template <int D>
 EIA_DEV void attn_units_pipelined(WaveAcc<D>& acc, const bf16x8 (&qf)[D / 32],
                                   const bf16_t* __restrict__ kc, const bf16_t* __restrict__ vc,
                                   const int* __restrict__ bt, int ub, int ue, int w, int L, int kvh,
-                                  int Hkv, int bs, float scale_log2, int kv_lo) {
+                                  int Hkv, int bs, float scale_log2, int kv_lo, int NW = 4) {
   int u = ub + w;
   if (u >= ue) return;
   KVFrag<D> fa, fb;
   load_unit<D>(fa, kc, vc, bt, 32 * u, L, kvh, Hkv, bs);
   for (;;) {
-    load_unit<D>(fb, kc, vc, bt, 32 * min(u + 4, ue - 1), L, kvh, Hkv, bs);
+    load_unit<D>(fb, kc, vc, bt, 32 * min(u + NW, ue - 1), L, kvh, Hkv, bs);
     compute_unit<D>(acc, qf, fa, 32 * u, L, scale_log2, 0x7fffffff, kv_lo);
-    u += 4;
+    u += NW;
     if (u >= ue) break;
-    load_unit<D>(fa, kc, vc, bt, 32 * min(u + 4, ue - 1), L, kvh, Hkv, bs);
+    load_unit<D>(fa, kc, vc, bt, 32 * min(u + NW, ue - 1), L, kvh, Hkv, bs);
     compute_unit<D>(acc, qf, fb, 32 * u, L, scale_log2, 0x7fffffff, kv_lo);
-    u += 4;
+    u += NW;
     if (u >= ue) break;
   }
 }
 
 // ---------------------------------------------------------------------------------- decode
 
-template <int D>
-__global__ void __launch_bounds__(256, D <= 128 ? 2 : 1)
+// NW waves per workgroup: 4 (default), or 2 (EIA_DECODE_WAVES=2; 4 workgroups per CU
+// resident instead of 2, but each wave walks twice the units -- measured slower).
+template <int D, int NW>
+__global__ void __launch_bounds__(NW * 64, D <= 128 ? 8 / NW : 4 / NW)
 paged_decode_kernel(const bf16_t* __restrict__ q, long q_stride,
                     const bf16_t* __restrict__ kc, const bf16_t* __restrict__ vc,
                     const int* __restrict__ block_tables, int bt_stride,
@@ -180,9 +184,9 @@ paged_decode_kernel(const bf16_t* __restrict__ q, long q_stride,
                     float scale_log2, int Hq, int Hkv, int bs, int Pmax, int NQG,
                     int sliding_window, int chunk_size, const int* __restrict__ p_dyn) {
   __shared__ int s_last;
-  __shared__ float sm[4][16];
-  __shared__ float sl[4][16];
-  __shared__ float so[4][D][17];
+  __shared__ float sm[NW][16];
+  __shared__ float sl[NW][16];
+  __shared__ float so[NW][D][17];
 
   const int b = blockIdx.x;
   const int kvh = blockIdx.y / NQG, qg = blockIdx.y % NQG;
@@ -224,7 +228,7 @@ paged_decode_kernel(const bf16_t* __restrict__ q, long q_stride,
   const int U = (L + 31) / 32 - U0;
   const int ub = U0 + (int)(((long)p * U) / P), ue = U0 + (int)(((long)(p + 1) * U) / P);
   const int* bt = block_tables + (long)b * bt_stride;
-  attn_units_pipelined<D>(acc, qf, kc, vc, bt, ub, ue, w, L, kvh, Hkv, bs, scale_log2, kv_lo);
+  attn_units_pipelined<D>(acc, qf, kc, vc, bt, ub, ue, w, L, kvh, Hkv, bs, scale_log2, kv_lo, NW);
 
   float lt = acc.l;
   lt += __shfl_xor(lt, 16, 64);
@@ -241,11 +245,11 @@ paged_decode_kernel(const bf16_t* __restrict__ q, long q_stride,
     if (cq >= nq) continue;
     float M = NEG_INF;
 #pragma unroll
-    for (int ww = 0; ww < 4; ++ww) M = fmaxf(M, sm[ww][cq]);
+    for (int ww = 0; ww < NW; ++ww) M = fmaxf(M, sm[ww][cq]);
     float Ls = 0.f, O = 0.f;
     if (M != NEG_INF) {
 #pragma unroll
-      for (int ww = 0; ww < 4; ++ww) {
+      for (int ww = 0; ww < NW; ++ww) {
         const float f = exp2f(sm[ww][cq] - M);
         Ls += sl[ww][cq] * f;
         O += so[ww][d][cq] * f;
@@ -410,12 +414,21 @@ EIA_API int eia_paged_decode(const void* q, long q_stride, const void* k_cache, 
   const int G = Hq / Hkv;
   const int NQG = (G + 15) / 16;
   const float sl2 = scale * 1.4426950408889634f;
-  dim3 grid(B, Hkv * NQG, P), block(256);
+  static const int nw_env = [] {
+    const char* e = getenv("EIA_DECODE_WAVES");
+    return e != nullptr ? atoi(e) : 0;
+  }();
+  // 4 waves by default: the 2-wave form measured 1.9-2.2x slower at B = 16..65, ctx 192..1024
+  // (scripts/bench_attn.py, EIA_DECODE_WAVES=2), even where the 4-wave grid overflows one round
+  const int nw = nw_env == 2 ? 2 : 4;
+  dim3 grid(B, Hkv * NQG, P);
+#define DEC_NW(DD, NW_)                                                                      \
+  hipLaunchKernelGGL((paged_decode_kernel<DD, NW_>), grid, dim3(64 * NW_), 0, st, (const bf16_t*)q, \
+                     q_stride, (const bf16_t*)k_cache, (const bf16_t*)v_cache, block_tables,      \
+                     bt_stride, seq_lens, (bf16_t*)out, out_stride, part_o, part_ml, part_cnt, sl2, \
+                     Hq, Hkv, bs, P, NQG, sliding_window, chunk_size, p_dyn);
 #define DEC(DD)                                                                             \
-  hipLaunchKernelGGL((paged_decode_kernel<DD>), grid, block, 0, st, (const bf16_t*)q, q_stride, \
-                     (const bf16_t*)k_cache, (const bf16_t*)v_cache, block_tables, bt_stride, \
-                     seq_lens, (bf16_t*)out, out_stride, part_o, part_ml, part_cnt, sl2, Hq, Hkv, bs, \
-                     P, NQG, sliding_window, chunk_size, p_dyn);                             \
+  if (nw == 2) { DEC_NW(DD, 2) } else { DEC_NW(DD, 4) }                                    \
   if (P > 1 && part_cnt == nullptr)                                                         \
     hipLaunchKernelGGL((paged_decode_reduce_kernel<DD>), dim3(B, Hq), dim3(DD < 256 ? DD : 256), 0, st, \
                        part_o, part_ml, (bf16_t*)out, out_stride, Hq, P, p_dyn);
@@ -426,6 +439,7 @@ EIA_API int eia_paged_decode(const void* q, long q_stride, const void* k_cache, 
     default: return EIA_UNSUPPORTED;
   }
 #undef DEC
+#undef DEC_NW
   EIA_LAUNCH_CHECK();
 }
 
