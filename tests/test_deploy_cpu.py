@@ -104,3 +104,46 @@ def test_read_config_file_and_platform(tmp_path):
     r = _bash(f'read_config_file "{cfg}" && normalise_platform && echo "$cpu_or_gpu $gpu_platform"')
     assert r.returncode == 0, r.stderr
     assert r.stdout.strip().splitlines()[-1] == "g mi300x"
+
+
+def test_playbook_file_references_exist():
+    """Files a playbook names under helm_charts_base / tasks/ exist in the tree."""
+    import re
+    pb_dir = os.path.join(ROOT, "playbooks")
+    for f in glob.glob(pb_dir + "/*.yml") + glob.glob(pb_dir + "/tasks/*.yml"):
+        s = open(f).read()
+        for rel in re.findall(r"(?<!remote_)helm_charts_base(?: ~ '|\s*}}\s*)(/[\w./-]+)", s):
+            assert os.path.exists(os.path.join(ROOT, "helm-charts") + rel.rstrip("'")), (f, rel)
+        for inc in re.findall(r"include_tasks:\s*([\w./-]+\.yml)", s):
+            base = os.path.dirname(f)
+            assert os.path.exists(os.path.join(base, inc)), (f, inc)
+
+
+def test_istio_and_ceph_flow_wiring():
+    istio = open(os.path.join(ROOT, "lib/components/istio.sh")).read()
+    assert "deploy-istio-openshift.yml" in istio and "deploy-istio.yml" in istio
+    ceph = open(os.path.join(ROOT, "lib/components/ceph.sh")).read()
+    assert ceph.index("generate-ceph-values.yml") < ceph.index("deploy-ceph-storage.yml")
+    pa = list(yaml.safe_load_all(open(os.path.join(ROOT, "helm-charts/istio/peer-auth-ingress.yaml"))))
+    assert pa[0]["spec"]["portLevelMtls"][443]["mode"] == "PERMISSIVE"
+
+
+def test_ibm_pattern_files():
+    d = os.path.join(os.path.dirname(ROOT), "third_party/IBM/patterns/quickstart")
+    for f in ("main.tf", "variables.tf", "versions.tf", "inference-config.tpl", "run_script.sh",
+              "templates/inventory.yaml.tftpl"):
+        assert os.path.exists(os.path.join(d, f)), f
+    r = subprocess.run(["bash", "-n", os.path.join(d, "run_script.sh")], capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr
+    # every ${var} of the config template is supplied by main.tf's templatefile() call
+    import re
+    tpl_vars = set(re.findall(r"\$\{(\w+)\}", open(os.path.join(d, "inference-config.tpl")).read()))
+    main = open(os.path.join(d, "main.tf")).read()
+    block = main[main.index('templatefile("${path.module}/inference-config.tpl"'):]
+    block = block[:block.index("})")]
+    assert tpl_vars <= set(re.findall(r"^\s*(\w+)\s*=", block, re.M)), tpl_vars
+    # keys written into inference-config.cfg are ones the installer reads
+    cfg_keys = {l.split("=")[0] for l in open(os.path.join(ROOT, "inventory/inference-config.cfg"))
+                if "=" in l}
+    tpl_keys = {l.split("=")[0] for l in open(os.path.join(d, "inference-config.tpl")) if "=" in l}
+    assert tpl_keys <= cfg_keys, tpl_keys - cfg_keys
