@@ -18,6 +18,9 @@
 #include "eia_common.h"
 
 #define NEG_INF (-INFINITY)
+#ifndef EIA_LEAN_OCC
+#define EIA_LEAN_OCC 3
+#endif
 
 template <int D>
 struct WaveAcc {
@@ -47,8 +50,42 @@ struct KVFrag {
 };
 
 template <int D>
+struct KVPtr {
+  const bf16_t *kp0, *kp1, *vp;
+};
+
+template <int D>
+EIA_DEV KVPtr<D> unit_ptrs(const bf16_t* __restrict__ kc, const bf16_t* __restrict__ vc,
+                           const int* __restrict__ bt, int tb, int L, int kvh, int Hkv, int bs);
+
+template <int D>
+EIA_DEV void load_k(bf16x8 (&k0)[D / 32], bf16x8 (&k1)[D / 32], const KVPtr<D>& p) {
+#pragma unroll
+  for (int s = 0; s < D / 32; ++s) {
+    k0[s] = *reinterpret_cast<const bf16x8*>(p.kp0 + 32 * s);
+    k1[s] = *reinterpret_cast<const bf16x8*>(p.kp1 + 32 * s);
+  }
+}
+
+template <int D>
+EIA_DEV void load_v(bf16x8 (&v)[D / 16], const KVPtr<D>& p, int bs) {
+  const int c = threadIdx.x & 15;
+#pragma unroll
+  for (int dt = 0; dt < D / 16; ++dt)
+    v[dt] = *reinterpret_cast<const bf16x8*>(p.vp + (long)(16 * dt + c) * bs);
+}
+
+template <int D>
 EIA_DEV void load_unit(KVFrag<D>& f, const bf16_t* __restrict__ kc, const bf16_t* __restrict__ vc,
                        const int* __restrict__ bt, int tb, int L, int kvh, int Hkv, int bs) {
+  const KVPtr<D> p = unit_ptrs<D>(kc, vc, bt, tb, L, kvh, Hkv, bs);
+  load_k<D>(f.k0, f.k1, p);
+  load_v<D>(f.v, p, bs);
+}
+
+template <int D>
+EIA_DEV KVPtr<D> unit_ptrs(const bf16_t* __restrict__ kc, const bf16_t* __restrict__ vc,
+                           const int* __restrict__ bt, int tb, int L, int kvh, int Hkv, int bs) {
   const int lane = threadIdx.x & 63;
   const int c = lane & 15, g = lane >> 4;
   const int tk0 = tb + 8 * (c >> 2) + (c & 3), tk1 = tk0 + 4;
@@ -71,32 +108,32 @@ EIA_DEV void load_unit(KVFrag<D>& f, const bf16_t* __restrict__ kc, const bf16_t
     kp1 = kc + ((long)bt[min(tk1 / bs, lastb)] * Hkv + kvh) * hk + (long)(tk1 % bs) * D + 8 * g;
     vp = vc + ((long)bt[min(tv / bs, lastb)] * Hkv + kvh) * hk + (tv % bs);
   }
-#pragma unroll
-  for (int s = 0; s < D / 32; ++s) {
-    f.k0[s] = *reinterpret_cast<const bf16x8*>(kp0 + 32 * s);
-    f.k1[s] = *reinterpret_cast<const bf16x8*>(kp1 + 32 * s);
-  }
-#pragma unroll
-  for (int dt = 0; dt < D / 16; ++dt)
-    f.v[dt] = *reinterpret_cast<const bf16x8*>(vp + (long)(16 * dt + c) * bs);
+  return KVPtr<D>{kp0, kp1, vp};
 }
 
-// Tokens [tb, tb+32) of one sequence for one wave (fragments already loaded).
-//   qf      : Q^T B-operand fragments (pre-loaded)
+// S^T tiles of one 32-token unit: K (A operand) x Q^T (B operand).
+template <int D>
+EIA_DEV void qk_unit(f32x4& s0, f32x4& s1, const bf16x8 (&qf)[D / 32], const bf16x8 (&k0)[D / 32],
+                     const bf16x8 (&k1)[D / 32]) {
+  s0 = (f32x4){0.f, 0.f, 0.f, 0.f};
+  s1 = (f32x4){0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int s = 0; s < D / 32; ++s) {
+    s0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(k0[s], qf[s], s0, 0, 0, 0);
+    s1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(k1[s], qf[s], s1, 0, 0, 0);
+  }
+}
+
+// Online softmax of tokens [tb, tb+32) of one sequence for one wave, and the P*V update.
 //   q_abs   : absolute position of this lane's query column (INT_MAX: no causal mask)
 //   kv_lo   : first token this lane's column may attend to (sliding window / chunk)
 // Tokens >= L inside the last block hold finite stale/zero data and are masked to p = 0.
 template <int D>
-EIA_DEV void compute_unit(WaveAcc<D>& acc, const bf16x8 (&qf)[D / 32], const KVFrag<D>& f, int tb,
-                          int L, float scale_log2, int q_abs, int kv_lo) {
+EIA_DEV void softmax_pv(WaveAcc<D>& acc, const f32x4& s0, const f32x4& s1,
+                        const bf16x8 (&vfr)[D / 16], int tb, int L, float scale_log2, int q_abs,
+                        int kv_lo) {
   const int lane = threadIdx.x & 63;
   const int g = lane >> 4;
-  f32x4 s0 = {0.f, 0.f, 0.f, 0.f}, s1 = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-  for (int s = 0; s < D / 32; ++s) {
-    s0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(f.k0[s], qf[s], s0, 0, 0, 0);
-    s1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(f.k1[s], qf[s], s1, 0, 0, 0);
-  }
   float v[8];
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
@@ -131,7 +168,96 @@ EIA_DEV void compute_unit(WaveAcc<D>& acc, const bf16x8 (&qf)[D / 32], const KVF
   }
 #pragma unroll
   for (int dt = 0; dt < D / 16; ++dt)
-    acc.o[dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(f.v[dt], pb, acc.o[dt], 0, 0, 0);
+    acc.o[dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vfr[dt], pb, acc.o[dt], 0, 0, 0);
+}
+
+template <int D>
+EIA_DEV void compute_unit(WaveAcc<D>& acc, const bf16x8 (&qf)[D / 32], const KVFrag<D>& f, int tb,
+                          int L, float scale_log2, int q_abs, int kv_lo) {
+  f32x4 s0, s1;
+  qk_unit<D>(s0, s1, qf, f.k0, f.k1);
+  softmax_pv<D>(acc, s0, s1, f.v, tb, L, scale_log2, q_abs, kv_lo);
+}
+
+// Lean pipeline: the next unit's K is issued before this unit's QK and its V right after it,
+// into the registers this unit's K just freed, so the live fragments peak at K + V + K'
+// (96 VGPRs at D = 128) instead of two full K/V sets (128): three decode workgroups fit a CU
+// (768 resident instead of 512 -- B = 65 x 8 KV heads = 520 then runs in one round).
+// Addressing (block size a multiple of 32, so a unit never straddles a block): the unit's K/V
+// bases are wave-uniform (one scalar block-table read) and each lane adds a CONSTANT 32-bit
+// byte offset, so the loads take the SGPR-base + VGPR-offset form -- no per-unit 64-bit
+// per-lane pointers held in VGPRs.
+template <int D>
+EIA_DEV void attn_units_lean(WaveAcc<D>& acc, const bf16x8 (&qs)[D / 32][64],
+                             const bf16_t* __restrict__ kc, const bf16_t* __restrict__ vc,
+                             const int* __restrict__ bt, int ub, int ue, int w, int L, int kvh,
+                             int Hkv, int bs, float scale_log2, int kv_lo, int NW) {
+  // the unit index is wave-uniform; say so, or the per-unit bases become 64-bit VGPR pointers
+  int u = __builtin_amdgcn_readfirstlane(ub + w);
+  if (u >= ue) return;
+  const int lane = threadIdx.x & 63;
+  const int c = lane & 15, g = lane >> 4;
+  const long hk = (long)bs * D;
+  // lane byte offsets inside a unit: K rows 8(c>>2)+(c&3) (+4 for tile 1), 16-B column group g;
+  // V^T row (dim) c of each 16-dim tile, tokens 8g..8g+7
+  const unsigned koff = (unsigned)(((8 * (c >> 2) + (c & 3)) * D + 8 * g) * 2);
+  const unsigned voff = (unsigned)((8 * g + c * bs) * 2);
+  auto bases = [&](int uu, const char*& kb, const char*& vb) {
+    const int tb = 32 * uu;
+    const int blk = bt[__builtin_amdgcn_readfirstlane(tb / bs)];
+    const long base = ((long)blk * Hkv + kvh) * hk;
+    const int o = __builtin_amdgcn_readfirstlane(tb % bs);
+    kb = reinterpret_cast<const char*>(kc + base + (long)o * D);
+    vb = reinterpret_cast<const char*>(vc + base + o);
+  };
+  auto ldk = [&](bf16x8 (&k0)[D / 32], bf16x8 (&k1)[D / 32], const char* kb) {
+#pragma unroll
+    for (int s = 0; s < D / 32; ++s) {
+      k0[s] = *reinterpret_cast<const bf16x8*>(kb + koff + 64 * s);
+      k1[s] = *reinterpret_cast<const bf16x8*>(kb + koff + 8 * D + 64 * s);
+    }
+  };
+  auto ldv = [&](bf16x8 (&v)[D / 16], const char* vb) {
+#pragma unroll
+    for (int dt = 0; dt < D / 16; ++dt)
+      v[dt] = *reinterpret_cast<const bf16x8*>(vb + (long)dt * 32 * bs + voff);
+  };
+  bf16x8 ka0[D / 32], ka1[D / 32], kb0[D / 32], kb1[D / 32], va[D / 16], vb[D / 16];
+  {
+    const char *kbp, *vbp;
+    bases(u, kbp, vbp);
+    ldk(ka0, ka1, kbp);
+    ldv(va, vbp);
+  }
+  // one unit: K(next) -> QK(cur) -> V(next) -> softmax + PV(cur); named sets a/b alternate
+  auto step = [&](bf16x8 (&kc0)[D / 32], bf16x8 (&kc1)[D / 32], bf16x8 (&vcur)[D / 16],
+                  bf16x8 (&kn0)[D / 32], bf16x8 (&kn1)[D / 32], bf16x8 (&vn)[D / 16], int uc) {
+    const char *kbp, *vbp;
+    bases(min(uc + NW, ue - 1), kbp, vbp);
+    f32x4 s0, s1;
+    {
+      bf16x8 qf[D / 32];
+#pragma unroll
+      for (int s = 0; s < D / 32; ++s) qf[s] = qs[s][lane];
+      qk_unit<D>(s0, s1, qf, kc0, kc1);
+    }
+    // next unit's K and V behind the QK MFMAs, into the registers K(cur) just freed (hoisted
+    // above them they would overlap K(cur)'s live range); the co-resident waves of the 3
+    // workgroups per CU hide what one unit of compute does not
+    __builtin_amdgcn_sched_barrier(0);
+    ldk(kn0, kn1, kbp);
+    ldv(vn, vbp);
+    __builtin_amdgcn_sched_barrier(0);
+    softmax_pv<D>(acc, s0, s1, vcur, 32 * uc, L, scale_log2, 0x7fffffff, kv_lo);
+  };
+  for (;;) {
+    step(ka0, ka1, va, kb0, kb1, vb, u);
+    u += NW;
+    if (u >= ue) break;
+    step(kb0, kb1, vb, ka0, ka1, va, u);
+    u += NW;
+    if (u >= ue) break;
+  }
 }
 
 template <int D>
@@ -170,10 +296,11 @@ EIA_DEV void attn_units_pipelined(WaveAcc<D>& acc, const bf16x8 (&qf)[D / 32],
 
 // ---------------------------------------------------------------------------------- decode
 
-// NW waves per workgroup: 4 (default), or 2 (EIA_DECODE_WAVES=2; 4 workgroups per CU
-// resident instead of 2, but each wave walks twice the units -- measured slower).
-template <int D, int NW>
-__global__ void __launch_bounds__(NW * 64, D <= 128 ? 8 / NW : 4 / NW)
+// 4 waves per workgroup.  LEAN: the attn_units_lean pipeline at 3 workgroups per CU (D <= 128);
+// otherwise two full K/V fragment sets at 2 per CU.  (A 2-wave form with 4 per CU measured
+// 1.9-2.2x slower at B = 16..65: each wave walks twice the units.)
+template <int D, bool LEAN>
+__global__ void __launch_bounds__(256, D <= 128 ? (LEAN ? EIA_LEAN_OCC : 2) : 1)
 paged_decode_kernel(const bf16_t* __restrict__ q, long q_stride,
                     const bf16_t* __restrict__ kc, const bf16_t* __restrict__ vc,
                     const int* __restrict__ block_tables, int bt_stride,
@@ -183,6 +310,7 @@ paged_decode_kernel(const bf16_t* __restrict__ q, long q_stride,
                     int* __restrict__ part_cnt,
                     float scale_log2, int Hq, int Hkv, int bs, int Pmax, int NQG,
                     int sliding_window, int chunk_size, const int* __restrict__ p_dyn) {
+  constexpr int NW = 4;
   __shared__ int s_last;
   __shared__ float sm[NW][16];
   __shared__ float sl[NW][16];
@@ -228,7 +356,17 @@ paged_decode_kernel(const bf16_t* __restrict__ q, long q_stride,
   const int U = (L + 31) / 32 - U0;
   const int ub = U0 + (int)(((long)p * U) / P), ue = U0 + (int)(((long)(p + 1) * U) / P);
   const int* bt = block_tables + (long)b * bt_stride;
-  attn_units_pipelined<D>(acc, qf, kc, vc, bt, ub, ue, w, L, kvh, Hkv, bs, scale_log2, kv_lo, NW);
+  if constexpr (LEAN) {
+    // Q fragments through LDS (one copy, re-read per unit): 16 fewer live VGPRs outside QK
+    __shared__ bf16x8 qs[D / 32][64];
+    if (w == 0) {
+#pragma unroll
+      for (int s = 0; s < D / 32; ++s) qs[s][lane] = qf[s];
+    }
+    __syncthreads();
+    attn_units_lean<D>(acc, qs, kc, vc, bt, ub, ue, w, L, kvh, Hkv, bs, scale_log2, kv_lo, NW);
+  } else
+    attn_units_pipelined<D>(acc, qf, kc, vc, bt, ub, ue, w, L, kvh, Hkv, bs, scale_log2, kv_lo, NW);
 
   float lt = acc.l;
   lt += __shfl_xor(lt, 16, 64);
@@ -414,21 +552,20 @@ EIA_API int eia_paged_decode(const void* q, long q_stride, const void* k_cache, 
   const int G = Hq / Hkv;
   const int NQG = (G + 15) / 16;
   const float sl2 = scale * 1.4426950408889634f;
-  static const int nw_env = [] {
-    const char* e = getenv("EIA_DECODE_WAVES");
-    return e != nullptr ? atoi(e) : 0;
+  static const int lean_env = [] {
+    const char* e = getenv("EIA_DECODE_LEAN");
+    return e != nullptr ? atoi(e) : -1;
   }();
-  // 4 waves by default: the 2-wave form measured 1.9-2.2x slower at B = 16..65, ctx 192..1024
-  // (scripts/bench_attn.py, EIA_DECODE_WAVES=2), even where the 4-wave grid overflows one round
-  const int nw = nw_env == 2 ? 2 : 4;
+  // lean form: whole 32-token units inside a block (bs % 32 == 0), uniform per-unit bases
+  const bool lean = (lean_env >= 0 ? lean_env != 0 : true) && bs % 32 == 0 && D <= 128;
   dim3 grid(B, Hkv * NQG, P);
-#define DEC_NW(DD, NW_)                                                                      \
-  hipLaunchKernelGGL((paged_decode_kernel<DD, NW_>), grid, dim3(64 * NW_), 0, st, (const bf16_t*)q, \
+#define DEC_V(DD, LEAN_)                                                                     \
+  hipLaunchKernelGGL((paged_decode_kernel<DD, LEAN_>), grid, dim3(256), 0, st, (const bf16_t*)q, \
                      q_stride, (const bf16_t*)k_cache, (const bf16_t*)v_cache, block_tables,      \
                      bt_stride, seq_lens, (bf16_t*)out, out_stride, part_o, part_ml, part_cnt, sl2, \
                      Hq, Hkv, bs, P, NQG, sliding_window, chunk_size, p_dyn);
 #define DEC(DD)                                                                             \
-  if (nw == 2) { DEC_NW(DD, 2) } else { DEC_NW(DD, 4) }                                    \
+  if (lean) { DEC_V(DD, true) } else { DEC_V(DD, false) }                                  \
   if (P > 1 && part_cnt == nullptr)                                                         \
     hipLaunchKernelGGL((paged_decode_reduce_kernel<DD>), dim3(B, Hq), dim3(DD < 256 ? DD : 256), 0, st, \
                        part_o, part_ml, (bf16_t*)out, out_stride, Hq, P, p_dyn);
@@ -439,7 +576,7 @@ EIA_API int eia_paged_decode(const void* q, long q_stride, const void* k_cache, 
     default: return EIA_UNSUPPORTED;
   }
 #undef DEC
-#undef DEC_NW
+#undef DEC_V
   EIA_LAUNCH_CHECK();
 }
 
