@@ -10,14 +10,17 @@
 // the reduction (rounded to bf16 exactly like the GEMM epilogue) is fused here, so the decode
 // QKV projection needs no separate reduce kernel.
 //
-// Mapping: one workgroup per token; each head is handled by TPH = D/16 lanes,
-// each lane owning 8 rotation pairs (two 16-B vectors), so q/k/v are read with
-// 16-B loads and written with 16-B stores (V: 2-B scattered stores into V^T,
-// merged by L2 since consecutive tokens of a block share lines).
+// Mapping: grid (token, head group): a 64-lane workgroup covers 64/TPH heads of one token
+// (TPH = D/16 lanes per head, each lane owning 8 rotation pairs = two 16-B vectors), so a
+// decode batch spreads over T * (Hq+2Hkv)/(64/TPH) workgroups (65 tokens x 12 = 780 at
+// Llama-8B) instead of T workgroups looping over the heads -- the kernel is latency-bound
+// and this removes the serial passes.  q/k/v are read with 16-B loads and written with
+// 16-B stores (V: 2-B scattered stores into V^T, merged by L2 since consecutive tokens of a
+// block share lines).
 #include "eia_common.h"
 
 template <int D, bool NEOX, bool QK_NORM, bool HAS_BIAS, bool SPLIT>
-__global__ void __launch_bounds__(256)
+__global__ void __launch_bounds__(64)
 rope_qkv_cache_kernel(const bf16_t* __restrict__ qkv, long qkv_stride,
                       const float* __restrict__ part, int sk, long slab,
                       const int* __restrict__ positions, const float* __restrict__ cos_sin,
@@ -48,8 +51,8 @@ rope_qkv_cache_kernel(const bf16_t* __restrict__ qkv, long qkv_stride,
     for (int j = 0; j < 8; ++j) { c[j] = cs[f0 + j]; s[j] = cs[D / 2 + f0 + j]; }
   }
 
-  for (int h0 = 0; h0 < ntot; h0 += hpb) {
-    const int h = h0 + hslot;
+  {
+    const int h = blockIdx.y * hpb + hslot;
     const bool active = h < ntot;
     // element offsets of the two 8-element halves this lane owns
     int e0, e1;
@@ -109,7 +112,7 @@ rope_qkv_cache_kernel(const bf16_t* __restrict__ qkv, long qkv_stride,
         }
       }
     }
-    if (!active) continue;
+    if (!active) return;
     if (h < nrot && cos_sin) {
       if (NEOX) {
 #pragma unroll
@@ -175,7 +178,8 @@ EIA_API int eia_rope_qkv_cache(const void* qkv, long qkv_stride, const float* pa
   if (T == 0) return EIA_OK;
   if ((q_norm_w == nullptr) != (k_norm_w == nullptr)) return EIA_BAD_SHAPE;
   if (part != nullptr && sk < 1) return EIA_BAD_SHAPE;
-  dim3 grid(T), block(256);
+  dim3 block(64);
+  dim3 grid(T, (Hq + 2 * Hkv + 64 / (D / 16) - 1) / (64 / (D / 16)));
   const long slab = (long)T * (Hq + 2 * Hkv) * D;
 #define ROPE_LAUNCH(DD, NX, QN, HB)                                                             \
   do {                                                                                         \
