@@ -471,8 +471,29 @@ paged_decode_reduce_kernel(const float* __restrict__ part_o, const float* __rest
 
 // ---------------------------------------------------------------------------------- prefill
 
-// work[2*i] = sequence index, work[2*i+1] = first query (multiple of 16*(4/HPW)).
-template <int D>
+// work[2*i] = sequence index, work[2*i+1] = first query (multiple of 16*QT*(4/HPW)).
+//
+// A wave owns QT consecutive 16-query tiles of one head and walks the KV range once: every
+// 32-token K/V unit is loaded ONCE into registers and multiplied against all QT tiles (QT x
+// the MFMA work per byte of the one-tile form, which re-streamed the whole context from L2 for
+// every 16 queries and ran at ~134 TFLOP/s on 8k prompts, profiles/rocprof_r1_prefill_long.md).
+// The unit loop is double-buffered (unit u+1's K/V loads are in flight while unit u is
+// multiplied).  Causal: a tile skips the units entirely above its diagonal (wave-uniform test),
+// so the per-tile work is exactly the one-tile kernel's.
+template <int D, int QT>
+EIA_DEV void prefill_compute(WaveAcc<D> (&acc)[QT], const bf16x8 (&qf)[QT][D / 32],
+                             const KVFrag<D>& f, int tb, int L, float sl2, const int (&q_abs)[QT],
+                             const int (&kv_lo)[QT], const int (&t_hi)[QT]) {
+#pragma unroll
+  for (int t = 0; t < QT; ++t) {
+    if (tb >= t_hi[t]) continue;   // wave-uniform: unit wholly after this tile's last query
+    f32x4 s0, s1;
+    qk_unit<D>(s0, s1, qf[t], f.k0, f.k1);
+    softmax_pv<D>(acc[t], s0, s1, f.v, tb, L, sl2, q_abs[t], kv_lo[t]);
+  }
+}
+
+template <int D, int QT>
 __global__ void __launch_bounds__(256)
 paged_prefill_kernel(const bf16_t* __restrict__ q, long q_stride,
                      bf16_t* __restrict__ out, long out_stride,
@@ -485,7 +506,7 @@ paged_prefill_kernel(const bf16_t* __restrict__ q, long q_stride,
   const int c = lane & 15, g = lane >> 4;
   const int hw = w % HPW, qsub = w / HPW;
   const int s = work[2 * blockIdx.x];
-  const int qstart = work[2 * blockIdx.x + 1] + 16 * qsub;
+  const int qstart = work[2 * blockIdx.x + 1] + 16 * QT * qsub;
   const int hq = blockIdx.y * HPW + hw;
   const int G = Hq / Hkv;
   const int kvh = hq / G;
@@ -494,47 +515,69 @@ paged_prefill_kernel(const bf16_t* __restrict__ q, long q_stride,
   if (qstart >= qlen) return;              // wave-uniform; kernel has no barriers
   const int L = seq_lens[s];
   const int ctx = L - qlen;
-  const int qi = qstart + c;
-  const bool cval = qi < qlen;
-  const long tokrow = q0 + (cval ? qi : qstart);
 
-  bf16x8 qf[D / 32];
-  {
-    const bf16_t* qp = q + tokrow * q_stride + (long)hq * D + 8 * g;
+  bf16x8 qf[QT][D / 32];
+  int q_abs[QT], kv_lo[QT], t_hi[QT];
+  long tokrow[QT];
+  bool cval[QT];
 #pragma unroll
-    for (int ss = 0; ss < D / 32; ++ss) qf[ss] = *reinterpret_cast<const bf16x8*>(qp + 32 * ss);
+  for (int t = 0; t < QT; ++t) {
+    const int qb = qstart + 16 * t;         // first query of tile t (may be >= qlen)
+    const int qi = qb + c;
+    cval[t] = qi < qlen;
+    const int qe = min(qi, qlen - 1);       // invalid columns mirror a valid row
+    tokrow[t] = q0 + qe;
+    const bf16_t* qp = q + tokrow[t] * q_stride + (long)hq * D + 8 * g;
+#pragma unroll
+    for (int ss = 0; ss < D / 32; ++ss) qf[t][ss] = *reinterpret_cast<const bf16x8*>(qp + 32 * ss);
+    const int qa = ctx + qe;
+    q_abs[t] = causal ? qa : 0x7fffffff;
+    int lo = 0;
+    if (sliding_window > 0) lo = max(lo, qa - sliding_window + 1);
+    if (chunk_size > 0) lo = max(lo, (qa / chunk_size) * chunk_size);
+    kv_lo[t] = lo;
+    // units starting at or past t_hi hold no token any column of tile t may see
+    t_hi[t] = (causal && qb < qlen) ? min(L, ctx + min(qb + 16, qlen)) : (qb < qlen ? L : 0);
   }
-  const int qa = ctx + (cval ? qi : qstart);
-  const int q_abs = causal ? qa : 0x7fffffff;
-  int kv_lo = 0;
-  if (sliding_window > 0) kv_lo = max(kv_lo, qa - sliding_window + 1);
-  if (chunk_size > 0) kv_lo = max(kv_lo, (qa / chunk_size) * chunk_size);
   // wave-wide token range
   const int qa_first = ctx + qstart;
   int lo_w = 0;
   if (sliding_window > 0) lo_w = max(lo_w, qa_first - sliding_window + 1);
   if (chunk_size > 0) lo_w = max(lo_w, (qa_first / chunk_size) * chunk_size);
   lo_w &= ~31;
-  const int hi_w = causal ? min(L, ctx + min(qstart + 16, qlen)) : L;
+  const int hi_w = causal ? min(L, ctx + min(qstart + 16 * QT, qlen)) : L;
 
-  WaveAcc<D> acc;
-  wave_acc_init(acc);
+  WaveAcc<D> acc[QT];
+#pragma unroll
+  for (int t = 0; t < QT; ++t) wave_acc_init(acc[t]);
   const int* bt = block_tables + (long)s * bt_stride;
-  for (int tb = lo_w; tb < hi_w; tb += 32)
-    attn_unit<D>(acc, qf, kc, vc, bt, tb, L, kvh, Hkv, bs, scale_log2, q_abs, kv_lo);
+  KVFrag<D> fa, fb;
+  int tb = lo_w;
+  if (tb < hi_w) load_unit<D>(fa, kc, vc, bt, tb, L, kvh, Hkv, bs);
+  for (; tb < hi_w; tb += 64) {
+    const bool more = tb + 32 < hi_w;
+    if (more) load_unit<D>(fb, kc, vc, bt, tb + 32, L, kvh, Hkv, bs);
+    prefill_compute<D, QT>(acc, qf, fa, tb, L, scale_log2, q_abs, kv_lo, t_hi);
+    if (!more) break;
+    if (tb + 64 < hi_w) load_unit<D>(fa, kc, vc, bt, tb + 64, L, kvh, Hkv, bs);
+    prefill_compute<D, QT>(acc, qf, fb, tb + 32, L, scale_log2, q_abs, kv_lo, t_hi);
+  }
 
-  float lt = acc.l;
-  lt += __shfl_xor(lt, 16, 64);
-  lt += __shfl_xor(lt, 32, 64);
-  if (!cval) return;
-  const float inv = lt > 0.f ? 1.f / lt : 0.f;
-  bf16_t* op = out + tokrow * out_stride + (long)hq * D + 4 * g;
 #pragma unroll
-  for (int dt = 0; dt < D / 16; ++dt) {
-    bf16x4 o4;
+  for (int t = 0; t < QT; ++t) {
+    float lt = acc[t].l;
+    lt += __shfl_xor(lt, 16, 64);
+    lt += __shfl_xor(lt, 32, 64);
+    if (!cval[t]) continue;
+    const float inv = lt > 0.f ? 1.f / lt : 0.f;
+    bf16_t* op = out + tokrow[t] * out_stride + (long)hq * D + 4 * g;
 #pragma unroll
-    for (int i = 0; i < 4; ++i) o4[i] = f2bf(acc.o[dt][i] * inv);
-    *reinterpret_cast<bf16x4*>(op + 16 * dt) = o4;
+    for (int dt = 0; dt < D / 16; ++dt) {
+      bf16x4 o4;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) o4[i] = f2bf(acc[t].o[dt][i] * inv);
+      *reinterpret_cast<bf16x4*>(op + 16 * dt) = o4;
+    }
   }
 }
 
@@ -584,23 +627,29 @@ EIA_API int eia_paged_prefill(const void* q, long q_stride, void* out, long out_
                               const void* k_cache, const void* v_cache, const int* block_tables,
                               int bt_stride, const int* seq_lens, const int* cu_q, const int* work,
                               int n_work, float scale, int Hq, int Hkv, int D, int bs, int HPW,
-                              int causal, int sliding_window, int chunk_size, hipStream_t st) {
+                              int causal, int sliding_window, int chunk_size, int qt,
+                              hipStream_t st) {
   if (Hkv <= 0 || Hq % Hkv != 0 || bs % 16 != 0) return EIA_BAD_SHAPE;
+  if (!(qt >= 1 && qt <= 4)) return EIA_BAD_SHAPE;
   if (!(HPW == 1 || HPW == 2 || HPW == 4) || (Hq / Hkv) % HPW != 0) return EIA_BAD_SHAPE;
   if (n_work == 0) return EIA_OK;
   const float sl2 = scale * 1.4426950408889634f;
   dim3 grid(n_work, Hq / HPW), block(256);
-#define PRE(DD)                                                                              \
-  hipLaunchKernelGGL((paged_prefill_kernel<DD>), grid, block, 0, st, (const bf16_t*)q, q_stride, \
-                     (bf16_t*)out, out_stride, (const bf16_t*)k_cache, (const bf16_t*)v_cache, \
-                     block_tables, bt_stride, seq_lens, cu_q, work, sl2, Hq, Hkv, bs, HPW, causal, \
-                     sliding_window, chunk_size);
+#define PRE(DD, QQ)                                                                          \
+  hipLaunchKernelGGL((paged_prefill_kernel<DD, QQ>), grid, block, 0, st, (const bf16_t*)q,     \
+                     q_stride, (bf16_t*)out, out_stride, (const bf16_t*)k_cache,               \
+                     (const bf16_t*)v_cache, block_tables, bt_stride, seq_lens, cu_q, work, sl2, \
+                     Hq, Hkv, bs, HPW, causal, sliding_window, chunk_size);
+#define PRE_Q(DD)                                                                            \
+  if (qt == 4) { PRE(DD, 4) } else if (qt == 3) { PRE(DD, 3) } else if (qt == 2) { PRE(DD, 2) } \
+  else { PRE(DD, 1) }
   switch (D) {
-    case 64: PRE(64) break;
-    case 128: PRE(128) break;
-    case 256: PRE(256) break;
+    case 64: PRE_Q(64) break;
+    case 128: PRE_Q(128) break;
+    case 256: if (qt != 1) return EIA_UNSUPPORTED; PRE(256, 1) break;   // register budget
     default: return EIA_UNSUPPORTED;
   }
+#undef PRE_Q
 #undef PRE
   EIA_LAUNCH_CHECK();
 }

@@ -23,16 +23,32 @@ def heads_per_workgroup(num_heads: int, num_kv_heads: int) -> int:
     return 4 if g % 4 == 0 else 2 if g % 2 == 0 else 1
 
 
-def prefill_query_block(num_heads: int, num_kv_heads: int) -> int:
-    """Queries covered by one prefill workgroup (4 waves x 16 columns / heads-per-WG)."""
-    return 16 * (4 // heads_per_workgroup(num_heads, num_kv_heads))
+# 16-query tiles per prefill wave (csrc/kernels/attention.hip paged_prefill_kernel): every K/V
+# unit a wave loads feeds QT tiles.
+# The wave keeps QT tiles of O accumulators and Q fragments plus two K/V unit buffers in
+# registers; QT = 4 at D = 128 spills (hipcc kernel-resource-usage).  Measured on MI355X
+# (scripts/bench_prefill_attn.py, profiles/prefill_attn_r1.log): D = 128 causal 1x8192
+# qt 1/2/3 = 3831/2076/1792 us; D = 64 (BERT, 12 heads, 32x512) qt 1/2/3/4 = 131/85/119/109 us.
+def prefill_tiles(head_dim: int) -> int:
+    return 2 if head_dim <= 64 else 3 if head_dim <= 128 else 1
+
+
+def prefill_query_block(num_heads: int, num_kv_heads: int, head_dim: int = 128,
+                        qt: Optional[int] = None) -> int:
+    """Queries covered by one prefill workgroup (4 waves x QT x 16 columns / heads-per-WG)."""
+    qt = qt or prefill_tiles(head_dim)
+    return 16 * qt * (4 // heads_per_workgroup(num_heads, num_kv_heads))
 
 
 def build_prefill_work(q_lens: Sequence[int], qblock: int) -> List[int]:
+    """[seq, first query] pairs, latest query blocks first: under the causal mask a block's
+    work grows with its position, so dispatching the long ones first balances the CUs' tails
+    (longest-processing-time order)."""
+    items = [(q0, s) for s, n in enumerate(q_lens) for q0 in range(0, n, qblock)]
+    items.sort(key=lambda it: -it[0])
     work: List[int] = []
-    for s, n in enumerate(q_lens):
-        for q0 in range(0, n, qblock):
-            work += [s, q0]
+    for q0, s in items:
+        work += [s, q0]
     return work
 
 
@@ -138,8 +154,9 @@ def paged_prefill(q: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tensor,
                   block_tables: torch.Tensor, seq_lens: torch.Tensor, cu_q: torch.Tensor,
                   work: Optional[torch.Tensor], n_work: int, scale: float, causal: bool = True,
                   sliding_window: Optional[int] = None, chunk_size: Optional[int] = None,
-                  out: Optional[torch.Tensor] = None) -> torch.Tensor:
-    """q [T, Hq, D] (varlen, cu_q) -> out [T, Hq, D]."""
+                  out: Optional[torch.Tensor] = None, qt: Optional[int] = None) -> torch.Tensor:
+    """q [T, Hq, D] (varlen, cu_q) -> out [T, Hq, D].  `work` must be built with
+    prefill_query_block(Hq, Hkv, D, qt) (qt = tiles per wave, default prefill_tiles(D))."""
     if not (use_hip(q, k_cache) and q.dtype == torch.bfloat16):
         r = ref.paged_attention_prefill(q, k_cache, v_cache, block_tables, cu_q, seq_lens, scale,
                                         causal, sliding_window, chunk_size)
@@ -158,7 +175,8 @@ def paged_prefill(q: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tensor,
     check(lib().eia_paged_prefill(
         ptr(q), q.stride(0), ptr(o), o.stride(0), ptr(k_cache), ptr(v_cache), ptr(block_tables),
         block_tables.stride(0), ptr(seq_lens), ptr(cu_q), ptr(work), n_work, float(scale), Hq, Hkv,
-        D, bs, hpw, 1 if causal else 0, sliding_window or 0, chunk_size or 0, stream(q)),
+        D, bs, hpw, 1 if causal else 0, sliding_window or 0, chunk_size or 0, qt or prefill_tiles(D),
+        stream(q)),
         "paged_prefill")
     return o
 

@@ -46,6 +46,9 @@ for s in $STEPS; do
       done ;;
     packed) run packed 900 python scripts/bench_gemm.py --packed --sweep --m ${GEMM_M:-65} \
             --shapes ${GEMM_SHAPES:-qkv_8b o_8b gate_up_8b down_8b lm_head_8b} ;;
+    sizing) run sizing_8b 1500 python scripts/sizing_sweep.py --model 8b --out gpurun_out/sizing_8b.md ;;
+    sizing70) run sizing_70b 1100 python scripts/sizing_sweep.py --model 70b --timeout 600 \
+            --cases ${SIZING70_CASES:-chatbot describe translate} --out gpurun_out/sizing_70b_tp1.md ;;
     probe) run probe 300 python scripts/probe_overlap.py ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac

@@ -8,6 +8,7 @@ import glob
 import os
 import shutil
 import subprocess
+import sys
 
 import pytest
 import yaml
@@ -147,3 +148,38 @@ def test_ibm_pattern_files():
                 if "=" in l}
     tpl_keys = {l.split("=")[0] for l in open(os.path.join(d, "inference-config.tpl")) if "=" in l}
     assert tpl_keys <= cfg_keys, tpl_keys - cfg_keys
+
+
+def test_ibm_standard_pattern_and_catalog():
+    """The standard flavor creates its own network and reuses the quickstart templates; the
+    catalog manifest lists every Terraform input of both flavors (generated, never stale)."""
+    import re
+    base = os.path.join(os.path.dirname(ROOT), "third_party/IBM/patterns")
+    main = open(os.path.join(base, "standard/main.tf")).read()
+    for res in ("ibm_is_vpc", "ibm_is_security_group", "ibm_is_public_gateway", "ibm_is_subnet"):
+        assert f'resource "{res}"' in main, res
+    assert "data \"ibm_is_vpc\"" not in main
+    for ref in re.findall(r'\$\{path\.module\}/([\w./-]+)', main):
+        assert os.path.exists(os.path.join(base, "standard", ref)), ref
+    # every var.X used by the pattern is declared
+    decl = set(re.findall(r'variable "(\w+)"', open(os.path.join(base, "standard/variables.tf")).read()))
+    used = set(re.findall(r"\bvar\.(\w+)", main))
+    assert used <= decl, used - decl
+    r = subprocess.run([sys.executable, os.path.join(os.path.dirname(ROOT), "scripts/gen_ibm_catalog.py"),
+                        "--check"], capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr
+
+
+def test_multi_node_example():
+    d = os.path.join(os.path.dirname(ROOT), "docs/examples/multi-node")
+    inv = yaml.safe_load(open(os.path.join(d, "hosts.yaml")))
+    ch = inv["all"]["children"]
+    cps = set(ch["kube_control_plane"]["hosts"])
+    assert len(cps) == 3 and set(ch["etcd"]["hosts"]) == cps
+    workers = set(ch["kube_node"]["hosts"])
+    assert workers and not (workers & cps)
+    assert all(inv["all"]["hosts"][w].get("devices") for w in workers)
+    cfg_keys = {l.split("=")[0] for l in open(os.path.join(ROOT, "inventory/inference-config.cfg"))
+                if "=" in l}
+    ex_keys = {l.split("=")[0] for l in open(os.path.join(d, "inference-config.cfg")) if "=" in l}
+    assert ex_keys == cfg_keys

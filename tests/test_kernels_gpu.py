@@ -193,12 +193,15 @@ def test_paged_prefill(Hq, Hkv, D, bs, causal):
     cu = torch.tensor([0] + list(torch.tensor(qlens).cumsum(0)), dtype=torch.int32, device=DEV)
     T = sum(qlens)
     q = torch.randn(T, Hq, D, device=DEV, dtype=BF)
-    qb = attention.prefill_query_block(Hq, Hkv)
-    work = torch.tensor(attention.build_prefill_work(qlens, qb), dtype=torch.int32, device=DEV)
-    o = attention.paged_prefill(q, k, v, bt, sl, cu, work, work.numel() // 2, D ** -0.5, causal)
     r = ref.paged_attention_prefill(q.cpu().float(), k.cpu().float(), v.cpu().float(), bt.cpu(),
                                     cu.cpu(), sl.cpu(), D ** -0.5, causal)
-    _close(o, r, 2e-2, 2e-2, "prefill")
+    # every tiles-per-wave variant the register budget allows at this head size
+    for qt in sorted({1, attention.prefill_tiles(D)} | ({2, 3, 4} if D <= 128 else set())):
+        qb = attention.prefill_query_block(Hq, Hkv, D, qt)
+        work = torch.tensor(attention.build_prefill_work(qlens, qb), dtype=torch.int32, device=DEV)
+        o = attention.paged_prefill(q, k, v, bt, sl, cu, work, work.numel() // 2, D ** -0.5,
+                                    causal, qt=qt)
+        _close(o, r, 2e-2, 2e-2, f"prefill qt={qt}")
 
 
 def test_paged_prefill_sliding_and_chunk():
@@ -212,7 +215,7 @@ def test_paged_prefill_sliding_and_chunk():
     sl = torch.tensor(lens, dtype=torch.int32, device=DEV)
     cu = torch.tensor([0, 90, 123], dtype=torch.int32, device=DEV)
     q = torch.randn(123, Hq, D, device=DEV, dtype=BF)
-    work = torch.tensor(attention.build_prefill_work(qlens, attention.prefill_query_block(Hq, Hkv)),
+    work = torch.tensor(attention.build_prefill_work(qlens, attention.prefill_query_block(Hq, Hkv, D)),
                         dtype=torch.int32, device=DEV)
     for sw, ch in ((50, None), (None, 64)):
         o = attention.paged_prefill(q, k, v, bt, sl, cu, work, work.numel() // 2, D ** -0.5, True,
