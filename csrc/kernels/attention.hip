@@ -581,6 +581,167 @@ paged_prefill_kernel(const bf16_t* __restrict__ q, long q_stride,
   }
 }
 
+// LDS-shared form (HPW == 4, block size a multiple of 32): the workgroup's four waves are the
+// four query heads of one KV group over the SAME query range, so they need the same K/V unit
+// at the same time.  Each 32-token unit is fetched from L2/HBM once per workgroup (every
+// thread one quarter: 4 x 16 B) into a double-buffered, row-padded LDS copy and every wave
+// reads its MFMA fragments from there -- a quarter of the fabric traffic of the register-
+// streamed form, whose per-CU K/V stream was the limit.  Unit u+1's global loads are issued
+// before unit u is multiplied and land in LDS after it; one barrier per unit orders both the
+// LDS writes before their reads and the reads of a buffer before its next overwrite.  The
+// unit loop bounds depend only on blockIdx, so every wave reaches every barrier.
+template <int D>
+struct PrefillLds {
+  static constexpr int KS = D + 8;                  // K row stride (elements): +16 B per token
+  static constexpr int VS = 32 + 8;                 // V^T row stride: 32 tokens + 16 B
+  static constexpr int KE = 32 * KS, VE = D * VS;   // elements per buffer
+  static constexpr int NCH = (32 * D / 8) / 256;    // 16-B K (and V) chunks per thread per unit
+};
+
+template <int D>
+EIA_DEV void prefill_lds_fetch(bf16x8 (&st)[2 * PrefillLds<D>::NCH], const bf16_t* __restrict__ kc,
+                               const bf16_t* __restrict__ vc, const int* __restrict__ bt, int tb,
+                               int kvh, int Hkv, int bs) {
+  const int tid = threadIdx.x;
+  const int blk = bt[tb / bs];
+  const long base = ((long)blk * Hkv + kvh) * ((long)bs * D);
+  const int o = tb % bs;
+  const bf16_t* kp = kc + base + (long)o * D;       // 32 x D contiguous
+  const bf16_t* vp = vc + base + o;                 // D rows of 32 tokens, row stride bs
+#pragma unroll
+  for (int i = 0; i < PrefillLds<D>::NCH; ++i) {
+    const int id = tid + 256 * i;
+    st[i] = *reinterpret_cast<const bf16x8*>(kp + 8 * id);
+    st[PrefillLds<D>::NCH + i] = *reinterpret_cast<const bf16x8*>(vp + (long)(id >> 2) * bs + 8 * (id & 3));
+  }
+}
+
+template <int D>
+EIA_DEV void prefill_lds_store(bf16_t* __restrict__ kl, bf16_t* __restrict__ vl,
+                               const bf16x8 (&st)[2 * PrefillLds<D>::NCH]) {
+  const int tid = threadIdx.x;
+#pragma unroll
+  for (int i = 0; i < PrefillLds<D>::NCH; ++i) {
+    const int id = tid + 256 * i;
+    const int r = id / (D / 8), c8 = id % (D / 8);
+    *reinterpret_cast<bf16x8*>(kl + r * PrefillLds<D>::KS + 8 * c8) = st[i];
+    *reinterpret_cast<bf16x8*>(vl + (id >> 2) * PrefillLds<D>::VS + 8 * (id & 3)) =
+        st[PrefillLds<D>::NCH + i];
+  }
+}
+
+template <int D, int QT>
+__global__ void __launch_bounds__(256)
+paged_prefill_lds_kernel(const bf16_t* __restrict__ q, long q_stride,
+                         bf16_t* __restrict__ out, long out_stride,
+                         const bf16_t* __restrict__ kc, const bf16_t* __restrict__ vc,
+                         const int* __restrict__ block_tables, int bt_stride,
+                         const int* __restrict__ seq_lens, const int* __restrict__ cu_q,
+                         const int* __restrict__ work, float scale_log2, int Hq, int Hkv, int bs,
+                         int causal, int sliding_window, int chunk_size) {
+  using LL = PrefillLds<D>;
+  __shared__ __attribute__((aligned(16))) bf16_t lds[2 * (LL::KE + LL::VE)];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int c = lane & 15, g = lane >> 4;
+  const int s = work[2 * blockIdx.x];
+  const int qstart = work[2 * blockIdx.x + 1];      // same for all four waves (HPW == 4)
+  const int hq = blockIdx.y * 4 + w;
+  const int kvh = hq / (Hq / Hkv);
+  const int q0 = cu_q[s];
+  const int qlen = cu_q[s + 1] - q0;
+  if (qstart >= qlen) return;                      // workgroup-uniform
+  const int L = seq_lens[s];
+  const int ctx = L - qlen;
+
+  bf16x8 qf[QT][D / 32];
+  int q_abs[QT], kv_lo[QT], t_hi[QT];
+  long tokrow[QT];
+  bool cval[QT];
+#pragma unroll
+  for (int t = 0; t < QT; ++t) {
+    const int qb = qstart + 16 * t;
+    const int qi = qb + c;
+    cval[t] = qi < qlen;
+    const int qe = min(qi, qlen - 1);
+    tokrow[t] = q0 + qe;
+    const bf16_t* qp = q + tokrow[t] * q_stride + (long)hq * D + 8 * g;
+#pragma unroll
+    for (int ss = 0; ss < D / 32; ++ss) qf[t][ss] = *reinterpret_cast<const bf16x8*>(qp + 32 * ss);
+    const int qa = ctx + qe;
+    q_abs[t] = causal ? qa : 0x7fffffff;
+    int lo = 0;
+    if (sliding_window > 0) lo = max(lo, qa - sliding_window + 1);
+    if (chunk_size > 0) lo = max(lo, (qa / chunk_size) * chunk_size);
+    kv_lo[t] = lo;
+    t_hi[t] = (causal && qb < qlen) ? min(L, ctx + min(qb + 16, qlen)) : (qb < qlen ? L : 0);
+  }
+  const int qa_first = ctx + qstart;
+  int lo_w = 0;
+  if (sliding_window > 0) lo_w = max(lo_w, qa_first - sliding_window + 1);
+  if (chunk_size > 0) lo_w = max(lo_w, (qa_first / chunk_size) * chunk_size);
+  lo_w &= ~31;
+  const int hi_w = causal ? min(L, ctx + min(qstart + 16 * QT, qlen)) : L;
+
+  WaveAcc<D> acc[QT];
+#pragma unroll
+  for (int t = 0; t < QT; ++t) wave_acc_init(acc[t]);
+  const int* bt = block_tables + (long)s * bt_stride;
+  bf16x8 st[2 * LL::NCH];
+  if (lo_w < hi_w) {
+    prefill_lds_fetch<D>(st, kc, vc, bt, lo_w, kvh, Hkv, bs);
+    prefill_lds_store<D>(lds, lds + 2 * LL::KE, st);
+  }
+  int buf = 0;
+  for (int tb = lo_w; tb < hi_w; tb += 32) {
+    const bool more = tb + 32 < hi_w;
+    if (more) prefill_lds_fetch<D>(st, kc, vc, bt, tb + 32, kvh, Hkv, bs);
+    __syncthreads();
+    const bf16_t* kl = lds + buf * LL::KE;
+    const bf16_t* vl = lds + 2 * LL::KE + buf * LL::VE;
+    {
+      // S^T for every live tile from one K fragment read
+      const int tk0 = 8 * (c >> 2) + (c & 3);
+      bf16x8 k0[D / 32], k1[D / 32];
+#pragma unroll
+      for (int ss = 0; ss < D / 32; ++ss) {
+        k0[ss] = *reinterpret_cast<const bf16x8*>(kl + tk0 * LL::KS + 8 * g + 32 * ss);
+        k1[ss] = *reinterpret_cast<const bf16x8*>(kl + (tk0 + 4) * LL::KS + 8 * g + 32 * ss);
+      }
+      f32x4 s0[QT], s1[QT];
+#pragma unroll
+      for (int t = 0; t < QT; ++t)
+        if (tb < t_hi[t]) qk_unit<D>(s0[t], s1[t], qf[t], k0, k1);
+      bf16x8 vf[D / 16];
+#pragma unroll
+      for (int dt = 0; dt < D / 16; ++dt)
+        vf[dt] = *reinterpret_cast<const bf16x8*>(vl + (16 * dt + c) * LL::VS + 8 * g);
+#pragma unroll
+      for (int t = 0; t < QT; ++t)
+        if (tb < t_hi[t])
+          softmax_pv<D>(acc[t], s0[t], s1[t], vf, tb, L, scale_log2, q_abs[t], kv_lo[t]);
+    }
+    if (more) prefill_lds_store<D>(lds + (buf ^ 1) * LL::KE, lds + 2 * LL::KE + (buf ^ 1) * LL::VE, st);
+    buf ^= 1;
+  }
+
+#pragma unroll
+  for (int t = 0; t < QT; ++t) {
+    float lt = acc[t].l;
+    lt += __shfl_xor(lt, 16, 64);
+    lt += __shfl_xor(lt, 32, 64);
+    if (!cval[t]) continue;
+    const float inv = lt > 0.f ? 1.f / lt : 0.f;
+    bf16_t* op = out + tokrow[t] * out_stride + (long)hq * D + 4 * g;
+#pragma unroll
+    for (int dt = 0; dt < D / 16; ++dt) {
+      bf16x4 o4;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) o4[i] = f2bf(acc[t].o[dt][i] * inv);
+      *reinterpret_cast<bf16x4*>(op + 16 * dt) = o4;
+    }
+  }
+}
+
 // ---------------------------------------------------------------------------------- launchers
 
 EIA_API int eia_paged_decode(const void* q, long q_stride, const void* k_cache, const void* v_cache,
@@ -630,7 +791,11 @@ EIA_API int eia_paged_prefill(const void* q, long q_stride, void* out, long out_
                               int causal, int sliding_window, int chunk_size, int qt,
                               hipStream_t st) {
   if (Hkv <= 0 || Hq % Hkv != 0 || bs % 16 != 0) return EIA_BAD_SHAPE;
+  // qt: tiles per wave; | 16 selects the LDS-shared form (needs HPW 4, 32 | bs, D <= 128)
+  const bool lds_form = (qt & 16) != 0;
+  qt &= 15;
   if (!(qt >= 1 && qt <= 4)) return EIA_BAD_SHAPE;
+  if (lds_form && (HPW != 4 || bs % 32 != 0 || !(D == 64 || D == 128))) return EIA_BAD_SHAPE;
   if (!(HPW == 1 || HPW == 2 || HPW == 4) || (Hq / Hkv) % HPW != 0) return EIA_BAD_SHAPE;
   if (n_work == 0) return EIA_OK;
   const float sl2 = scale * 1.4426950408889634f;
@@ -643,6 +808,20 @@ EIA_API int eia_paged_prefill(const void* q, long q_stride, void* out, long out_
 #define PRE_Q(DD)                                                                            \
   if (qt == 4) { PRE(DD, 4) } else if (qt == 3) { PRE(DD, 3) } else if (qt == 2) { PRE(DD, 2) } \
   else { PRE(DD, 1) }
+#define PRE_L(DD, QQ)                                                                        \
+  hipLaunchKernelGGL((paged_prefill_lds_kernel<DD, QQ>), grid, block, 0, st, (const bf16_t*)q, \
+                     q_stride, (bf16_t*)out, out_stride, (const bf16_t*)k_cache,               \
+                     (const bf16_t*)v_cache, block_tables, bt_stride, seq_lens, cu_q, work, sl2, \
+                     Hq, Hkv, bs, causal, sliding_window, chunk_size);
+  if (lds_form) {
+    if (D == 128) {
+      if (qt == 4) { PRE_L(128, 4) } else if (qt == 3) { PRE_L(128, 3) } else if (qt == 2) { PRE_L(128, 2) } else { PRE_L(128, 1) }
+    } else {
+      if (qt == 4) { PRE_L(64, 4) } else if (qt == 3) { PRE_L(64, 3) } else if (qt == 2) { PRE_L(64, 2) } else { PRE_L(64, 1) }
+    }
+    EIA_LAUNCH_CHECK();
+  }
+#undef PRE_L
   switch (D) {
     case 64: PRE_Q(64) break;
     case 128: PRE_Q(128) break;

@@ -119,7 +119,8 @@ class ModelRunner:
     # ------------------------------------------------------------------ buffers
     def _alloc_staging(self) -> None:
         T, S, mb = self.max_tokens, self.max_num_seqs, self.maxb
-        qb = attn_ops.prefill_query_block(self.num_heads, self.num_kv_heads, self.head_dim)
+        qb = attn_ops.prefill_query_block(self.num_heads, self.num_kv_heads, self.head_dim,
+                                          block_size=self.block_size)
         self.max_work = T // qb + S + 1
         pin = self.is_gpu
         # graph (decode) header, fixed offsets:
@@ -236,7 +237,8 @@ class ModelRunner:
         cu = torch.tensor([0] + list(np.cumsum(qls)), dtype=torch.int32, device=self.device)
         lens = torch.tensor(qls, dtype=torch.int32, device=self.device)
         bt = torch.zeros(nseq, max(1, self.maxb), dtype=torch.int32, device=self.device)
-        qb = attn_ops.prefill_query_block(self.num_heads, self.num_kv_heads, self.head_dim)
+        qb = attn_ops.prefill_query_block(self.num_heads, self.num_kv_heads, self.head_dim,
+                                          block_size=self.block_size)
         work = attn_ops.build_prefill_work(qls, qb)
         md = attn_ops.AttentionMetadata(
             num_decode=0, num_prefill_tokens=n, slot_mapping=slots, positions=pos,
@@ -369,7 +371,8 @@ class ModelRunner:
                             base + 4 * o["plen"], T - nd)
             buf[o["cu"]] = 0
             buf[o["cu"] + 1:o["cu"] + 1 + npf] = np.cumsum(qlens)
-        qb = attn_ops.prefill_query_block(self.num_heads, self.num_kv_heads, self.head_dim)
+        qb = attn_ops.prefill_query_block(self.num_heads, self.num_kv_heads, self.head_dim,
+                                          block_size=self.block_size)
         work = attn_ops.build_prefill_work(qlens, qb)
         take("work", len(work))
         if work:

@@ -86,7 +86,7 @@ class BertLayer(nn.Module):
             kc = torch.empty(b.num_blocks, nh, _ENC_BLOCK, hd, dtype=qkv.dtype, device=qkv.device)
             vc = torch.zeros(b.num_blocks, nh, hd, _ENC_BLOCK, dtype=qkv.dtype, device=qkv.device)
             q = rope_qkv_cache(qkv, None, None, b.slots, kc, vc, nh, nh, hd)
-            qb = attn_ops.prefill_query_block(nh, nh, hd)
+            qb = attn_ops.prefill_query_block(nh, nh, hd, block_size=_ENC_BLOCK)
             work = attn_ops.build_prefill_work(b.lens, qb)
             wt = torch.tensor(work, dtype=torch.int32, device=qkv.device)
             o = attn_ops.paged_prefill(q, kc, vc, b.block_tables, b.seq_lens, b.cu_t, wt,

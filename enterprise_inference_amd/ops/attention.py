@@ -33,11 +33,28 @@ def prefill_tiles(head_dim: int) -> int:
     return 2 if head_dim <= 64 else 3 if head_dim <= 128 else 1
 
 
+PREFILL_LDS = 16          # kernel variant flag: K/V units shared by the workgroup through LDS
+# LDS form, D = 128 causal (profiles/prefill_attn_lds_r1.log): qt 1/2/3/4 = 1296/1905/1865/2186 us
+# at 1x8192 (register form qt 3: 1867 us).  qt 1 needs 185 registers -> 2 waves/SIMD, and with
+# the K/V traffic already cut 4x by LDS sharing, occupancy is what pays.
+PREFILL_LDS_QT = {64: 1, 128: 1}
+
+
+def prefill_variant(num_heads: int, num_kv_heads: int, head_dim: int,
+                    block_size: Optional[int] = None) -> int:
+    """Kernel variant code: tiles per wave, | PREFILL_LDS for the LDS-shared form (the four
+    waves of a workgroup are four query heads of one KV group; needs 32 | block size)."""
+    if (heads_per_workgroup(num_heads, num_kv_heads) == 4 and block_size is not None
+            and block_size % 32 == 0 and head_dim in PREFILL_LDS_QT):
+        return PREFILL_LDS | PREFILL_LDS_QT[head_dim]
+    return prefill_tiles(head_dim)
+
+
 def prefill_query_block(num_heads: int, num_kv_heads: int, head_dim: int = 128,
-                        qt: Optional[int] = None) -> int:
+                        qt: Optional[int] = None, block_size: Optional[int] = None) -> int:
     """Queries covered by one prefill workgroup (4 waves x QT x 16 columns / heads-per-WG)."""
-    qt = qt or prefill_tiles(head_dim)
-    return 16 * qt * (4 // heads_per_workgroup(num_heads, num_kv_heads))
+    code = qt or prefill_variant(num_heads, num_kv_heads, head_dim, block_size)
+    return 16 * (code & 15) * (4 // heads_per_workgroup(num_heads, num_kv_heads))
 
 
 def build_prefill_work(q_lens: Sequence[int], qblock: int) -> List[int]:
@@ -156,7 +173,8 @@ def paged_prefill(q: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tensor,
                   sliding_window: Optional[int] = None, chunk_size: Optional[int] = None,
                   out: Optional[torch.Tensor] = None, qt: Optional[int] = None) -> torch.Tensor:
     """q [T, Hq, D] (varlen, cu_q) -> out [T, Hq, D].  `work` must be built with
-    prefill_query_block(Hq, Hkv, D, qt) (qt = tiles per wave, default prefill_tiles(D))."""
+    prefill_query_block(Hq, Hkv, D, qt, block_size) (qt = variant code, default
+    prefill_variant(Hq, Hkv, D, block_size))."""
     if not (use_hip(q, k_cache) and q.dtype == torch.bfloat16):
         r = ref.paged_attention_prefill(q, k_cache, v_cache, block_tables, cu_q, seq_lens, scale,
                                         causal, sliding_window, chunk_size)
@@ -175,7 +193,7 @@ def paged_prefill(q: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tensor,
     check(lib().eia_paged_prefill(
         ptr(q), q.stride(0), ptr(o), o.stride(0), ptr(k_cache), ptr(v_cache), ptr(block_tables),
         block_tables.stride(0), ptr(seq_lens), ptr(cu_q), ptr(work), n_work, float(scale), Hq, Hkv,
-        D, bs, hpw, 1 if causal else 0, sliding_window or 0, chunk_size or 0, qt or prefill_tiles(D),
+        D, bs, hpw, 1 if causal else 0, sliding_window or 0, chunk_size or 0, qt or prefill_variant(Hq, Hkv, D, bs),
         stream(q)),
         "paged_prefill")
     return o

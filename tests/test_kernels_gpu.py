@@ -196,7 +196,10 @@ def test_paged_prefill(Hq, Hkv, D, bs, causal):
     r = ref.paged_attention_prefill(q.cpu().float(), k.cpu().float(), v.cpu().float(), bt.cpu(),
                                     cu.cpu(), sl.cpu(), D ** -0.5, causal)
     # every tiles-per-wave variant the register budget allows at this head size
-    for qt in sorted({1, attention.prefill_tiles(D)} | ({2, 3, 4} if D <= 128 else set())):
+    qts = {1, attention.prefill_tiles(D)} | ({2, 3, 4} if D <= 128 else set())
+    if attention.heads_per_workgroup(Hq, Hkv) == 4 and bs % 32 == 0 and D in (64, 128):
+        qts |= {attention.PREFILL_LDS | t for t in (1, 2, 3, 4)}
+    for qt in sorted(qts):
         qb = attention.prefill_query_block(Hq, Hkv, D, qt)
         work = torch.tensor(attention.build_prefill_work(qlens, qb), dtype=torch.int32, device=DEV)
         o = attention.paged_prefill(q, k, v, bt, sl, cu, work, work.numel() // 2, D ** -0.5,
@@ -215,8 +218,8 @@ def test_paged_prefill_sliding_and_chunk():
     sl = torch.tensor(lens, dtype=torch.int32, device=DEV)
     cu = torch.tensor([0, 90, 123], dtype=torch.int32, device=DEV)
     q = torch.randn(123, Hq, D, device=DEV, dtype=BF)
-    work = torch.tensor(attention.build_prefill_work(qlens, attention.prefill_query_block(Hq, Hkv, D)),
-                        dtype=torch.int32, device=DEV)
+    work = torch.tensor(attention.build_prefill_work(
+        qlens, attention.prefill_query_block(Hq, Hkv, D, block_size=bs)), dtype=torch.int32, device=DEV)
     for sw, ch in ((50, None), (None, 64)):
         o = attention.paged_prefill(q, k, v, bt, sl, cu, work, work.numel() // 2, D ** -0.5, True,
                                     sw, ch)
