@@ -91,6 +91,8 @@ class ModelRunner:
         self.is_gpu = device.type == "cuda"
         if self.is_gpu:
             _native.kernels()         # fail loudly now if the HIP library is unusable
+            from ..ops import gemm as _gemm_ops
+            _gemm_ops.enable_prefill_tuning()
         torch.manual_seed(cfg.seed)
         t0 = time.time()
         self.model = build_model(cfg, device)

@@ -27,6 +27,10 @@ TUNING_FILE = os.environ.get("EIA_GEMM_TUNING",
                              os.path.join(os.path.dirname(os.path.abspath(__file__)),
                                           "gemm_tuning.json"))
 
+PREFILL_TUNING_FILE = os.environ.get(
+    "EIA_PREFILL_GEMM_TUNING",
+    os.path.join(os.path.dirname(os.path.abspath(__file__)), "tunableop_mi355x.csv"))
+
 MODE_BF16, MODE_SPLIT, MODE_SWIGLU = 0, 1, 2
 # kernel configs: bit0 -> 2 W tiles (32 rows) per wave, bit1 -> 4 waves per workgroup
 # bit0 NT=2, bit1 WAVES=4, bits2-3 pipeline stages-2, bit4 128-deep K chunks (else 256)
@@ -215,6 +219,23 @@ def swiglu_gemm(x: torch.Tensor, w_gate_up: torch.Tensor, cfg: Optional[int] = N
                                 ptr(out), out.stride(0), M, N, K, 1, MODE_SWIGLU, cfg, stream(x)),
           "gemm_skinny_swiglu")
     return out
+
+
+@functools.lru_cache(maxsize=1)
+def enable_prefill_tuning() -> bool:
+    """Load the in-tree TunableOp results (scripts/tune_prefill_gemm.py) for the prefill
+    F.linear GEMMs, lookup only: tuning stays OFF so a serving step never times kernels, and
+    shapes missing from the file keep hipBLASLt's default pick.  TunableOp rejects a file
+    whose recorded torch/ROCm/hipBLASLt/arch validators differ from this process's."""
+    if os.environ.get("EIA_PREFILL_GEMM_TUNING", "") == "off" or not os.path.exists(
+            PREFILL_TUNING_FILE) or not torch.cuda.is_available():
+        return False
+    t = torch.cuda.tunable
+    t.enable(True)
+    t.set_tuning_enabled(False)
+    t.write_file_on_exit(False)          # never rewrite the in-tree file
+    t.read_file(PREFILL_TUNING_FILE)
+    return True
 
 
 def linear(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = None,
