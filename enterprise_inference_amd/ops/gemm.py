@@ -12,24 +12,25 @@ from __future__ import annotations
 import functools
 import json
 import os
+import tempfile
 from typing import Optional
 
 import torch
 import torch.nn.functional as F
 
+from ..utils.cache_dir import resolve
 from ._dispatch import check, lib, ptr, stream, use_hip
 
 MAX_M = 128
 KC = 256
 TARGET_WGS = int(os.environ.get("EIA_SKINNY_TARGET_WGS", "512"))
 DISABLE = os.environ.get("EIA_DISABLE_SKINNY_GEMM", "0") == "1"
-TUNING_FILE = os.environ.get("EIA_GEMM_TUNING",
-                             os.path.join(os.path.dirname(os.path.abspath(__file__)),
-                                          "gemm_tuning.json"))
-
-PREFILL_TUNING_FILE = os.environ.get(
-    "EIA_PREFILL_GEMM_TUNING",
-    os.path.join(os.path.dirname(os.path.abspath(__file__)), "tunableop_mi355x.csv"))
+_HERE = os.path.dirname(os.path.abspath(__file__))
+# env override > persistent PVC cache ($EIA_CACHE_DIR, utils/cache_dir.py) > in-tree table
+TUNING_FILE = resolve("gemm_tuning.json", os.path.join(_HERE, "gemm_tuning.json"),
+                      "EIA_GEMM_TUNING")
+PREFILL_TUNING_FILE = resolve("tunableop_mi355x.csv", os.path.join(_HERE, "tunableop_mi355x.csv"),
+                              "EIA_PREFILL_GEMM_TUNING")
 
 MODE_BF16, MODE_SPLIT, MODE_SWIGLU = 0, 1, 2
 # kernel configs: bit0 -> 2 W tiles (32 rows) per wave, bit1 -> 4 waves per workgroup
@@ -232,8 +233,10 @@ def enable_prefill_tuning() -> bool:
         return False
     t = torch.cuda.tunable
     t.enable(True)
-    t.set_tuning_enabled(False)
-    t.write_file_on_exit(False)          # never rewrite the in-tree file
+    t.tuning_enable(False)
+    # results are written back on exit to the current filename: point it at scratch so the
+    # in-tree (or cache-dir) file is never rewritten by a serving process
+    t.set_filename(os.path.join(tempfile.gettempdir(), "eia_tunableop_results%d.csv"), True)
     t.read_file(PREFILL_TUNING_FILE)
     return True
 

@@ -80,6 +80,8 @@ def main():
     ap.add_argument("--tune", action="store_true")
     ap.add_argument("--sweep", action="store_true", help="time every candidate (no table write)")
     ap.add_argument("--out", default=None, help="also write the tuning table here")
+    ap.add_argument("--persist", action="store_true",
+                    help="also copy the table into the PVC tuning cache ($EIA_CACHE_DIR)")
     ap.add_argument("--packed", action="store_true",
                     help="sweep the tile-packed-weight configurations (cfg bit 6)")
     a = ap.parse_args()
@@ -143,6 +145,9 @@ def main():
             with open(a.out, "w") as f:
                 json.dump({"device": torch.cuda.get_device_name(0), "entries": tuned}, f, indent=0,
                           sort_keys=True)
+        if a.persist:
+            from enterprise_inference_amd.utils.cache_dir import persist
+            print("persisted", persist(gemm.TUNING_FILE, "gemm_tuning.json"))
 
 
 if __name__ == "__main__":

@@ -43,6 +43,8 @@ def main():
     ap.add_argument("--model", nargs="*", default=["8b"])
     ap.add_argument("--m", type=int, nargs="*", default=[8192, 4096, 2048, 192])
     ap.add_argument("--out", default="enterprise_inference_amd/ops/tunableop_mi355x.csv")
+    ap.add_argument("--persist", action="store_true",
+                    help="also copy the results into the PVC tuning cache ($EIA_CACHE_DIR)")
     a = ap.parse_args()
     t = torch.cuda.tunable
     dev, bf = "cuda", torch.bfloat16
@@ -53,7 +55,7 @@ def main():
         w = torch.randn(n, k, device=dev, dtype=bf)
         base[(m, n, k)] = timeit(lambda: F.linear(x, w))
     t.enable(True)
-    t.set_tuning_enabled(True)
+    t.tuning_enable(True)
     t.set_max_tuning_duration(30)
     t.set_max_tuning_iterations(20)
     t.set_filename(os.path.abspath(a.out))
@@ -64,7 +66,7 @@ def main():
         F.linear(x, w)                       # first call tunes this shape
         torch.cuda.synchronize()
         print(f"tuned {m}x{n}x{k} at {time.time() - t0:.0f}s", flush=True)
-    t.set_tuning_enabled(False)
+    t.tuning_enable(False)
     for m, n, k in cases:
         x = torch.randn(m, k, device=dev, dtype=bf)
         w = torch.randn(n, k, device=dev, dtype=bf)
@@ -76,6 +78,9 @@ def main():
                           "tuned_PF": round(fl / us / 1e9, 2)}), flush=True)
     t.write_file()
     print("wrote", a.out)
+    if a.persist:
+        from enterprise_inference_amd.utils.cache_dir import persist
+        print("persisted", persist(os.path.abspath(a.out), "tunableop_mi355x.csv"))
 
 
 if __name__ == "__main__":

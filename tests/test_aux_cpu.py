@@ -142,3 +142,23 @@ def test_concurrent_streaming_stress(tmp_path):
         assert sum(toks) == sum(6 + i % 5 for i in range(32))
     finally:
         aeng.shutdown()
+
+
+def test_tuning_cache_dir_lookup(tmp_path, monkeypatch):
+    """tuning results persist on the PVC and win over the in-tree tables."""
+    from enterprise_inference_amd.utils import cache_dir as cd
+    in_tree = tmp_path / "in_tree.json"
+    in_tree.write_text("{}")
+    monkeypatch.setenv("EIA_CACHE_DIR", str(tmp_path / "cache"))
+    monkeypatch.delenv("EIA_GEMM_TUNING", raising=False)
+    assert cd.resolve("gemm_tuning.json", str(in_tree), "EIA_GEMM_TUNING") == str(in_tree)
+    dst = cd.persist(str(in_tree), "gemm_tuning.json")
+    assert dst == str(tmp_path / "cache" / "gemm_tuning.json") and os.path.isfile(dst)
+    assert cd.resolve("gemm_tuning.json", str(in_tree), "EIA_GEMM_TUNING") == dst
+    # an explicit override wins only when it names an existing file ("off" passes through)
+    monkeypatch.setenv("EIA_GEMM_TUNING", str(tmp_path / "missing.json"))
+    assert cd.resolve("gemm_tuning.json", str(in_tree), "EIA_GEMM_TUNING") == dst
+    monkeypatch.setenv("EIA_GEMM_TUNING", "off")
+    assert cd.resolve("gemm_tuning.json", str(in_tree), "EIA_GEMM_TUNING") == "off"
+    monkeypatch.setenv("EIA_CACHE_DIR", "")
+    assert cd.cache_dir() is None and cd.persist(str(in_tree)) is None
