@@ -241,10 +241,35 @@ def enable_prefill_tuning() -> bool:
     return True
 
 
+# Prefill rows are split into a PREFILL_ALIGN-aligned body (one library GEMM written in place)
+# and a remainder (skinny kernel when <= MAX_M rows): hipBLASLt's default pick at ragged M
+# (e.g. 8320 = 8192 + 128) runs up to 1.7x slower than at the aligned M below it
+# (profiles/tune_prefill_gemm_r1.log).  Off by default: the ragged-M probe
+# (profiles/probe_prefill_split_r1.log) shows the split winning big where the default pick
+# falls off a cliff (down_proj at M = 4100 / 6200 / 8320: 1.5-2.3x) but losing where the
+# aligned body itself hits one (M = 7000 -> 6912 rows); exact shapes go through TunableOp.
+PREFILL_ALIGN = int(os.environ.get("EIA_PREFILL_ALIGN_M", "0"))
+
+
+def _aligned_linear(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor]):
+    m = x.shape[0]
+    body = m - m % PREFILL_ALIGN
+    out = torch.empty(m, w.shape[0], dtype=x.dtype, device=x.device)
+    if bias is not None:
+        torch.addmm(bias, x[:body], w.t(), out=out[:body])
+    else:
+        torch.matmul(x[:body], w.t(), out=out[:body])
+    out[body:] = linear(x[body:], w, bias)
+    return out
+
+
 def linear(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = None,
            defer_reduce: bool = False):
     if x.dim() == 2 and skinny_ok(x, w):
         return skinny(x, w, bias, defer_reduce)
+    if (PREFILL_ALIGN and x.dim() == 2 and x.shape[0] > PREFILL_ALIGN
+            and x.shape[0] % PREFILL_ALIGN and x.is_cuda and x.is_contiguous()):
+        return _aligned_linear(x, w, bias)
     return F.linear(x, w, bias)
 
 
