@@ -147,6 +147,12 @@ def engine_config_from_args(args: argparse.Namespace):
         enable_chunked_prefill=bool(args.enable_chunked_prefill),
         decode_bs_bucket_step=int(os.environ.get("VLLM_DECODE_BS_BUCKET_STEP", 16)),
         delayed_sampling=_truthy(os.environ.get("VLLM_DELAYED_SAMPLING", "true")))
+    kvd = (args.kv_cache_dtype or "auto").lower()
+    if kvd not in ("auto", "bfloat16", "bf16", "float16", "fp16", "half", "float32"):
+        # fp8 KV (vLLM --kv-cache-dtype fp8*) is not implemented: the paged decode/prefill
+        # kernels read bf16 K/V.  Keep serving in the model dtype, loudly.
+        logger.warning("--kv-cache-dtype %s is not supported; the KV cache stays in the model "
+                       "dtype (%s)", kvd, dtype)
     cache = CacheConfig(block_size=args.block_size,
                         gpu_memory_utilization=args.gpu_memory_utilization,
                         cpu_kvcache_space_gb=float(os.environ.get("VLLM_CPU_KVCACHE_SPACE", 4)),

@@ -162,3 +162,17 @@ def test_tuning_cache_dir_lookup(tmp_path, monkeypatch):
     assert cd.resolve("gemm_tuning.json", str(in_tree), "EIA_GEMM_TUNING") == "off"
     monkeypatch.setenv("EIA_CACHE_DIR", "")
     assert cd.cache_dir() is None and cd.persist(str(in_tree)) is None
+
+
+def test_kv_cache_dtype_fp8_warns_and_keeps_model_dtype(tmp_path, caplog):
+    from enterprise_inference_amd.entrypoints.cli_args import engine_config_from_args
+    from enterprise_inference_amd.models import catalog
+    d = tmp_path / "tiny"
+    d.mkdir(exist_ok=True)
+    (d / "config.json").write_text(json.dumps(catalog.tiny_config(vocab_size=300)))
+    args = parse_args(["--model", str(d), "--device", "cpu", "--load-format", "dummy",
+                       "--kv-cache-dtype", "fp8_e4m3"])
+    with caplog.at_level("WARNING"):
+        cfg = engine_config_from_args(args)
+    assert "kv-cache-dtype fp8_e4m3 is not supported" in caplog.text
+    assert cfg.cache.cache_dtype == cfg.dtype
