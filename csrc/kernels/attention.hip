@@ -21,6 +21,14 @@
 #ifndef EIA_LEAN_OCC
 #define EIA_LEAN_OCC 3
 #endif
+// waves/SIMD the one-tile LDS prefill kernel is register-bounded for (2 or 3)
+// units of K/V global loads in flight ahead of the one being multiplied (1 or 2)
+#ifndef EIA_PREFILL_DEPTH
+#define EIA_PREFILL_DEPTH 1
+#endif
+#ifndef EIA_PREFILL_OCC
+#define EIA_PREFILL_OCC 2
+#endif
 
 template <int D>
 struct WaveAcc {
@@ -161,6 +169,57 @@ EIA_DEV void softmax_pv(WaveAcc<D>& acc, const f32x4& s0, const f32x4& s1,
     psum += bf2f(pbf);     // normalise with exactly the weights fed to the MFMA
   }
   acc.l = acc.l * alpha + psum;
+  acc.m = mnew;
+  if (!__all(alpha == 1.f)) {
+#pragma unroll
+    for (int dt = 0; dt < D / 16; ++dt) acc.o[dt] *= alpha;
+  }
+#pragma unroll
+  for (int dt = 0; dt < D / 16; ++dt)
+    acc.o[dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vfr[dt], pb, acc.o[dt], 0, 0, 0);
+}
+
+// softmax_pv for the LDS prefill kernel, trimmed of VALU work (the kernel issues ~9 VALU per
+// MFMA, profiles/pmc_prefill_r1.md): the running max is taken on raw scores and scaled once,
+// the scale folds into the exponent's FMA, the row sum adds the fp32 weights (their bf16
+// rounding, fed to the MFMA, is < 2^-9 relative), and mask = false -- a unit every query of
+// the tile sees whole (below the causal diagonal, inside L, no window) -- skips the per-score
+// position tests (one code path: two inlined copies measured slower at QT = 1).
+template <int D>
+EIA_DEV void softmax_pv_lean(WaveAcc<D>& acc, const f32x4& s0, const f32x4& s1,
+                             const bf16x8 (&vfr)[D / 16], int tb, int L, float scale_log2,
+                             int q_abs, int kv_lo, bool mask) {
+  float v[8];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    v[i] = s0[i];
+    v[4 + i] = s1[i];
+  }
+  if (mask) {                                       // wave-uniform branch
+    const int g = (threadIdx.x & 63) >> 4;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int t0 = tb + 8 * g + i, t1 = t0 + 4;
+      if (!((t0 < L) && (t0 <= q_abs) && (t0 >= kv_lo))) v[i] = NEG_INF;
+      if (!((t1 < L) && (t1 <= q_abs) && (t1 >= kv_lo))) v[4 + i] = NEG_INF;
+    }
+  }
+  float mloc = fmaxf(fmaxf(fmaxf(v[0], v[1]), fmaxf(v[2], v[3])),
+                     fmaxf(fmaxf(v[4], v[5]), fmaxf(v[6], v[7])));
+  mloc = fmaxf(mloc, __shfl_xor(mloc, 16, 64));
+  mloc = fmaxf(mloc, __shfl_xor(mloc, 32, 64));
+  const float mnew = fmaxf(acc.m, mloc * scale_log2);
+  const float muse = (mnew == NEG_INF) ? 0.f : mnew;
+  const float alpha = exp2f(acc.m - muse);
+  bf16x8 pb;
+  float psum = 0.f;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const float p = exp2f(fmaf(v[i], scale_log2, -muse));
+    pb[i] = f2bf(p);
+    psum += p;
+  }
+  acc.l = fmaf(acc.l, alpha, psum);
   acc.m = mnew;
   if (!__all(alpha == 1.f)) {
 #pragma unroll
@@ -631,7 +690,7 @@ EIA_DEV void prefill_lds_store(bf16_t* __restrict__ kl, bf16_t* __restrict__ vl,
 }
 
 template <int D, int QT>
-__global__ void __launch_bounds__(256)
+__global__ void __launch_bounds__(256, QT == 1 ? EIA_PREFILL_OCC : (QT == 2 ? 2 : 1))
 paged_prefill_lds_kernel(const bf16_t* __restrict__ q, long q_stride,
                          bf16_t* __restrict__ out, long out_stride,
                          const bf16_t* __restrict__ kc, const bf16_t* __restrict__ vc,
@@ -686,43 +745,79 @@ paged_prefill_lds_kernel(const bf16_t* __restrict__ q, long q_stride,
 #pragma unroll
   for (int t = 0; t < QT; ++t) wave_acc_init(acc[t]);
   const int* bt = block_tables + (long)s * bt_stride;
+  const bool nowin = sliding_window <= 0 && chunk_size <= 0;
+  int q_first[QT];                                   // smallest causal bound in each tile
+#pragma unroll
+  for (int t = 0; t < QT; ++t) q_first[t] = causal ? ctx + qstart + 16 * t : 0x7fffffff;
+  // one 32-token unit from LDS buffer `b`: S^T for every live tile from one K fragment read
+  auto unit = [&](int tb, int b) {
+    const bf16_t* kl = lds + b * LL::KE;
+    const bf16_t* vl = lds + 2 * LL::KE + b * LL::VE;
+    const int tk0 = 8 * (c >> 2) + (c & 3);
+    bf16x8 k0[D / 32], k1[D / 32];
+#pragma unroll
+    for (int ss = 0; ss < D / 32; ++ss) {
+      k0[ss] = *reinterpret_cast<const bf16x8*>(kl + tk0 * LL::KS + 8 * g + 32 * ss);
+      k1[ss] = *reinterpret_cast<const bf16x8*>(kl + (tk0 + 4) * LL::KS + 8 * g + 32 * ss);
+    }
+    f32x4 s0[QT], s1[QT];
+#pragma unroll
+    for (int t = 0; t < QT; ++t)
+      if (tb < t_hi[t]) qk_unit<D>(s0[t], s1[t], qf[t], k0, k1);
+    bf16x8 vf[D / 16];
+#pragma unroll
+    for (int dt = 0; dt < D / 16; ++dt)
+      vf[dt] = *reinterpret_cast<const bf16x8*>(vl + (16 * dt + c) * LL::VS + 8 * g);
+#pragma unroll
+    for (int t = 0; t < QT; ++t) {
+      if (tb >= t_hi[t]) continue;
+      // wave-uniform: is every score of this unit visible to every query of tile t?
+      const bool whole = nowin && tb + 32 <= L && tb + 31 <= q_first[t];
+      softmax_pv_lean<D>(acc[t], s0[t], s1[t], vf, tb, L, scale_log2, q_abs[t], kv_lo[t], !whole);
+    }
+  };
+  bf16_t* const lk = lds;
+  bf16_t* const lv = lds + 2 * LL::KE;
+#if EIA_PREFILL_DEPTH >= 2
+  // Two units in flight: unit i+2's global loads are issued before unit i is multiplied, so a
+  // load has two units of compute to land (one unit, ~0.2 us of MFMA + softmax, hides only a
+  // fraction of the L2/HBM latency).  Two register staging sets alternate by loop half (no
+  // runtime-indexed register arrays); LDS stays double-buffered: unit i+1 is written after
+  // unit i is multiplied, into the buffer unit i-1 used, which every wave left before this
+  // half's barrier.  Loop bounds are workgroup-uniform, so every wave reaches every barrier.
+  bf16x8 sa[2 * LL::NCH], sb[2 * LL::NCH];
+  if (lo_w < hi_w) {
+    prefill_lds_fetch<D>(sa, kc, vc, bt, lo_w, kvh, Hkv, bs);
+    prefill_lds_store<D>(lk, lv, sa);
+  }
+  if (lo_w + 32 < hi_w) prefill_lds_fetch<D>(sb, kc, vc, bt, lo_w + 32, kvh, Hkv, bs);
+  for (int tb = lo_w; tb < hi_w; tb += 64) {
+    if (tb + 64 < hi_w) prefill_lds_fetch<D>(sa, kc, vc, bt, tb + 64, kvh, Hkv, bs);
+    __syncthreads();
+    unit(tb, 0);
+    if (tb + 32 >= hi_w) break;
+    prefill_lds_store<D>(lk + LL::KE, lv + LL::VE, sb);
+    if (tb + 96 < hi_w) prefill_lds_fetch<D>(sb, kc, vc, bt, tb + 96, kvh, Hkv, bs);
+    __syncthreads();
+    unit(tb + 32, 1);
+    if (tb + 64 < hi_w) prefill_lds_store<D>(lk, lv, sa);
+  }
+#else
   bf16x8 st[2 * LL::NCH];
   if (lo_w < hi_w) {
     prefill_lds_fetch<D>(st, kc, vc, bt, lo_w, kvh, Hkv, bs);
-    prefill_lds_store<D>(lds, lds + 2 * LL::KE, st);
+    prefill_lds_store<D>(lk, lv, st);
   }
   int buf = 0;
   for (int tb = lo_w; tb < hi_w; tb += 32) {
     const bool more = tb + 32 < hi_w;
     if (more) prefill_lds_fetch<D>(st, kc, vc, bt, tb + 32, kvh, Hkv, bs);
     __syncthreads();
-    const bf16_t* kl = lds + buf * LL::KE;
-    const bf16_t* vl = lds + 2 * LL::KE + buf * LL::VE;
-    {
-      // S^T for every live tile from one K fragment read
-      const int tk0 = 8 * (c >> 2) + (c & 3);
-      bf16x8 k0[D / 32], k1[D / 32];
-#pragma unroll
-      for (int ss = 0; ss < D / 32; ++ss) {
-        k0[ss] = *reinterpret_cast<const bf16x8*>(kl + tk0 * LL::KS + 8 * g + 32 * ss);
-        k1[ss] = *reinterpret_cast<const bf16x8*>(kl + (tk0 + 4) * LL::KS + 8 * g + 32 * ss);
-      }
-      f32x4 s0[QT], s1[QT];
-#pragma unroll
-      for (int t = 0; t < QT; ++t)
-        if (tb < t_hi[t]) qk_unit<D>(s0[t], s1[t], qf[t], k0, k1);
-      bf16x8 vf[D / 16];
-#pragma unroll
-      for (int dt = 0; dt < D / 16; ++dt)
-        vf[dt] = *reinterpret_cast<const bf16x8*>(vl + (16 * dt + c) * LL::VS + 8 * g);
-#pragma unroll
-      for (int t = 0; t < QT; ++t)
-        if (tb < t_hi[t])
-          softmax_pv<D>(acc[t], s0[t], s1[t], vf, tb, L, scale_log2, q_abs[t], kv_lo[t]);
-    }
-    if (more) prefill_lds_store<D>(lds + (buf ^ 1) * LL::KE, lds + 2 * LL::KE + (buf ^ 1) * LL::VE, st);
+    unit(tb, buf);
+    if (more) prefill_lds_store<D>(lk + (buf ^ 1) * LL::KE, lv + (buf ^ 1) * LL::VE, st);
     buf ^= 1;
   }
+#endif
 
 #pragma unroll
   for (int t = 0; t < QT; ++t) {

@@ -36,8 +36,12 @@ def prefill_tiles(head_dim: int) -> int:
 PREFILL_LDS = 16          # kernel variant flag: K/V units shared by the workgroup through LDS
 # LDS form, D = 128 causal (profiles/prefill_attn_lds_r1.log): qt 1/2/3/4 = 1296/1905/1865/2186 us
 # at 1x8192 (register form qt 3: 1867 us).  qt 1 needs 185 registers -> 2 waves/SIMD, and with
-# the K/V traffic already cut 4x by LDS sharing, occupancy is what pays.
-PREFILL_LDS_QT = {64: 1, 128: 1}
+# the K/V traffic already cut 4x by LDS sharing, occupancy is what pays.  After the VALU trim
+# (softmax_pv_lean: uniform unmasked units, scale folded into the exponent FMA; PMC counts had
+# ~9 VALU per MFMA, profiles/pmc_prefill_r1.md) and a 2-wave register bound for qt 2, qt 2
+# wins at 1x8192 / 4x2048 / 65x128 = 1045 / 270 / 52.5 us vs qt 1 1181 / 276 / 55.1 us, and
+# loses at 16x512 (90 vs 85 us) (profiles/prefill_attn_lean_r1.log).
+PREFILL_LDS_QT = {64: 1, 128: 2}
 
 
 def prefill_variant(num_heads: int, num_kv_heads: int, head_dim: int,
