@@ -649,12 +649,24 @@ paged_prefill_kernel(const bf16_t* __restrict__ q, long q_stride,
 // before unit u is multiplied and land in LDS after it; one barrier per unit orders both the
 // LDS writes before their reads and the reads of a buffer before its next overwrite.  The
 // unit loop bounds depend only on blockIdx, so every wave reaches every barrier.
+// D = 128 stores K and V^T unpadded with XOR-swizzled 16-B chunks instead of padded rows: the
+// padded rows left the fragment reads 2-way bank conflicted (SQ_LDS_BANK_CONFLICT = 1.7x the
+// LDS-active cycles, profiles/pmc_prefill_r1.md).  ds_read_b128 serves 4 groups of 16 lanes
+// ({0-3,12-15,20-27}, {4-11,16-19,28-31}, +32), each conflict-free when its 16 lanes hit 16
+// distinct 16-B slots of the 256-B bank row.  K row r (256 B), chunk j -> slot j ^ kswz(r):
+// the fragment rows 8(c>>2)+(c&3) (+4) of the c = lane&15 columns with chunk g = lane>>4
+// land on 16 distinct slots in every group (kswz found by exhaustive search over XOR-linear
+// maps).  V^T row d (64 B, four rows per bank row), chunk j -> j ^ vswz(d).  The stores
+// (ds_write_b128, 8 contiguous lanes per 128 B) stay conflict-free under both maps.
 template <int D>
 struct PrefillLds {
-  static constexpr int KS = D + 8;                  // K row stride (elements): +16 B per token
-  static constexpr int VS = 32 + 8;                 // V^T row stride: 32 tokens + 16 B
+  static constexpr bool SWZ = (D == 128);
+  static constexpr int KS = SWZ ? D : D + 8;        // K row stride (elements)
+  static constexpr int VS = SWZ ? 32 : 32 + 8;      // V^T row stride: 32 tokens (+16 B pad)
   static constexpr int KE = 32 * KS, VE = D * VS;   // elements per buffer
   static constexpr int NCH = (32 * D / 8) / 256;    // 16-B K (and V) chunks per thread per unit
+  static EIA_DEV int kswz(int r) { return SWZ ? ((r & 3) | ((r >> 1) & 12)) : 0; }
+  static EIA_DEV int vswz(int d) { return SWZ ? ((d >> 2) & 2) : 0; }
 };
 
 template <int D>
@@ -683,8 +695,9 @@ EIA_DEV void prefill_lds_store(bf16_t* __restrict__ kl, bf16_t* __restrict__ vl,
   for (int i = 0; i < PrefillLds<D>::NCH; ++i) {
     const int id = tid + 256 * i;
     const int r = id / (D / 8), c8 = id % (D / 8);
-    *reinterpret_cast<bf16x8*>(kl + r * PrefillLds<D>::KS + 8 * c8) = st[i];
-    *reinterpret_cast<bf16x8*>(vl + (id >> 2) * PrefillLds<D>::VS + 8 * (id & 3)) =
+    *reinterpret_cast<bf16x8*>(kl + r * PrefillLds<D>::KS + 8 * (c8 ^ PrefillLds<D>::kswz(r))) = st[i];
+    const int vd = id >> 2;
+    *reinterpret_cast<bf16x8*>(vl + vd * PrefillLds<D>::VS + 8 * ((id & 3) ^ PrefillLds<D>::vswz(vd))) =
         st[PrefillLds<D>::NCH + i];
   }
 }
@@ -754,11 +767,13 @@ paged_prefill_lds_kernel(const bf16_t* __restrict__ q, long q_stride,
     const bf16_t* kl = lds + b * LL::KE;
     const bf16_t* vl = lds + 2 * LL::KE + b * LL::VE;
     const int tk0 = 8 * (c >> 2) + (c & 3);
+    const int ksw = LL::kswz(tk0);                   // == kswz(tk0 + 4)
     bf16x8 k0[D / 32], k1[D / 32];
 #pragma unroll
     for (int ss = 0; ss < D / 32; ++ss) {
-      k0[ss] = *reinterpret_cast<const bf16x8*>(kl + tk0 * LL::KS + 8 * g + 32 * ss);
-      k1[ss] = *reinterpret_cast<const bf16x8*>(kl + (tk0 + 4) * LL::KS + 8 * g + 32 * ss);
+      const int j = 8 * ((g + 4 * ss) ^ ksw);
+      k0[ss] = *reinterpret_cast<const bf16x8*>(kl + tk0 * LL::KS + j);
+      k1[ss] = *reinterpret_cast<const bf16x8*>(kl + (tk0 + 4) * LL::KS + j);
     }
     f32x4 s0[QT], s1[QT];
 #pragma unroll
@@ -767,7 +782,8 @@ paged_prefill_lds_kernel(const bf16_t* __restrict__ q, long q_stride,
     bf16x8 vf[D / 16];
 #pragma unroll
     for (int dt = 0; dt < D / 16; ++dt)
-      vf[dt] = *reinterpret_cast<const bf16x8*>(vl + (16 * dt + c) * LL::VS + 8 * g);
+      vf[dt] = *reinterpret_cast<const bf16x8*>(vl + (16 * dt + c) * LL::VS +
+                                                 8 * (g ^ LL::vswz(16 * dt + c)));
 #pragma unroll
     for (int t = 0; t < QT; ++t) {
       if (tb >= t_hi[t]) continue;

@@ -40,7 +40,9 @@ PREFILL_LDS = 16          # kernel variant flag: K/V units shared by the workgro
 # (softmax_pv_lean: uniform unmasked units, scale folded into the exponent FMA; PMC counts had
 # ~9 VALU per MFMA, profiles/pmc_prefill_r1.md) and a 2-wave register bound for qt 2, qt 2
 # wins at 1x8192 / 4x2048 / 65x128 = 1045 / 270 / 52.5 us vs qt 1 1181 / 276 / 55.1 us, and
-# loses at 16x512 (90 vs 85 us) (profiles/prefill_attn_lean_r1.log).
+# loses at 16x512 (90 vs 85 us) (profiles/prefill_attn_lean_r1.log).  With the bank-conflict-
+# free swizzled LDS layout: qt 2 = 1018 / 269 / 89 / 51.7 us, qt 1 = 1090 / 254 / 80 / 54.2 us
+# at 1x8192 / 4x2048 / 16x512 / 65x128 (profiles/prefill_attn_swizzle_r1.log).
 PREFILL_LDS_QT = {64: 1, 128: 2}
 
 

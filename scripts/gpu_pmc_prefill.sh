@@ -10,7 +10,7 @@ cd /tmp
 pass() {  # name counters...
   local n=$1; shift
   timeout -s KILL 120 rocprofv3 --kernel-trace --pmc "$@" -d "$OUT/$n" -o run --output-format csv \
-    -- python3 "$R/scripts/bench_prefill_attn.py" --shapes 1x8192 --qt 17 --iters 2 > "$OUT/$n.log" 2>&1
+    -- python3 "$R/scripts/bench_prefill_attn.py" --shapes 1x8192 --qt ${PMC_QT:-18} --iters 2 > "$OUT/$n.log" 2>&1
   local rc=$?; tail -2 "$OUT/$n.log"; return $rc
 }
 pass p1 SQ_WAVES SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_INSTS_MFMA SQ_INSTS_LDS SQ_INSTS_VALU &&
