@@ -27,6 +27,10 @@ SHAPES = {  # name: (N, K, swiglu)
     "qkv_70b_tp8": (1280, 8192, False), "o_70b_tp8": (8192, 1024, False),
     "gate_up_70b_tp8": (7168, 8192, True), "down_70b_tp8": (8192, 3584, False),
     "lm_head_70b_tp8": (16032, 8192, False),
+    # Llama-3.3-70B on one GPU (profiles/sizing_70b_tp1_r1.md)
+    "qkv_70b": (10240, 8192, False), "o_70b": (8192, 8192, False),
+    "gate_up_70b": (57344, 8192, True), "down_70b": (8192, 28672, False),
+    "lm_head_70b": (128256, 8192, False),
 }
 
 
