@@ -31,6 +31,13 @@ SHAPES = {  # name: (N, K, swiglu)
     "qkv_70b": (10240, 8192, False), "o_70b": (8192, 8192, False),
     "gate_up_70b": (57344, 8192, True), "down_70b": (8192, 28672, False),
     "lm_head_70b": (128256, 8192, False),
+    # Llama-3.x-70B at TP4 (the reference's 70B deployment) and Llama-3.1-405B at TP8, per rank
+    "qkv_70b_tp4": (2560, 8192, False), "o_70b_tp4": (8192, 2048, False),
+    "gate_up_70b_tp4": (14336, 8192, True), "down_70b_tp4": (8192, 7168, False),
+    "lm_head_70b_tp4": (32064, 8192, False),
+    "qkv_405b_tp8": (2304, 16384, False), "o_405b_tp8": (16384, 2048, False),
+    "gate_up_405b_tp8": (13312, 16384, True), "down_405b_tp8": (16384, 6656, False),
+    "lm_head_405b_tp8": (16032, 16384, False),
 }
 
 
