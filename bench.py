@@ -1,23 +1,35 @@
 #!/usr/bin/env python3
-"""Flagship serving benchmark (BASELINE.json metric on its config #2).
+"""Flagship serving benchmark: the BASELINE.json metric, measured through the OpenAI endpoint.
 
-Metric: output tokens/s for the reference sizing-guide "Chatbot" use case
-(third_party/IBM/docs/sizing-guide.md:56: Llama-3.1-8B-Instruct, 128 input / 128
-output tokens, 65 concurrent users, 1 accelerator -> 3264 tok/s on Gaudi 3),
-plus p50/p90 TTFT.  Weights are random (no checkpoints offline), prompts are
-synthetic random token ids of exactly --input-len tokens, every request
-generates exactly --output-len tokens (ignore_eos).  Sampling is the server
-default (temperature 1.0) so the full sampler kernel runs.
+Metric: output tokens/s (+ TTFT p50/p90) of the reference sizing-guide "Chatbot" use
+case (third_party/IBM/docs/sizing-guide.md:56: Llama-3.1-8B-Instruct, 128 input /
+128 output tokens, 65 concurrent users, one accelerator -> 3264 tok/s, TTFT p90
+1300 ms on Gaudi 3), measured the way the guide does (sizing-guide.md:50-56):
+concurrent streaming requests against the OpenAI-compatible server.
 
-One "step" = one benchmark round: all --users requests arrive together and the
-round ends when the last one finishes (continuous batching inside).  W untimed
-rounds, then K timed rounds bracketed by barrier + device sync.
+Per replica this process (which never touches the GPU) starts
+  * the real server, ``python -m enterprise_inference_amd.entrypoints.openai.api_server``
+    (API process + engine-core process + TP workers), random-init weights
+    (``--load-format dummy``; no checkpoints offline), and
+  * client worker processes (aiohttp) that hold the --users concurrent streams:
+    streaming ``POST /v1/completions`` with exactly --input-len synthetic prompt token
+    ids, ``max_tokens=--output-len``, ``ignore_eos`` (exact output length), server-default
+    temperature 1.0 (the full sampler kernel runs).  TTFT = first SSE token chunk.
+
+One "step" = one round: all --users requests arrive together, the round ends when the
+last stream sent ``[DONE]``.  W untimed rounds, then K timed rounds bracketed on both
+sides by ``POST /eia/sync`` (the engine core runs ``torch.cuda.synchronize()``) and a
+barrier over all ranks (gloo, CPU); ms_per_step = max over ranks.  Tokens are counted
+from each stream's ``usage`` chunk and checked against --output-len.
 
 Multi-GPU (torchrun, one rank per GPU): each group of --tp ranks is one serving
-replica (default TP=1 -> N data-parallel replicas, the reference's one-pod-per-
-card deployment, third_party/IBM/patterns/quickstart/run_script.sh:79-81);
-per-GPU work is fixed -> weak scaling.  value = total output tokens of all
-replicas / max wall time over ranks.
+replica whose first rank launches a server on those GPUs (default TP=1 -> N
+data-parallel replicas, the reference's one-pod-per-card deployment,
+third_party/IBM/patterns/quickstart/run_script.sh:79-81): weak scaling.
+``value`` = total output tokens of all replicas / max wall time over ranks.
+
+``--mode engine`` drives ``LLMEngine`` in-process instead (no HTTP; for kernel
+profiling); its line says ``"measured_via": "engine"``.
 """
 
 from __future__ import annotations
@@ -26,7 +38,10 @@ import argparse
 import json
 import os
 import random
+import signal
+import socket
 import statistics
+import subprocess
 import sys
 import time
 
@@ -36,6 +51,7 @@ sys.path.insert(0, ROOT)
 BASELINE_TOK_S = {  # third_party/IBM/docs/sizing-guide.md (Gaudi 3, vLLM 0.7.2), per replica
     ("meta-llama/Llama-3.1-8B-Instruct", 128, 128): (3264.0, 1),
     ("meta-llama/Llama-3.3-70B-Instruct", 128, 128): (1120.0, 4),
+    ("meta-llama/Llama-3.1-405B-Instruct", 128, 128): (493.0, 8),
 }
 METRIC = "output tokens/sec (node) + p50 TTFT via OpenAI endpoint, Llama-3-8B/70B"
 
@@ -45,6 +61,7 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--mode", default="endpoint", choices=["endpoint", "engine"])
     ap.add_argument("--model", default="meta-llama/Llama-3.1-8B-Instruct")
     ap.add_argument("--tp", type=int, default=1)
     ap.add_argument("--users", type=int, default=65)
@@ -56,13 +73,281 @@ def parse():
     ap.add_argument("--gpu-memory-utilization", type=float, default=0.90)
     ap.add_argument("--temperature", type=float, default=1.0)
     ap.add_argument("--enforce-eager", action="store_true")
+    ap.add_argument("--client-procs", type=int, default=4,
+                    help="client worker processes per replica (streams are split among them)")
+    ap.add_argument("--server-args", default="", help="extra api_server flags")
+    ap.add_argument("--startup-timeout", type=float, default=1500)
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--verbose", action="store_true")
     return ap.parse_args()
 
 
-def main() -> int:
-    args = parse()
+def _pct(a, p):
+    return a[min(len(a) - 1, int(p / 100.0 * len(a)))] if a else None
+
+
+def _free_port() -> int:
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+# --------------------------------------------------------------------------- clients
+
+def _client_worker(conn, url: str, model: str, max_tokens: int, temperature: float,
+                   timeout: float) -> None:
+    """One client process: runs its share of the concurrent streams for every round."""
+    import asyncio
+
+    import aiohttp
+
+    async def one(session, prompt):
+        body = {"model": model, "prompt": prompt, "max_tokens": max_tokens, "ignore_eos": True,
+                "temperature": temperature, "stream": True,
+                "stream_options": {"include_usage": True}}
+        t0 = time.perf_counter()
+        first = None
+        usage = None
+        done = False
+        try:
+            async with session.post(url, json=body) as r:
+                if r.status != 200:
+                    return (False, 0.0, 0.0, 0, f"HTTP {r.status}: {(await r.text())[:200]}")
+                async for line in r.content:
+                    if not line.startswith(b"data: "):
+                        continue
+                    if first is None and line.startswith(b'data: {"id"') and b'"text":' in line:
+                        first = time.perf_counter()
+                    if b'"usage"' in line:
+                        usage = json.loads(line[6:])["usage"]
+                    elif line.startswith(b"data: [DONE]"):
+                        done = True
+                        break
+        except Exception as e:  # noqa: BLE001 - reported as a failed request
+            return (False, 0.0, 0.0, 0, repr(e))
+        t1 = time.perf_counter()
+        if not done or usage is None:
+            return (False, 0.0, 0.0, 0, "stream ended without usage/[DONE]")
+        return (True, (first or t1) - t0, t1 - t0, int(usage["completion_tokens"]), "")
+
+    async def main():
+        conn_limit = aiohttp.TCPConnector(limit=0, force_close=False)
+        to = aiohttp.ClientTimeout(total=timeout)
+        async with aiohttp.ClientSession(connector=conn_limit, timeout=to) as session:
+            loop = asyncio.get_running_loop()
+            while True:
+                prompts = await loop.run_in_executor(None, conn.recv)
+                if prompts is None:
+                    return
+                res = await asyncio.gather(*(one(session, p) for p in prompts))
+                conn.send(res)
+
+    asyncio.run(main())
+
+
+class ClientPool:
+    def __init__(self, n: int, url: str, model: str, max_tokens: int, temperature: float,
+                 timeout: float = 3600.0):
+        import multiprocessing as mp
+
+        ctx = mp.get_context("spawn")
+        self.conns, self.procs = [], []
+        for _ in range(n):
+            a, b = ctx.Pipe()
+            p = ctx.Process(target=_client_worker, args=(b, url, model, max_tokens, temperature,
+                                                         timeout), daemon=True)
+            p.start()
+            self.conns.append(a)
+            self.procs.append(p)
+
+    def round(self, prompts):
+        n = len(self.conns)
+        shares = [prompts[i::n] for i in range(n)]
+        for c, s in zip(self.conns, shares):
+            c.send(s)
+        out = []
+        for c in self.conns:
+            out += c.recv()
+        return out
+
+    def close(self):
+        for c in self.conns:
+            try:
+                c.send(None)
+            except OSError:
+                pass
+        for p in self.procs:
+            p.join(timeout=10)
+            if p.is_alive():
+                p.terminate()
+
+
+# --------------------------------------------------------------------------- server
+
+def _visible_devices(first: int, n: int) -> str:
+    cur = os.environ.get("HIP_VISIBLE_DEVICES") or os.environ.get("CUDA_VISIBLE_DEVICES")
+    ids = cur.split(",") if cur else [str(i) for i in range(first + n)]
+    return ",".join(ids[first:first + n])
+
+
+def start_server(args, local_rank: int, port: int, log_path: str) -> subprocess.Popen:
+    env = {k: v for k, v in os.environ.items()
+           if k not in ("RANK", "LOCAL_RANK", "WORLD_SIZE", "LOCAL_WORLD_SIZE", "GROUP_RANK",
+                        "ROLE_RANK", "MASTER_ADDR", "MASTER_PORT", "TORCHELASTIC_RUN_ID")}
+    env["HIP_VISIBLE_DEVICES"] = _visible_devices(local_rank, args.tp)
+    env.pop("CUDA_VISIBLE_DEVICES", None)
+    env["PYTHONPATH"] = ROOT + os.pathsep + env.get("PYTHONPATH", "")
+    cmd = [sys.executable, "-m", "enterprise_inference_amd.entrypoints.openai.api_server",
+           "--model", args.model, "--port", str(port), "--host", "127.0.0.1",
+           "--load-format", "dummy", "--tensor-parallel-size", str(args.tp),
+           "--max-model-len", str(args.input_len + args.output_len + 64),
+           "--max-num-seqs", str(args.max_num_seqs),
+           "--max-num-batched-tokens", str(args.max_num_batched_tokens),
+           "--block-size", str(args.block_size),
+           "--gpu-memory-utilization", str(args.gpu_memory_utilization),
+           "--seed", str(args.seed), "--disable-log-requests", "--uvicorn-log-level", "warning"]
+    if args.enforce_eager:
+        cmd.append("--enforce-eager")
+    cmd += args.server_args.split()
+    log = open(log_path, "w")
+    return subprocess.Popen(cmd, cwd=ROOT, env=env, stdout=log, stderr=subprocess.STDOUT,
+                            start_new_session=True)
+
+
+def _http(method: str, url: str, timeout: float = 600.0):
+    import urllib.request
+
+    req = urllib.request.Request(url, method=method, data=b"" if method == "POST" else None)
+    with urllib.request.urlopen(req, timeout=timeout) as r:
+        return r.status, r.read()
+
+
+def wait_healthy(base: str, proc: subprocess.Popen, timeout: float, log_path: str) -> None:
+    t0 = time.time()
+    while time.time() - t0 < timeout:
+        if proc.poll() is not None:
+            tail = open(log_path).read()[-4000:]
+            raise RuntimeError(f"server exited with code {proc.returncode}:\n{tail}")
+        try:
+            if _http("GET", base + "/health", 2.0)[0] == 200:
+                return
+        except Exception:  # noqa: BLE001 - not up yet
+            pass
+        time.sleep(0.5)
+    raise TimeoutError("server did not become healthy")
+
+
+def stop_server(proc: subprocess.Popen) -> None:
+    if proc.poll() is None:
+        os.killpg(proc.pid, signal.SIGTERM)
+        try:
+            proc.wait(timeout=60)
+        except subprocess.TimeoutExpired:
+            os.killpg(proc.pid, signal.SIGKILL)
+            proc.wait(timeout=30)
+
+
+def run_endpoint(args) -> int:
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus and rank == 0:
+        print(f"warning: --gpus {args.gpus} but WORLD_SIZE={world}", file=sys.stderr)
+    leader = local % args.tp == 0
+    logdir = os.environ.get("EIA_BENCH_LOGDIR") or os.path.join(ROOT, "gpurun_out")
+    os.makedirs(logdir, exist_ok=True)
+    log_path = os.path.join(logdir, f"bench_server_rank{rank}.log")
+    proc = pool = None
+    base = None
+    # children first: nothing in this process ever initialises the GPU
+    if leader:
+        port = _free_port()
+        base = f"http://127.0.0.1:{port}"
+        proc = start_server(args, local, port, log_path)
+        pool = ClientPool(max(1, min(args.client_procs, args.users)), base + "/v1/completions",
+                          args.model, args.output_len, args.temperature)
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        t_init = time.time()
+        if leader:
+            wait_healthy(base, proc, args.startup_timeout, log_path)
+        init_s = time.time() - t_init
+        from enterprise_inference_amd.models.catalog import resolve_name
+        from enterprise_inference_amd.models.loader import resolve_model_config
+        vocab = min(resolve_model_config(resolve_name(args.model)).vocab_size, 128000)
+        rng = random.Random(args.seed * 7919 + rank)
+
+        def one_round():
+            prompts = [[rng.randrange(1000, vocab) for _ in range(args.input_len)]
+                       for _ in range(args.users)]
+            t0 = time.time()
+            res = pool.round(prompts)
+            return res, time.time() - t0
+
+        def barrier():
+            if leader:
+                _http("POST", base + "/eia/sync")
+            if dist is not None:
+                dist.barrier()
+
+        for _ in range(args.warmup if leader else 0):
+            res, _dt = one_round()
+            bad = [r for r in res if not r[0]]
+            if bad:
+                raise RuntimeError(f"warmup request failed: {bad[0][4]}")
+        stats0 = json.loads(_http("GET", base + "/eia/stats")[1]) if leader else None
+        barrier()
+        t0 = time.time()
+        tot_tokens, ttft, tpot, e2e, failed = 0, [], [], [], []
+        for s in range(args.steps if leader else 0):
+            res, dt = one_round()
+            for ok, tt, ee, n, err in res:
+                if not ok or n != args.output_len:
+                    failed.append(err or f"got {n} tokens, expected {args.output_len}")
+                    continue
+                tot_tokens += n
+                ttft.append(tt)
+                e2e.append(ee)
+                if n > 1:
+                    tpot.append((ee - tt) / (n - 1))
+            if args.verbose:
+                ok_tt = sorted(r[1] for r in res if r[0])
+                print(f"[rank {rank}] round {s}: {sum(r[3] for r in res)} tok in {dt:.3f}s, "
+                      f"ttft p50 {1000 * statistics.median(ok_tt):.1f} ms", file=sys.stderr)
+        if leader:
+            _http("POST", base + "/eia/sync")
+        elapsed = time.time() - t0
+        if dist is not None:
+            dist.barrier()
+        local_stats = None
+        if leader:
+            stats1 = json.loads(_http("GET", base + "/eia/stats")[1])
+            busy = stats1["step_time_s"] - stats0["step_time_s"]
+            local_stats = {"tokens": tot_tokens, "elapsed": elapsed, "ttft": ttft, "tpot": tpot,
+                           "e2e": e2e, "failed": failed, "init_s": init_s,
+                           "engine_gen_tokens": stats1["num_generation_tokens"]
+                           - stats0["num_generation_tokens"],
+                           "engine_steps": stats1["num_steps"] - stats0["num_steps"],
+                           "engine_busy_s": busy, "num_blocks": stats1["num_blocks"]}
+        _report(args, dist, local_stats, rank, world, via="endpoint")
+        if failed and rank == 0:
+            print(f"error: {len(failed)} failed requests, e.g. {failed[0]}", file=sys.stderr)
+        return 1 if failed else 0
+    finally:
+        if pool is not None:
+            pool.close()
+        if proc is not None:
+            stop_server(proc)
+        if dist is not None:
+            dist.destroy_process_group()
+
+
+# --------------------------------------------------------------------------- engine mode
+
+def run_engine(args) -> int:
     import torch
     import torch.distributed as dist
 
@@ -76,9 +361,8 @@ def main() -> int:
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world != args.gpus and rank == 0:
-        print(f"warning: --gpus {args.gpus} but WORLD_SIZE={world}", file=sys.stderr)
-    if torch.cuda.is_available():
+    gpu = torch.cuda.is_available()
+    if gpu:
         torch.cuda.set_device(local)
     tp = args.tp
     if world > 1 or tp > 1:
@@ -93,22 +377,19 @@ def main() -> int:
                                   max_num_batched_tokens=args.max_num_batched_tokens,
                                   max_model_len=args.input_len + args.output_len + 64),
         parallel=ParallelConfig(tensor_parallel_size=tp),
-        device="cuda" if torch.cuda.is_available() else "cpu",
-        dtype=torch.bfloat16 if torch.cuda.is_available() else torch.float32,
-        seed=args.seed, enforce_eager=args.enforce_eager, served_model_name=model_id)
-
+        device="cuda" if gpu else "cpu", dtype=torch.bfloat16 if gpu else torch.float32,
+        seed=args.seed, enforce_eager=args.enforce_eager, served_model_name=model_id,
+        load_format="dummy")
     t_init = time.time()
-    is_driver = pstate.tp_rank() == 0
-    if tp > 1 and not is_driver:
+    if tp > 1 and pstate.tp_rank() != 0:
         # non-driver TP rank: replay the driver's plans until it shuts down
         from enterprise_inference_amd.engine.executor import setup_runner, worker_loop
         runner = setup_runner(cfg)
         ring = [None]
         dist.broadcast_object_list(ring, src=pstate.tp_ranks()[0], group=pstate.tp_cpu_group())
         worker_loop(runner, ring[0])
-        _report(args, dist, None, rank, world)
+        _report(args, dist, None, rank, world, via="engine")
         return 0
-
     from enterprise_inference_amd.engine.executor import TPExecutor, UniprocExecutor
     from enterprise_inference_amd.engine.llm_engine import LLMEngine
     if tp > 1:
@@ -141,16 +422,20 @@ def main() -> int:
                         tpots.append((m.last_token_time - m.first_token_time) / (n - 1))
         return out_tokens, ttfts, tpots, time.time() - t0
 
-    # barriers among replica drivers only (TP workers are busy replaying plans)
-    bgroup = pstate.dp_group() if tp > 1 else None
+    def sync_barrier():
+        if gpu:
+            torch.cuda.synchronize()
+        if dist.is_initialized():
+            if tp > 1:
+                dist.barrier(group=pstate.dp_group())
+            else:
+                dist.barrier()
+        if gpu:
+            torch.cuda.synchronize()
+
     for w in range(args.warmup):
         one_round(f"warm{w}")
-    _sync_and_barrier(torch, dist, bgroup)
-    prof = None
-    if os.environ.get("EIA_BENCH_CPROFILE"):      # host-side profile of the timed rounds
-        import cProfile
-        prof = cProfile.Profile()
-        prof.enable()
+    sync_barrier()
     engine.phase_times.clear()
     t0 = time.time()
     tot_tokens, all_ttft, all_tpot = 0, [], []
@@ -159,16 +444,8 @@ def main() -> int:
         tot_tokens += n
         all_ttft += tt
         all_tpot += tp_
-        if args.verbose:
-            print(f"[rank {rank}] round {s}: {n} tok in {dt:.3f}s -> {n / dt:.0f} tok/s, "
-                  f"ttft p50 {1000 * statistics.median(tt):.1f} ms", file=sys.stderr)
-    _sync_and_barrier(torch, dist, bgroup)
+    sync_barrier()
     elapsed = time.time() - t0
-    if prof is not None:
-        import pstats
-        prof.disable()
-        with open(os.environ["EIA_BENCH_CPROFILE"], "w") as f:
-            pstats.Stats(prof, stream=f).sort_stats("tottime").print_stats(45)
     if args.verbose and engine.phase_times:
         n = max(1, engine.stats.num_steps)
         print("[rank %d] host ms/step: %s" % (rank, {k: round(1e3 * v / n, 3) for k, v in
@@ -176,30 +453,17 @@ def main() -> int:
     if tp > 1:
         ex.shutdown()
     local_stats = {"tokens": tot_tokens, "elapsed": elapsed, "ttft": all_ttft, "tpot": all_tpot,
-                   "init_s": init_s, "steps": engine.stats.num_steps,
-                   "num_blocks": engine.num_blocks}
-    _report(args, dist, local_stats, rank, world)
+                   "e2e": [], "failed": [], "init_s": init_s, "num_blocks": engine.num_blocks}
+    _report(args, dist, local_stats, rank, world, via="engine")
     return 0
 
 
-def _sync_and_barrier(torch, dist, group=None):
-    if torch.cuda.is_available():
-        torch.cuda.synchronize()
-    if dist.is_initialized():
-        if group is not None:
-            dist.barrier(group=group)
-        elif int(os.environ.get("WORLD_SIZE", "1")) > 1 and dist.get_world_size() > 1:
-            from enterprise_inference_amd.parallel import state as pstate
-            if pstate.tp_size() == 1:
-                dist.barrier()
-    if torch.cuda.is_available():
-        torch.cuda.synchronize()
+# --------------------------------------------------------------------------- report
 
-
-def _report(args, dist, local_stats, rank, world):
+def _report(args, dist, local_stats, rank, world, via: str):
     from enterprise_inference_amd.models.catalog import resolve_name
 
-    if dist.is_initialized():
+    if dist is not None and dist.is_initialized():
         gathered = [None] * world
         dist.all_gather_object(gathered, local_stats)
     else:
@@ -211,19 +475,19 @@ def _report(args, dist, local_stats, rank, world):
     elapsed = max(g["elapsed"] for g in reps)
     ttft = sorted(x for g in reps for x in g["ttft"])
     tpot = sorted(x for g in reps for x in g["tpot"])
-
-    def pct(a, p):
-        return a[min(len(a) - 1, int(p / 100.0 * len(a)))] if a else None
-
+    e2e = sorted(x for g in reps for x in g["e2e"])
     value = tokens / elapsed
     model_id = resolve_name(args.model)
     base = BASELINE_TOK_S.get((model_id, args.input_len, args.output_len))
     n_replicas = max(1, world // args.tp)
     vs = None
     if base is not None:
-        # published number is per replica (1 Gaudi 3 for 8B); node figure = replicas x that
+        # published number is per replica (e.g. 1 Gaudi 3 for 8B); node = replicas x that
         vs = value / (base[0] * n_replicas)
-    total_tok_s = value * (args.input_len + args.output_len) / args.output_len
+
+    def ms(v, nd=2):
+        return None if v is None else round(1000 * v, nd)
+
     out = {
         "metric": METRIC,
         "value": round(value, 2),
@@ -243,14 +507,35 @@ def _report(args, dist, local_stats, rank, world):
                    "users_per_replica": args.users,
                    "parallelism": f"dp{n_replicas}" + (f"xtp{args.tp}" if args.tp > 1 else ""),
                    "weights": "random-init", "temperature": args.temperature},
-        "ttft_p50_ms": round(1000 * pct(ttft, 50), 2) if ttft else None,
-        "ttft_p90_ms": round(1000 * pct(ttft, 90), 2) if ttft else None,
-        "tpot_p50_ms": round(1000 * pct(tpot, 50), 3) if tpot else None,
-        "total_tok_s": round(total_tok_s, 2),
+        "measured_via": via,
+        "ttft_p50_ms": ms(_pct(ttft, 50)),
+        "ttft_p90_ms": ms(_pct(ttft, 90)),
+        "tpot_p50_ms": ms(_pct(tpot, 50), 3),
+        "tpot_p90_ms": ms(_pct(tpot, 90), 3),
+        "e2e_p50_ms": ms(_pct(e2e, 50)),
+        "total_tok_s": round(value * (args.input_len + args.output_len) / args.output_len, 2),
         "baseline_tok_s_per_replica": None if base is None else base[0],
+        "baseline_ttft_p90_ms_gaudi3": 1300.0 if base is not None and base[1] == 1 else None,
+        "failed_requests": sum(len(g["failed"]) for g in reps),
         "init_s": round(max(g["init_s"] for g in reps), 1),
     }
+    if via == "endpoint":
+        busy = max(g["engine_busy_s"] for g in reps)
+        gen = sum(g["engine_gen_tokens"] for g in reps)
+        # engine-level throughput over the engine core's busy time (no HTTP / client), and the
+        # fraction of the timed window the engine loop was stepping
+        out["engine_tok_s"] = round(gen / max(busy, 1e-9) * 1.0, 2) if n_replicas == 1 else \
+            round(sum(g["engine_gen_tokens"] / max(g["engine_busy_s"], 1e-9) for g in reps), 2)
+        out["engine_busy_frac"] = round(busy / elapsed, 3)
+        out["engine_steps"] = sum(g["engine_steps"] for g in reps)
     print(json.dumps(out), flush=True)
+
+
+def main() -> int:
+    args = parse()
+    if args.mode == "engine":
+        return run_engine(args)
+    return run_endpoint(args)
 
 
 if __name__ == "__main__":

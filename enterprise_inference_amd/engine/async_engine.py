@@ -39,6 +39,8 @@ class EngineDeadError(RuntimeError):
 class AsyncLLMEngine:
     def __init__(self, engine: LLMEngine, metrics=None, log_requests: bool = True):
         self.engine = engine
+        self.tokenizer = engine.tokenizer
+        engine.delta_outputs = True        # handlers read deltas; finals carry the full text
         self.metrics = metrics
         self.log_requests = log_requests
         self._cmds: "queue.Queue" = queue.Queue()
@@ -107,6 +109,17 @@ class AsyncLLMEngine:
         self._cmds.put(("call", fn, fut))
         self._wake.set()
         return fut
+
+    async def start(self) -> None:
+        """Interface parity with ``MPEngineClient`` (the loop thread is already running)."""
+
+    async def wait_ready(self, timeout=None) -> None:
+        self.check_health()
+
+    async def run_op(self, op: str):
+        """Named engine operation between steps: profile_start/stop, sync, stats."""
+        from .core_proc import _run_op
+        return await asyncio.wrap_future(self.call_in_engine_thread(lambda: _run_op(self.engine, op)))
 
     def shutdown(self) -> None:
         self._stop = True

@@ -156,7 +156,35 @@ class TPExecutor:
         self.procs = []
 
 
+class FakeExecutor:
+    """Test double for host-path benchmarking (``EIA_FAKE_STEP_MS=<ms>``): no model; every step
+    sleeps the given time (a stand-in for the GPU) and samples uniform random tokens.  With it
+    the API server / engine core / SSE path can be load-tested on a CPU box at the real step
+    cadence (tests/test_serving_hostpath_cpu.py, scripts/hostpath_bench.sh)."""
+
+    supports_overlap = False
+
+    def __init__(self, cfg: EngineConfig, step_ms: float):
+        import random as _random
+        self.step_s = step_ms / 1000.0
+        self.num_blocks = cfg.cache.num_gpu_blocks or 16384
+        self.vocab = cfg.model.vocab_size
+        self._rng = _random.Random(cfg.seed)
+
+    def execute(self, bm, sched) -> StepOutput:
+        import time as _time
+        n = len(sched.decodes) + sum(1 for p in sched.prefills if p.samples)
+        _time.sleep(self.step_s)
+        return StepOutput([self._rng.randrange(3, self.vocab) for _ in range(n)], None)
+
+    def shutdown(self) -> None:
+        pass
+
+
 def make_executor(cfg: EngineConfig):
+    fake = os.environ.get("EIA_FAKE_STEP_MS")
+    if fake:
+        return FakeExecutor(cfg, float(fake))
     if cfg.parallel.tensor_parallel_size * cfg.parallel.pipeline_parallel_size > 1:
         if dist.is_initialized():
             # launched under torchrun: this process is TP rank 0 of its group

@@ -24,7 +24,7 @@ from .sequence import FINISH_REASON, SeqStatus, Sequence
 logger = logging.getLogger(__name__)
 
 
-@dataclasses.dataclass
+@dataclasses.dataclass(slots=True)
 class CompletionOutput:
     index: int
     text: str
@@ -41,7 +41,7 @@ class CompletionOutput:
         return self.finish_reason is not None
 
 
-@dataclasses.dataclass
+@dataclasses.dataclass(slots=True)
 class RequestMetrics:
     arrival_time: float
     first_scheduled_time: Optional[float] = None
@@ -54,7 +54,7 @@ class RequestMetrics:
         return None if self.first_token_time is None else self.first_token_time - self.arrival_time
 
 
-@dataclasses.dataclass
+@dataclasses.dataclass(slots=True)
 class RequestOutput:
     request_id: str
     prompt: Optional[str]
@@ -125,6 +125,10 @@ class LLMEngine:
             getattr(executor, "supports_overlap", False)
         self._pending = None        # StepHandle of the launched, not yet processed step
         self.phase_times: Dict[str, float] = {}   # host seconds per step phase (overlap path)
+        # Servers consume only the per-step deltas until a request finishes: with
+        # ``delta_outputs`` the full text / token list / logprobs of a request are materialised
+        # once, in its final RequestOutput, instead of being copied every step (O(n^2)).
+        self.delta_outputs = False
 
     # ------------------------------------------------------------------ requests
     def add_request(self, request_id: str, prompt: Optional[str] = None,
@@ -348,14 +352,17 @@ class LLMEngine:
                 seqs = sorted(seqs, key=lambda s: s.cumulative_logprob, reverse=True)[:r.params.n]
             elif r.params.best_of > r.params.n:
                 continue     # best_of is only returned at the end
+            full = finished or not self.delta_outputs
+            want_lp = full and r.params.logprobs is not None
             comps = []
             for i, s in enumerate(seqs):
                 d = deltas.get(s.seq_id, ("", [], None))
                 comps.append(CompletionOutput(
                     index=i if r.params.best_of > r.params.n else s.index,
-                    text=s.output_text, token_ids=list(s.output_token_ids),
-                    cumulative_logprob=s.cumulative_logprob if r.params.logprobs is not None else None,
-                    logprobs=s.output_logprobs if r.params.logprobs is not None else None,
+                    text=s.output_text if full else "",
+                    token_ids=list(s.output_token_ids) if full else [],
+                    cumulative_logprob=s.cumulative_logprob if want_lp else None,
+                    logprobs=s.output_logprobs if want_lp else None,
                     finish_reason=FINISH_REASON.get(s.status), stop_reason=s.stop_reason,
                     new_text=d[0], new_token_ids=d[1], new_logprobs=d[2]))
             s0 = r.seqs[0]

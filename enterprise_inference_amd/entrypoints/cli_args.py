@@ -93,6 +93,10 @@ def make_parser(description: str = "MI355X OpenAI-compatible LLM server") -> arg
     a("--kv-cache-dtype", default="auto")
     a("--quantization", "-q", default=None)
     a("--max-seq-len-to-capture", type=int, default=None)
+    a("--engine-mode", default=os.environ.get("EIA_ENGINE_MODE", "process"),
+      choices=["process", "thread"],
+      help="process: scheduler + GPU loop in an engine-core process (default); "
+           "thread: in this process")
     return p
 
 
@@ -135,7 +139,9 @@ def engine_config_from_args(args: argparse.Namespace):
     mcfg = resolve_model_config(cfg_id)
     dev = args.device
     if dev in ("auto", "rocm"):
-        dev = "cuda" if torch.cuda.is_available() else "cpu"
+        # device_count() does not initialise HIP: the API process stays GPU-free so the
+        # engine-core / TP worker processes can be started after this point
+        dev = "cuda" if torch.cuda.device_count() > 0 else "cpu"
     dtype = parse_dtype(args.dtype) if dev == "cuda" else torch.float32
     max_len = args.max_model_len or min(mcfg.max_position_embeddings, 32768)
     mbt = args.max_num_batched_tokens

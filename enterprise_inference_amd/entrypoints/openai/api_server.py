@@ -39,18 +39,32 @@ def _error(msg: str, code: int, kind: str) -> JSONResponse:
                         status_code=code)
 
 
+class _BearerAuth:
+    """``Authorization: Bearer <api_key>`` on ``/v1/*`` (vLLM ``--api-key`` semantics)."""
+
+    def __init__(self, app, api_key: str):
+        self.app = app
+        self.expected = f"Bearer {api_key}".encode()
+
+    async def __call__(self, scope, receive, send):
+        if scope["type"] == "http" and scope["path"].startswith("/v1"):
+            auth = dict(scope.get("headers") or []).get(b"authorization")
+            if auth != self.expected:
+                await _error("Unauthorized", 401, "AuthenticationError")(scope, receive, send)
+                return
+        await self.app(scope, receive, send)
+
+
 def build_app(ctx: ServingContext, metrics=None, embedder=None, api_key: Optional[str] = None,
-              served_model_name: Optional[str] = None) -> FastAPI:
+              served_model_name: Optional[str] = None, wait_ready: bool = False) -> FastAPI:
     """FastAPI app over a ServingContext (LLM) and/or an embedding engine (TEI-style)."""
     app = FastAPI(title="enterprise-inference-amd", version=__version__)
     model_name = served_model_name or (ctx.model if ctx else embedder.model_name)
 
-    @app.middleware("http")
-    async def auth(request: Request, call_next):
-        if api_key and request.url.path.startswith("/v1"):
-            if request.headers.get("Authorization") != f"Bearer {api_key}":
-                return _error("Unauthorized", 401, "AuthenticationError")
-        return await call_next(request)
+    if api_key:
+        # Pure ASGI middleware (Starlette's BaseHTTPMiddleware re-streams every SSE chunk
+        # through anyio memory streams: ~25 us/chunk of API-process CPU at 13k chunks/s).
+        app.add_middleware(_BearerAuth, api_key=api_key)
 
     @app.exception_handler(RequestValidationError)
     async def validation_error(_, exc):
@@ -75,6 +89,7 @@ def build_app(ctx: ServingContext, metrics=None, embedder=None, api_key: Optiona
             if eng.dead is not None:
                 return Response(status_code=500)
             if not eng.healthy:
+                # still loading / capturing graphs, or a step exceeded the watchdog
                 return Response(status_code=503)
         return Response(status_code=200)
 
@@ -129,23 +144,35 @@ def build_app(ctx: ServingContext, metrics=None, embedder=None, api_key: Optiona
         async def detokenize(body: dict):
             return {"prompt": ctx.tokenizer.decode(body.get("tokens", []))}
 
+        @app.post("/eia/sync")
+        async def engine_sync():
+            """Barrier with the device: returns once the engine drained its GPU queue
+            (bench.py brackets its timed region with it)."""
+            await ctx.engine.run_op("sync")
+            return {"ok": True}
+
+        @app.get("/eia/stats")
+        async def engine_stats():
+            return await ctx.engine.run_op("stats")
+
         from ...utils.profiling import profiler_dir
         if profiler_dir():
             # vLLM-compatible profiler control (only with EIA/VLLM_TORCH_PROFILER_DIR set)
-            import asyncio as _asyncio
-
             @app.post("/start_profile")
             async def start_profile():
-                eng = ctx.engine
-                await _asyncio.wrap_future(eng.call_in_engine_thread(eng.engine.profiler.start))
+                await ctx.engine.run_op("profile_start")
                 return Response(status_code=200)
 
             @app.post("/stop_profile")
             async def stop_profile():
-                eng = ctx.engine
-                path = await _asyncio.wrap_future(
-                    eng.call_in_engine_thread(eng.engine.profiler.stop))
-                return JSONResponse({"trace": path})
+                return JSONResponse({"trace": await ctx.engine.run_op("profile_stop")})
+
+        async def _start_engine():
+            await ctx.engine.start()
+            if wait_ready:      # tests: serve only once the engine core reported ready
+                await ctx.engine.wait_ready()
+
+        app.router.on_startup.append(_start_engine)
 
     if embedder is not None:
         from ..tei.server import register_openai_embeddings
@@ -159,34 +186,48 @@ def build_app(ctx: ServingContext, metrics=None, embedder=None, api_key: Optiona
     return app
 
 
-def build_from_args(args):
-    """Engine + app for parsed CLI args (used by ``main`` and the in-process tests)."""
+def build_from_args(args, engine_mode: Optional[str] = None, wait_ready: bool = False):
+    """Engine + app for parsed CLI args (used by ``main`` and the in-process tests).
+
+    ``engine_mode``: ``process`` (default for the server: the step loop runs in an
+    engine-core process, engine/core_proc.py, and this process never touches the GPU) or
+    ``thread`` (step loop on a thread of this process; tests, torchrun-launched TP ranks)."""
     from ...engine.llm_engine import LLMEngine
     from ...metrics import EngineMetrics
 
     cfg = engine_config_from_args(args)
+    mode = engine_mode or getattr(args, "engine_mode", None) or \
+        os.environ.get("EIA_ENGINE_MODE", "process")
     if cfg.model.is_encoder:
         from ..tei.server import EmbeddingEngine
         emb = EmbeddingEngine(cfg)
         metrics = EngineMetrics(cfg.served_model_name)
         return build_app(None, metrics, embedder=emb, api_key=args.api_key,
                          served_model_name=cfg.served_model_name), None
-    if cfg.parallel.world_size > 1 or os.environ.get("WORLD_SIZE"):
-        from ...parallel import state as pstate
+    metrics = EngineMetrics(cfg.served_model_name)
+    if os.environ.get("WORLD_SIZE"):
+        mode = "thread"          # torchrun-launched TP rank 0: this process is the driver
+    if mode == "process":
+        from ...engine.core_proc import MPEngineClient
+        env = {k: v for k, v in os.environ.items()
+               if k not in ("RANK", "LOCAL_RANK", "WORLD_SIZE", "MASTER_ADDR", "MASTER_PORT")}
+        aengine = MPEngineClient(cfg, metrics, log_requests=not args.disable_log_requests,
+                                 env=env)
+    else:
         if os.environ.get("WORLD_SIZE"):
+            from ...parallel import state as pstate
             pstate.init_distributed(cfg.parallel.tensor_parallel_size,
                                     enable_expert_parallel=cfg.parallel.enable_expert_parallel,
                                     pp_size=cfg.parallel.pipeline_parallel_size)
-    engine = LLMEngine(cfg)
-    metrics = EngineMetrics(cfg.served_model_name)
-    aengine = AsyncLLMEngine(engine, metrics, log_requests=not args.disable_log_requests)
+        engine = LLMEngine(cfg)
+        aengine = AsyncLLMEngine(engine, metrics, log_requests=not args.disable_log_requests)
     gen_defaults = dict(args.override_generation_config or {})
     ctx = ServingContext(aengine, cfg.served_model_name, cfg.scheduler.max_model_len,
                          chat_template=resolve_chat_template(args.chat_template),
                          tool_parser=args.tool_call_parser,
                          enable_auto_tool_choice=args.enable_auto_tool_choice,
                          generation_defaults=gen_defaults)
-    return build_app(ctx, metrics, api_key=args.api_key), aengine
+    return build_app(ctx, metrics, api_key=args.api_key, wait_ready=wait_ready), aengine
 
 
 def main(argv=None) -> int:
@@ -198,6 +239,18 @@ def main(argv=None) -> int:
     app, aengine = build_from_args(args)
     logger.info("serving %s on %s:%d", (args.served_model_name or [args.model])[0], args.host,
                 args.port)
+    if os.environ.get("EIA_API_CPROFILE"):      # host-side profile of the API process
+        import cProfile
+        import pstats
+        prof = cProfile.Profile()
+        prof.enable()
+
+        async def _dump_profile():
+            prof.disable()
+            with open(os.environ["EIA_API_CPROFILE"], "w") as f:
+                pstats.Stats(prof, stream=f).sort_stats("tottime").print_stats(60)
+
+        app.router.on_shutdown.append(_dump_profile)
     try:
         uvicorn.run(app, host=args.host, port=args.port, log_level=args.uvicorn_log_level,
                     timeout_keep_alive=5)

@@ -71,19 +71,30 @@ class EngineMetrics:
     def _l(self, m):
         return m.labels(model_name=self.model_name)
 
+    @staticmethod
+    def engine_snapshot(engine, step_s: float) -> tuple:
+        """Cumulative counters + gauges of an engine after a step (what ``observe_stats`` takes;
+        the engine-core process ships this tuple to the API process every step)."""
+        st, sch = engine.stats, engine.scheduler
+        swapped = getattr(sch, "num_swapped", lambda: 0)()
+        return (st.num_prompt_tokens, st.num_generation_tokens, st.num_preemptions,
+                len(sch.running), len(sch.waiting), swapped, engine.kv_cache_usage(),
+                engine.cpu_cache_usage() if hasattr(engine, "cpu_cache_usage") else 0.0, step_s)
+
     def observe_step(self, engine, step_s: float) -> None:
-        st = engine.stats
-        self._l(self.prompt_tokens).inc(max(0, st.num_prompt_tokens - self._last_prompt))
-        self._l(self.gen_tokens).inc(max(0, st.num_generation_tokens - self._last_gen))
-        self._l(self.preemptions).inc(max(0, st.num_preemptions - self._last_preempt))
-        self._last_prompt, self._last_gen = st.num_prompt_tokens, st.num_generation_tokens
-        self._last_preempt = st.num_preemptions
-        sch = engine.scheduler
-        self._l(self.running).set(len(sch.running))
-        self._l(self.waiting).set(len(sch.waiting))
-        self._l(self.swapped).set(0)
-        self._l(self.gpu_cache).set(engine.kv_cache_usage())
-        self._l(self.cpu_cache).set(0.0)
+        self.observe_stats(self.engine_snapshot(engine, step_s))
+
+    def observe_stats(self, snap: tuple) -> None:
+        prompt, gen, preempt, running, waiting, swapped, gpu_kv, cpu_kv, step_s = snap
+        self._l(self.prompt_tokens).inc(max(0, prompt - self._last_prompt))
+        self._l(self.gen_tokens).inc(max(0, gen - self._last_gen))
+        self._l(self.preemptions).inc(max(0, preempt - self._last_preempt))
+        self._last_prompt, self._last_gen, self._last_preempt = prompt, gen, preempt
+        self._l(self.running).set(running)
+        self._l(self.waiting).set(waiting)
+        self._l(self.swapped).set(swapped)
+        self._l(self.gpu_cache).set(gpu_kv)
+        self._l(self.cpu_cache).set(cpu_kv)
         self._l(self.step_time).observe(step_s)
 
     def observe_finished(self, out) -> None:

@@ -30,7 +30,7 @@ def server(tmp_path_factory):
                        "/workspace/vllm/examples/tool_chat_template_llama3.1_json.jinja",
                        "--gpu-memory-util", "0.5", "--num_scheduler_steps", "1",
                        "--use-padding-aware-scheduling", "--disable-log-requests"])
-    app, aeng = build_from_args(args)
+    app, aeng = build_from_args(args, wait_ready=True)
     with TestClient(app) as c:
         yield c
     aeng.shutdown()
@@ -147,3 +147,31 @@ def test_tokenize_roundtrip(server):
     t = server.post("/tokenize", json={"prompt": "abc"}).json()
     assert t["count"] == len(t["tokens"])
     assert "abc" in server.post("/detokenize", json={"tokens": t["tokens"]}).json()["prompt"]
+
+
+@pytest.mark.parametrize("text,finish,stop", [("hi", None, None), ('a "q" \\ é\n日本', "stop", None),
+                                              ("", "length", None), ("x", "stop", 128009),
+                                              ("y", "stop", "</s>")])
+def test_fast_sse_chunks_match_pydantic(text, finish, stop):
+    """The hand-framed SSE hot path is JSON-equal to the pydantic models it replaces."""
+    from enterprise_inference_amd.entrypoints.openai import serving as sv
+    from enterprise_inference_amd.entrypoints.openai.protocol import (
+        ChatCompletionResponseStreamChoice, ChatCompletionStreamResponse, CompletionStreamChoice,
+        CompletionStreamResponse, DeltaMessage)
+
+    def body(frame):
+        assert frame.startswith("data: ") and frame.endswith("\n\n")
+        return json.loads(frame[6:-2])
+
+    ref = sv._sse(CompletionStreamResponse(
+        id="cmpl-1", created=7, model="m/x", choices=[CompletionStreamChoice(
+            index=3, text=text, finish_reason=finish, stop_reason=stop)]))
+    got = sv.fast_completion_chunk(sv.completion_chunk_head("cmpl-1", 7, "m/x"), 3, text,
+                                   finish, stop)
+    assert body(got) == body(ref)
+    ref = sv._sse(ChatCompletionStreamResponse(
+        id="chatcmpl-1", created=7, model="m/x", choices=[ChatCompletionResponseStreamChoice(
+            index=0, delta=DeltaMessage(content=text or None, tool_calls=[]),
+            finish_reason=finish, stop_reason=stop)]))
+    got = sv.fast_chat_chunk(sv.chat_chunk_head("chatcmpl-1", 7, "m/x"), 0, text, finish, stop)
+    assert body(got) == body(ref)

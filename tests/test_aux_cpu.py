@@ -12,7 +12,7 @@ from fastapi.testclient import TestClient
 from enterprise_inference_amd.entrypoints.cli_args import parse_args
 
 
-def _build(tmp_path, extra=()):
+def _build(tmp_path, extra=(), mode=None):
     from enterprise_inference_amd.entrypoints.openai.api_server import build_from_args
     from enterprise_inference_amd.models import catalog
     d = tmp_path / "tiny"
@@ -22,7 +22,7 @@ def _build(tmp_path, extra=()):
                        "--load-format", "dummy", "--max-model-len", "512", "--max-num-seqs", "16",
                        "--max-num-batched-tokens", "256", "--block-size", "16",
                        "--disable-log-requests", *extra])
-    return build_from_args(args)
+    return build_from_args(args, engine_mode=mode, wait_ready=True)
 
 
 def test_profiler_start_stop(tmp_path, monkeypatch):
@@ -54,7 +54,7 @@ def test_profiler_routes_absent_without_env(tmp_path, monkeypatch):
 def test_invariant_checker_runs_and_fires(tmp_path, monkeypatch):
     from enterprise_inference_amd.engine.sampling_params import SamplingParams
     monkeypatch.setenv("EIA_CHECK_INVARIANTS", "1")
-    app, aeng = _build(tmp_path)
+    app, aeng = _build(tmp_path, mode="thread")
     try:
         eng = aeng.engine
         aeng.shutdown()          # drive the engine synchronously from here
