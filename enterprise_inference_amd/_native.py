@@ -97,10 +97,13 @@ def kernels() -> ctypes.CDLL:
         if not os.path.exists(_KERNELS_SO):
             _build_kernels()
         lib = ctypes.CDLL(_KERNELS_SO, mode=ctypes.RTLD_GLOBAL)
+        missing = [n for n in _SIGNATURES if not hasattr(lib, n)]
+        if missing:
+            # a stale build: fail here, not at the first call of the missing kernel
+            raise RuntimeError(f"{_KERNELS_SO} lacks {missing}; rebuild it "
+                               "(python -c 'import __graft_entry__ as g; g.build()')")
         for name, argtypes in _SIGNATURES.items():
-            fn = getattr(lib, name, None)
-            if fn is None:
-                continue
+            fn = getattr(lib, name)
             fn.argtypes = argtypes
             fn.restype = ctypes.c_int
         _kernels = lib

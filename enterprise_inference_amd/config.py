@@ -242,6 +242,10 @@ class EngineConfig:
     tokenizer: Optional[str] = None
     seed: int = 0
     enforce_eager: bool = False
+    skip_warmup: bool = False                 # VLLM_SKIP_WARMUP: no warm-up runs before capture
+    # servers with a real checkpoint: a missing / broken tokenizer is an error (no byte-level
+    # stand-in); programmatic token-id-only use may leave it off
+    strict_tokenizer: bool = False
     load_format: str = "auto"                 # auto | safetensors | dummy
     trust_remote_code: bool = False
     engine_iteration_timeout_s: float = 120.0  # VLLM_ENGINE_ITERATION_TIMEOUT_S

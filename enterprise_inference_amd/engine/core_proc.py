@@ -247,9 +247,9 @@ class MPEngineClient:
         self.cfg = cfg
         self.metrics = metrics
         m = cfg.model
-        self.tokenizer = tokenizer or get_tokenizer(cfg.tokenizer or cfg.model_path,
-                                                    m.vocab_size, m.eos_token_id,
-                                                    m.bos_token_id, cfg.trust_remote_code)
+        self.tokenizer = tokenizer or get_tokenizer(
+            cfg.tokenizer or cfg.model_path, m.vocab_size, m.eos_token_id, m.bos_token_id,
+            cfg.trust_remote_code, allow_byte_fallback=not cfg.strict_tokenizer)
         self.timeout_s = float(os.environ.get("VLLM_ENGINE_ITERATION_TIMEOUT_S",
                                               cfg.engine_iteration_timeout_s))
         self.dead: Optional[BaseException] = None

@@ -100,9 +100,9 @@ class LLMEngine:
         self.num_blocks = executor.num_blocks
         self.scheduler = Scheduler(cfg.scheduler, cfg.cache, self.num_blocks)
         m = cfg.model
-        self.tokenizer = tokenizer or get_tokenizer(cfg.tokenizer or cfg.model_path, m.vocab_size,
-                                                    m.eos_token_id, m.bos_token_id,
-                                                    cfg.trust_remote_code)
+        self.tokenizer = tokenizer or get_tokenizer(
+            cfg.tokenizer or cfg.model_path, m.vocab_size, m.eos_token_id, m.bos_token_id,
+            cfg.trust_remote_code, allow_byte_fallback=not cfg.strict_tokenizer)
         eos = m.eos_token_id
         eos_ids = set(eos if isinstance(eos, list) else ([eos] if eos is not None else []))
         tok_eos = getattr(self.tokenizer, "eos_token_id", None)

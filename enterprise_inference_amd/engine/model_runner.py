@@ -616,10 +616,11 @@ class ModelRunner:
         stream = torch.cuda.Stream()
         stream.wait_stream(torch.cuda.current_stream())
         with torch.cuda.stream(stream):
-            for Bp in sorted(buckets, reverse=True):
+            for bi, Bp in enumerate(sorted(buckets, reverse=True)):
                 P = self._decode_partitions(Bp, self.cfg.scheduler.max_model_len)
                 self.graph_P[Bp] = P          # upper bound; the step's P is read on device
-                for _ in range(2):       # warm-up (hipBLASLt heuristics, allocator)
+                # warm-up (hipBLASLt heuristics, allocator); VLLM_SKIP_WARMUP: first bucket only
+                for _ in range((1 if bi == 0 else 0) if self.cfg.skip_warmup else 2):
                     self._graph_forward(Bp, P)
                 g = torch.cuda.CUDAGraph()
                 with torch.cuda.graph(g, pool=self.graph_pool, stream=stream):

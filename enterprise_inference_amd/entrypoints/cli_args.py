@@ -83,6 +83,7 @@ def make_parser(description: str = "MI355X OpenAI-compatible LLM server") -> arg
     a("--tokenizer", default=None)
     a("--load-format", default="auto", choices=["auto", "safetensors", "pt", "dummy"])
     a("--download-dir", default=None)
+    a("--revision", default=None)
     a("--seed", type=int, default=0)
     a("--swap-space", type=float, default=4)
     a("--api-key", default=os.environ.get("VLLM_API_KEY"))
@@ -111,18 +112,16 @@ def parse_args(argv: Optional[List[str]] = None, parser=None) -> argparse.Namesp
     return args
 
 
-def resolve_model_source(model: str, download_dir: Optional[str] = None):
-    """(model_path or None, config id). Local dirs (e.g. HF_HOME=/data snapshots) load weights."""
-    if os.path.isdir(model) and os.path.exists(os.path.join(model, "config.json")):
-        return model, model
-    for root in filter(None, (download_dir, os.environ.get("HF_HOME"))):
-        snap = os.path.join(root, "hub", "models--" + model.replace("/", "--"), "snapshots")
-        if os.path.isdir(snap):
-            for d in sorted(os.listdir(snap)):
-                p = os.path.join(snap, d)
-                if os.path.exists(os.path.join(p, "config.json")):
-                    return p, p
-    return None, model
+def resolve_model_source(model: str, download_dir: Optional[str] = None,
+                         load_format: str = "auto", revision: Optional[str] = None):
+    """(model_path or None, config id).  A local dir or HF-cache snapshot is used as is; an
+    HF id that is not cached is downloaded into --download-dir / HF_HOME (the reference's
+    /data PVC).  Raises when real weights are wanted but cannot be obtained; ``None`` is
+    returned only for ``--load-format dummy`` (random weights from the catalog preset)."""
+    from ..models.hub import ensure_local_model
+
+    path = ensure_local_model(model, load_format, download_dir, revision)
+    return path, (path or model)
 
 
 def engine_config_from_args(args: argparse.Namespace):
@@ -135,7 +134,8 @@ def engine_config_from_args(args: argparse.Namespace):
     for k in os.environ:
         if k.startswith(IGNORED_ENV):
             logger.debug("ignoring HPU/Xeon-only env %s", k)
-    path, cfg_id = resolve_model_source(args.model, args.download_dir)
+    path, cfg_id = resolve_model_source(args.model, args.download_dir, args.load_format,
+                                        args.revision)
     mcfg = resolve_model_config(cfg_id)
     dev = args.device
     if dev in ("auto", "rocm"):
@@ -169,11 +169,15 @@ def engine_config_from_args(args: argparse.Namespace):
                          distributed_executor_backend=args.distributed_executor_backend,
                          disable_custom_all_reduce=args.disable_custom_all_reduce)
     served = (args.served_model_name or [args.model])[0]
-    enforce_eager = args.enforce_eager or _truthy(os.environ.get("VLLM_SKIP_WARMUP", "false"))
+    # VLLM_SKIP_WARMUP only shortens start-up (no warm-up forwards before each HIP-graph
+    # capture); it never turns graphs off -- that is --enforce-eager's job
+    enforce_eager = args.enforce_eager
     return EngineConfig(model=mcfg, cache=cache, scheduler=sched, parallel=par, dtype=dtype,
                         device=dev, model_path=path if args.load_format != "dummy" else None,
                         served_model_name=served, tokenizer=args.tokenizer or path, seed=args.seed,
                         enforce_eager=enforce_eager, load_format=args.load_format,
+                        skip_warmup=_truthy(os.environ.get("VLLM_SKIP_WARMUP", "false")),
+                        strict_tokenizer=args.load_format != "dummy",
                         trust_remote_code=args.trust_remote_code,
                         engine_iteration_timeout_s=float(
                             os.environ.get("VLLM_ENGINE_ITERATION_TIMEOUT_S", 120)))

@@ -56,7 +56,8 @@ class EmbeddingEngine:
         m = cfg.model
         self.model_name = cfg.served_model_name or m.name
         self.tokenizer = get_tokenizer(cfg.tokenizer or cfg.model_path, m.vocab_size,
-                                       m.eos_token_id, m.bos_token_id, cfg.trust_remote_code)
+                                       m.eos_token_id, m.bos_token_id, cfg.trust_remote_code,
+                                       allow_byte_fallback=not cfg.strict_tokenizer)
         self.max_len = m.max_position_embeddings - m.position_offset
         self.max_batch_tokens = max_batch_tokens
         self.auto_truncate = auto_truncate
@@ -269,15 +270,23 @@ def main(argv=None) -> int:
                     default=int(os.environ.get("MAX_BATCH_TOKENS", 16384)))
     ap.add_argument("--dtype", default=os.environ.get("DTYPE", "bfloat16"))
     ap.add_argument("--pooling", default=os.environ.get("POOLING", "cls"))
+    ap.add_argument("--load-format", default=os.environ.get("LOAD_FORMAT", "auto"),
+                    choices=["auto", "safetensors", "pt", "dummy"],
+                    help="dummy: random weights (benchmarks); otherwise download / load")
+    ap.add_argument("--huggingface-hub-cache", default=os.environ.get("HF_HUB_CACHE"))
     args, unknown = ap.parse_known_args(normalise_argv(list(sys.argv[1:] if argv is None else argv)))
     if unknown:
         logger.warning("ignoring unsupported arguments: %s", unknown)
-    path, cfg_id = resolve_model_source(args.model_id, os.environ.get("HF_HUB_CACHE"))
+    path, cfg_id = resolve_model_source(args.model_id, args.huggingface_hub_cache,
+                                        args.load_format)
     mcfg = resolve_model_config(cfg_id)
     gpu = torch.cuda.is_available()
     cfg = EngineConfig(model=mcfg, cache=CacheConfig(), device="cuda" if gpu else "cpu",
-                       dtype=torch.bfloat16 if gpu else torch.float32, model_path=path,
-                       served_model_name=args.model_id, tokenizer=path)
+                       dtype=torch.bfloat16 if gpu else torch.float32,
+                       model_path=path if args.load_format != "dummy" else None,
+                       served_model_name=args.model_id, tokenizer=path,
+                       load_format=args.load_format,
+                       strict_tokenizer=args.load_format != "dummy")
     emb = EmbeddingEngine(cfg, args.max_batch_tokens, args.auto_truncate)
     if hasattr(emb.model, "pooling"):
         emb.model.pooling = args.pooling

@@ -3,8 +3,9 @@ or deterministic random init (``--load-format dummy``; the north-star benchmark
 mode, no checkpoints are available offline).
 
 Reference behaviour: weights are downloaded into the /data PVC with HF_HOME=/data
-(core/helm-charts/vllm/templates/configmap.yaml:20); here a local directory is
-read directly and nothing is fetched.
+(core/helm-charts/vllm/templates/configmap.yaml:20); the download itself is
+models/hub.py (run by the CLI before the engine starts), this module reads the
+local snapshot and fails loudly when it holds no weights.
 """
 
 from __future__ import annotations
@@ -14,12 +15,16 @@ import json
 import os
 from typing import Iterator, Optional, Tuple
 
+import logging
+
 import torch
 import torch.nn as nn
 
 from ..config import EngineConfig, ModelConfig
 from . import get_model_class
 from .layers import init_random_
+
+logger = logging.getLogger(__name__)
 
 
 def iter_safetensors(path: str) -> Iterator[Tuple[str, torch.Tensor]]:
@@ -50,15 +55,19 @@ def build_model(cfg: EngineConfig, device: torch.device) -> nn.Module:
     model.eval()
     fmt = cfg.load_format
     if cfg.model_path is None or fmt == "dummy":
+        logger.info("random-init weights (load_format=%s, no checkpoint)", fmt)
         init_random_(model, seed=cfg.seed)
         post = getattr(model, "post_load", None)
         if post:
             post()
         return model
-    if glob.glob(os.path.join(cfg.model_path, "*.safetensors")):
+    if glob.glob(os.path.join(cfg.model_path, "*.safetensors")) and fmt != "pt":
         it = iter_safetensors(cfg.model_path)
-    else:
+    elif glob.glob(os.path.join(cfg.model_path, "*.bin")):
         it = iter_torch_bins(cfg.model_path)
+    else:
+        raise FileNotFoundError(f"no *.safetensors or *.bin weights under {cfg.model_path} "
+                                "(use --load-format dummy for random weights)")
     with torch.no_grad():
         model.load_weights(it)
     post = getattr(model, "post_load", None)

@@ -1,10 +1,12 @@
 """Tokenizer loading.
 
 Uses a local HF tokenizer directory when one is given (``--tokenizer`` or the
-model dir, the reference mounts it under HF_HOME=/data).  Without network and
-without a local tokenizer the server falls back to a byte-level tokenizer so the
-full serving path (chat templates, streaming detokenisation, stop strings) still
-works on random-init weights -- the north-star benchmark setting.
+model dir, the reference mounts it under HF_HOME=/data).  The byte-level
+tokenizer below is used only when the caller allows it -- random-init weights
+(``--load-format dummy``, the north-star benchmark setting) or a bare
+``ModelConfig`` in tests -- so the full serving path (chat templates, streaming
+detokenisation, stop strings) still works without a checkpoint.  A real
+checkpoint without a loadable tokenizer is an error.
 """
 
 from __future__ import annotations
@@ -86,8 +88,9 @@ class ByteTokenizer:
 
 def get_tokenizer(path: Optional[str], vocab_size: int = 32000, eos_token_id=None,
                   bos_token_id=None, trust_remote_code: bool = False,
-                  chat_template: Optional[str] = None):
+                  chat_template: Optional[str] = None, allow_byte_fallback: bool = True):
     tok = None
+    err = None
     if path and os.path.isdir(path) and any(
             os.path.exists(os.path.join(path, f))
             for f in ("tokenizer.json", "tokenizer.model", "tokenizer_config.json", "vocab.txt")):
@@ -96,8 +99,12 @@ def get_tokenizer(path: Optional[str], vocab_size: int = 32000, eos_token_id=Non
 
             tok = AutoTokenizer.from_pretrained(path, local_files_only=True,
                                                 trust_remote_code=trust_remote_code)
-        except Exception:   # noqa: BLE001 - fall back to byte level
-            tok = None
+        except Exception as e:   # noqa: BLE001 - byte level only if allowed
+            tok, err = None, e
+    if tok is None and not allow_byte_fallback:
+        raise RuntimeError(f"no loadable tokenizer under {path!r}"
+                           + (f": {err!r}" if err else "") +
+                           " (pass --tokenizer, or --load-format dummy for random weights)")
     if tok is None:
         eos = eos_token_id[0] if isinstance(eos_token_id, list) else eos_token_id
         tok = ByteTokenizer(vocab_size, eos, bos_token_id, name=path or "byte-level")
