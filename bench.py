@@ -385,16 +385,17 @@ def run_engine(args) -> int:
         # non-driver TP rank: replay the driver's plans until it shuts down
         from enterprise_inference_amd.engine.executor import setup_runner, worker_loop
         runner = setup_runner(cfg)
-        ring = [None]
+        ring = [None, None]
         dist.broadcast_object_list(ring, src=pstate.tp_ranks()[0], group=pstate.tp_cpu_group())
-        worker_loop(runner, ring[0])
+        worker_loop(runner, ring[0], ring[1])
         _report(args, dist, None, rank, world, via="engine")
         return 0
     from enterprise_inference_amd.engine.executor import TPExecutor, UniprocExecutor
     from enterprise_inference_amd.engine.llm_engine import LLMEngine
     if tp > 1:
         ex = TPExecutor(cfg, spawn=False)
-        dist.broadcast_object_list([ex.ring_name], src=rank, group=pstate.tp_cpu_group())
+        dist.broadcast_object_list([ex.ring_name, os.getpid()], src=rank,
+                                   group=pstate.tp_cpu_group())
     else:
         ex = UniprocExecutor(cfg)
     engine = LLMEngine(cfg, executor=ex)

@@ -84,13 +84,18 @@ EIA_DEV void block_barrier(const ArPeers& P, int rank, int world, uint32_t ep, A
   __syncthreads();
 }
 
-EIA_DEV void sum_peers(const ArPeers& P, int W, int rank, long off, long i, float (&acc)[8]) {
-#pragma unroll 1
-  for (int p = 0; p < W; ++p) {
-    const int src = (rank + p) % W;   // start at a different peer on every rank (spread links)
-    const bf16x8 v = reinterpret_cast<const bf16x8*>(P.data[src] + off)[i];
+// All W loads are issued before the first add (every link busy at once) and summed in rank
+// order 0..W-1 on every rank, so all ranks produce bit-identical sums: replicated TP
+// activations (the residual stream) never drift apart between ranks.
+template <int W>
+EIA_DEV void sum_peers(const ArPeers& P, long off, long i, float (&acc)[8]) {
+  bf16x8 v[W];
 #pragma unroll
-    for (int j = 0; j < 8; ++j) acc[j] += bf2f(v[j]);
+  for (int p = 0; p < W; ++p) v[p] = reinterpret_cast<const bf16x8*>(P.data[p] + off)[i];
+#pragma unroll
+  for (int p = 0; p < W; ++p) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[j] += bf2f(v[p][j]);
   }
 }
 
@@ -116,7 +121,7 @@ ar_oneshot_kernel(ArPeers P, const bf16_t* __restrict__ in, bf16_t* __restrict__
   block_barrier(P, rank, W, ep, own);
   for (long i = first; i < n8; i += stride) {
     float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-    sum_peers(P, W, rank, off, i, acc);
+    sum_peers<W>(P, off, i, acc);
     reinterpret_cast<bf16x8*>(out)[i] = pack8(acc);
   }
 }
@@ -140,7 +145,7 @@ ar_twoshot_kernel(ArPeers P, const bf16_t* __restrict__ in, bf16_t* __restrict__
   // reduce-scatter: slice `rank` from every peer -> own buffer
   for (long j = first; j < per && rank * per + j < n8; j += stride) {
     float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-    sum_peers(P, W, rank, off, rank * per + j, acc);
+    sum_peers<W>(P, off, rank * per + j, acc);
     mine[rank * per + j] = pack8(acc);
   }
   const uint32_t ep2 = block_epoch(own);
@@ -152,6 +157,114 @@ ar_twoshot_kernel(ArPeers P, const bf16_t* __restrict__ in, bf16_t* __restrict__
     for (long j = first; j < per && src * per + j < n8; j += stride)
       reinterpret_cast<bf16x8*>(out)[src * per + j] = sp[src * per + j];
   }
+}
+
+// ---------------------------------------------------------------------------------------
+// Fused all-reduce + residual add + RMSNorm (C1/C2 + K5): the row-parallel o_proj / down_proj
+// partial sums of T rows x H are reduced over the TP group and, in the same kernel,
+//   s        = bf16(sum over ranks)            (what a plain all-reduce would store)
+//   residual = bf16(s + residual)              (in place; identical on every rank)
+//   out      = bf16(rmsnorm(residual) * w)
+// which is exactly the unfused all-reduce -> fused_add_rms_norm pair, minus one launch and
+// one T x H round trip through HBM per layer and per projection.
+// Rows, not elements, are the unit of work (the norm needs the whole row in one block):
+// row j belongs to block (j mod per) mod G in EVERY phase and on EVERY rank (per = rows per
+// rank slice), which keeps the "a peer's block b only reads what my block b staged before
+// its flag" invariant of the element kernels above.
+//   one-shot (1 sync):  stage rows -> barrier -> each block sums its rows over W peers,
+//                       adds, normalises.  Small T*H (latency-bound decode).
+//   two-shot (2 syncs): stage -> barrier -> reduce-scatter: rank r sums rows of slice r into
+//                       its own buffer -> barrier -> every rank reads each row's sum from its
+//                       owner, adds, normalises.  Every link carries 2S/W bytes.
+// 512 threads per block; each thread keeps VPT bf16x8 vectors of a row in registers.
+template <int W, int VPT>
+__global__ void __launch_bounds__(512)
+ar_add_rmsnorm_kernel(ArPeers P, const bf16_t* __restrict__ in, bf16_t* __restrict__ residual,
+                      const bf16_t* __restrict__ w, bf16_t* __restrict__ out, float eps, int rank,
+                      int T, int H, long half_off, int twoshot) {
+  __shared__ float scratch[8];
+  ArSignal* own = P.sig[rank];
+  const long off = call_half_off(own, half_off);
+  const uint32_t ep = block_epoch(own);
+  const int G = gridDim.x, b = blockIdx.x;
+  const int nvec = H >> 3;
+  const int per = twoshot ? (T + W - 1) / W : T;
+  bf16x8* mine = reinterpret_cast<bf16x8*>(P.data[rank] + off);
+  const bf16x8* xin = reinterpret_cast<const bf16x8*>(in);
+  // phase 0: stage every row this block owns (all slices)
+  for (int s = 0; s * per < T; ++s)
+    for (int k = b; k < per && s * per + k < T; k += G) {
+      const long row = (long)(s * per + k) * nvec;
+#pragma unroll
+      for (int i = 0; i < VPT; ++i) {
+        const int idx = threadIdx.x + i * 512;
+        if (idx < nvec) mine[row + idx] = xin[row + idx];
+      }
+    }
+  block_barrier(P, rank, W, ep, own);
+  if (twoshot) {
+    // phase 1: reduce-scatter -- sums of this rank's slice, written over its own staging
+    for (int k = b; k < per && rank * per + k < T; k += G) {
+      const long row = (long)(rank * per + k) * nvec;
+#pragma unroll
+      for (int i = 0; i < VPT; ++i) {
+        const int idx = threadIdx.x + i * 512;
+        if (idx < nvec) {
+          float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+          sum_peers<W>(P, off, row + idx, acc);
+          mine[row + idx] = pack8(acc);
+        }
+      }
+    }
+    const uint32_t ep2 = block_epoch(own);
+    block_barrier(P, rank, W, ep2, own);
+  }
+  // final phase: every row this block owns -> residual add + RMSNorm
+  const bf16x8* wv = reinterpret_cast<const bf16x8*>(w);
+  for (int s = 0; s * per < T; ++s)
+    for (int k = b; k < per && s * per + k < T; k += G) {
+      const long row = (long)(s * per + k) * nvec;
+      const bf16x8* src = reinterpret_cast<const bf16x8*>(P.data[twoshot ? s : 0] + off);
+      bf16x8* rr = reinterpret_cast<bf16x8*>(residual) + row;
+      float v[VPT][8];
+      float ss = 0.f;
+#pragma unroll
+      for (int i = 0; i < VPT; ++i) {
+        const int idx = threadIdx.x + i * 512;
+        if (idx < nvec) {
+          bf16x8 sum;
+          if (twoshot) {
+            sum = src[row + idx];
+          } else {
+            float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+            sum_peers<W>(P, off, row + idx, acc);
+            sum = pack8(acc);
+          }
+          const bf16x8 r = rr[idx];
+          bf16x8 t;
+#pragma unroll
+          for (int j = 0; j < 8; ++j) {
+            t[j] = f2bf(bf2f(sum[j]) + bf2f(r[j]));
+            v[i][j] = bf2f(t[j]);
+            ss += v[i][j] * v[i][j];
+          }
+          rr[idx] = t;
+        }
+      }
+      const float inv = rsqrtf(block_sum(ss, scratch) / (float)H + eps);
+      bf16x8* orow = reinterpret_cast<bf16x8*>(out) + row;
+#pragma unroll
+      for (int i = 0; i < VPT; ++i) {
+        const int idx = threadIdx.x + i * 512;
+        if (idx < nvec) {
+          const bf16x8 ww = wv[idx];
+          bf16x8 o;
+#pragma unroll
+          for (int j = 0; j < 8; ++j) o[j] = f2bf(v[i][j] * inv * bf2f(ww[j]));
+          orow[idx] = o;
+        }
+      }
+    }
 }
 
 }  // namespace
@@ -200,6 +313,48 @@ EIA_API int eia_ar_run(void* const* peers_sig, void* const* peers_data, int rank
   }
 #undef AR_W
 #undef AR_LAUNCH
+  EIA_LAUNCH_CHECK();
+}
+
+// in [T,H] (partial sums, may alias out), residual [T,H] updated in place, w [H], out [T,H].
+EIA_API int eia_ar_add_rmsnorm(void* const* peers_sig, void* const* peers_data, int rank,
+                               int world, const void* in, void* residual, const void* w,
+                               void* out, float eps, int T, int H, long max_bytes, int twoshot,
+                               int nblocks, hipStream_t st) {
+  if (world < 2 || world > AR_MAXR || rank < 0 || rank >= world) return EIA_BAD_SHAPE;
+  if (H % 8 != 0 || T < 0 || (long)T * H * 2 > max_bytes || nblocks < 1 || nblocks > AR_MAXB)
+    return EIA_BAD_SHAPE;
+  if (T == 0) return EIA_OK;
+  const int nvec = H / 8;
+  const int vpt = (nvec + 511) / 512;
+  if (vpt > 4) return EIA_UNSUPPORTED;
+  ArPeers P;
+  for (int i = 0; i < AR_MAXR; ++i) {
+    P.sig[i] = i < world ? static_cast<ArSignal*>(peers_sig[i]) : nullptr;
+    P.data[i] = i < world ? static_cast<char*>(peers_data[i]) : nullptr;
+  }
+#define ARN_LAUNCH(WW, V)                                                                    \
+  hipLaunchKernelGGL((ar_add_rmsnorm_kernel<WW, V>), dim3(nblocks), dim3(512), 0, st, P,      \
+                     static_cast<const bf16_t*>(in), static_cast<bf16_t*>(residual),         \
+                     static_cast<const bf16_t*>(w), static_cast<bf16_t*>(out), eps, rank, T, H, \
+                     max_bytes, twoshot)
+#define ARN_V(WW)                                              \
+  switch (vpt) {                                               \
+    case 1: ARN_LAUNCH(WW, 1); break;                          \
+    case 2: ARN_LAUNCH(WW, 2); break;                          \
+    default: ARN_LAUNCH(WW, 4); break;                         \
+  }
+  switch (world) {
+    case 2: ARN_V(2) break;
+    case 3: ARN_V(3) break;
+    case 4: ARN_V(4) break;
+    case 5: ARN_V(5) break;
+    case 6: ARN_V(6) break;
+    case 7: ARN_V(7) break;
+    default: ARN_V(8) break;
+  }
+#undef ARN_V
+#undef ARN_LAUNCH
   EIA_LAUNCH_CHECK();
 }
 

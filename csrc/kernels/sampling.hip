@@ -171,10 +171,12 @@ EIA_API int eia_sample(const float* logits, long stride, int B, int V, const flo
 // identical to sample_kernel, so both paths return the same token for the same seed.
 #define SPLIT_THREADS 256
 
+// vocab_offset: global id of column 0 (a tensor-parallel vocab shard); the RNG is keyed by the
+// GLOBAL token id, so a shard's winner is exactly what the full row would produce there.
 __global__ void __launch_bounds__(SPLIT_THREADS)
 sample_split_kernel(const float* __restrict__ logits, long stride, int V, int chunk,
                     const float* __restrict__ temperature, const uint64_t* __restrict__ seeds,
-                    float* __restrict__ part_v, int* __restrict__ part_i) {
+                    float* __restrict__ part_v, int* __restrict__ part_i, int vocab_offset) {
   __shared__ float sv[SPLIT_THREADS / 64];
   __shared__ int si[SPLIT_THREADS / 64];
   const int b = blockIdx.y, c = blockIdx.x, C = gridDim.x;
@@ -186,12 +188,13 @@ sample_split_kernel(const float* __restrict__ logits, long stride, int V, int ch
   ArgMax best{-INFINITY, 0x7fffffff};
   for (int i = lo + threadIdx.x; i < hi; i += SPLIT_THREADS) {
     const float l = row[i];
+    const int gi = i + vocab_offset;
     float v = l;
     if (!greedy) {
-      const float u = rng_uniform(seed, (uint32_t)i);
+      const float u = rng_uniform(seed, (uint32_t)gi);
       v = l / T - logf(-logf(u));
     }
-    best = argmax_combine(best, ArgMax{v, i});
+    best = argmax_combine(best, ArgMax{v, gi});
   }
   best = block_argmax(best, sv, si);
   if (threadIdx.x == 0) {
@@ -202,7 +205,7 @@ sample_split_kernel(const float* __restrict__ logits, long stride, int V, int ch
 
 __global__ void __launch_bounds__(64)
 sample_merge_kernel(const float* __restrict__ part_v, const int* __restrict__ part_i, int C,
-                    int* __restrict__ out_tokens) {
+                    int* __restrict__ out_tokens, float* __restrict__ out_v) {
   const int b = blockIdx.x;
   ArgMax best{-INFINITY, 0x7fffffff};
   for (int c = threadIdx.x; c < C; c += 64)
@@ -212,7 +215,10 @@ sample_merge_kernel(const float* __restrict__ part_v, const int* __restrict__ pa
     ArgMax y{__shfl_xor(best.v, o, 64), __shfl_xor(best.i, o, 64)};
     best = argmax_combine(best, y);
   }
-  if (threadIdx.x == 0) out_tokens[b] = best.i == 0x7fffffff ? 0 : best.i;
+  if (threadIdx.x == 0) {
+    out_tokens[b] = best.i == 0x7fffffff ? 0 : best.i;
+    if (out_v) out_v[b] = best.v;
+  }
 }
 
 // part_v / part_i: >= B * ceil(V / chunk) entries each.
@@ -224,8 +230,28 @@ EIA_API int eia_sample_split(const float* logits, long stride, int B, int V, int
   const int C = (V + chunk - 1) / chunk;
   if (C > 4096) return EIA_BAD_SHAPE;
   hipLaunchKernelGGL(sample_split_kernel, dim3(C, B), dim3(SPLIT_THREADS), 0, st, logits, stride,
-                     V, chunk, temperature, seeds, part_v, part_i);
-  hipLaunchKernelGGL(sample_merge_kernel, dim3(B), dim3(64), 0, st, part_v, part_i, C, out_tokens);
+                     V, chunk, temperature, seeds, part_v, part_i, 0);
+  hipLaunchKernelGGL(sample_merge_kernel, dim3(B), dim3(64), 0, st, part_v, part_i, C, out_tokens,
+                     nullptr);
+  EIA_LAUNCH_CHECK();
+}
+
+// Tensor-parallel LM head (C4 without the full-logit gather): each rank samples its vocab
+// shard [vocab_offset, vocab_offset + V) of unfiltered rows and writes the shard winner's
+// (perturbed value, global id); the ranks then exchange B (value, id) pairs and keep the max,
+// lowest id on ties -- the same token the full-row sampler picks.
+EIA_API int eia_sample_shard(const float* logits, long stride, int B, int V, int chunk,
+                             int vocab_offset, const float* temperature, const uint64_t* seeds,
+                             float* part_v, int* part_i, float* out_v, int* out_i,
+                             hipStream_t st) {
+  if (B < 0 || V <= 0 || chunk <= 0 || vocab_offset < 0) return EIA_BAD_SHAPE;
+  if (B == 0) return EIA_OK;
+  const int C = (V + chunk - 1) / chunk;
+  if (C > 4096) return EIA_BAD_SHAPE;
+  hipLaunchKernelGGL(sample_split_kernel, dim3(C, B), dim3(SPLIT_THREADS), 0, st, logits, stride,
+                     V, chunk, temperature, seeds, part_v, part_i, vocab_offset);
+  hipLaunchKernelGGL(sample_merge_kernel, dim3(B), dim3(64), 0, st, part_v, part_i, C, out_i,
+                     out_v);
   EIA_LAUNCH_CHECK();
 }
 

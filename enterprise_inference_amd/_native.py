@@ -46,6 +46,7 @@ _SIGNATURES = {
     "eia_sample": [P, L, I, I, P, P, P, P, P, P, S],
     "eia_apply_penalties": [P, L, P, P, P, I, P, P, P, S],
     "eia_sample_split": [P, L, I, I, I, P, P, P, P, P, S],
+    "eia_sample_shard": [P, L, I, I, I, I, P, P, P, P, P, P, S],
     "eia_fill_ids": [P, P, P, I, S],
     "eia_moe_topk": [P, I, I, I, I, I, I, P, P, S],
     "eia_moe_align": [P, I, I, I, I, P, P, P, I, S],
@@ -59,6 +60,7 @@ _SIGNATURES = {
     "eia_ar_signal_bytes": [],
     "eia_ar_run": [P, P, I, I, P, P, L, L, I, I, S],
     "eia_ar_read_err": [P, P],
+    "eia_ar_add_rmsnorm": [P, P, I, I, P, P, P, P, F, I, I, L, I, I, S],
 }
 
 

@@ -15,8 +15,8 @@ from __future__ import annotations
 import logging
 import multiprocessing as mp
 import os
-import pickle
 import socket
+import time
 from typing import Optional
 
 import torch
@@ -75,39 +75,60 @@ class UniprocExecutor:
         pass
 
 
-def worker_loop(runner: ModelRunner, ring_name: str) -> None:
-    """Non-driver TP rank: replay every plan the driver publishes until None arrives."""
+def _alive(pid: Optional[int]) -> bool:
+    if not pid:
+        return True
+    try:
+        os.kill(pid, 0)
+        return True
+    except ProcessLookupError:
+        return False
+    except PermissionError:
+        return True
+
+
+def worker_loop(runner: ModelRunner, ring_name: str, driver_pid: Optional[int] = None) -> None:
+    """Non-driver TP rank: replay every plan the driver publishes until the empty shutdown
+    message arrives (or the driver process is gone -- then the collectives could never
+    complete, so the worker exits instead of waiting forever)."""
     ring = _native.runtime().ShmRing(ring_name, False)
-    while True:
-        msg = ring.get(-1.0)
-        if msg is None:
-            break
-        obj = pickle.loads(msg)
-        if obj is None:
-            break
-        plan, payload = obj
-        runner.load_payload(plan, payload)
-        with torch.no_grad():
-            runner.run(plan)
+    with torch.no_grad():
+        while True:
+            msg = ring.get(1.0)
+            if msg is None:
+                if not _alive(driver_pid):
+                    logger.error("TP driver %s is gone; worker exiting", driver_pid)
+                    return
+                continue
+            if not msg:
+                return
+            runner.replay(runner.load_message(msg))
 
 
-def _spawned_worker(cfg: EngineConfig, rank: int, world: int, port: int, ring_name: str) -> None:
+def _spawned_worker(cfg: EngineConfig, rank: int, world: int, port: int, ring_name: str,
+                    driver_pid: int) -> None:
     os.environ.update(RANK=str(rank), WORLD_SIZE=str(world), LOCAL_RANK=str(rank),
                       MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
-    if torch.cuda.is_available():
+    if cfg.device == "cuda" and torch.cuda.device_count() > 0:
         torch.cuda.set_device(rank)
     pstate.init_distributed(cfg.parallel.tensor_parallel_size,
                             enable_expert_parallel=cfg.parallel.enable_expert_parallel,
                             pp_size=cfg.parallel.pipeline_parallel_size)
     runner = setup_runner(cfg)
-    worker_loop(runner, ring_name)
+    worker_loop(runner, ring_name, driver_pid)
     pstate.destroy_distributed()
 
 
 class TPExecutor:
-    """Driver side of tensor (and pipeline) parallelism: one process per rank of the replica."""
+    """Driver side of tensor (and pipeline) parallelism: one process per rank of the replica.
 
-    supports_overlap = False    # workers replay plans synchronously; tokens are read each step
+    Per step the driver publishes ONE message through the native shm ring: a fixed 32-word
+    plan header + the staging bytes (ids/positions/slots/block tables + sampling params);
+    every rank replays it and samples on its gathered logits, so the next step can be
+    launched before this one's tokens reach the host (overlapped scheduling, as TP=1).
+    Worker processes are watched: if one dies the driver cannot complete another
+    collective, so it fails fast (``os._exit``) and the pod restarts instead of hanging
+    until the RCCL timeout."""
 
     def __init__(self, cfg: EngineConfig, spawn: bool = True):
         tp = cfg.parallel.tensor_parallel_size * cfg.parallel.pipeline_parallel_size
@@ -115,38 +136,65 @@ class TPExecutor:
         self.ring_name = f"/eia_ring_{os.getpid()}_{id(self) & 0xffff}"
         rt = _native.runtime()
         self.ring = rt.ShmRing(self.ring_name, True, tp - 1, 8, 16 << 20)
+        self.supports_overlap = cfg.parallel.pipeline_parallel_size == 1
+        self._closed = False
         if spawn and not dist.is_initialized():
             port = _free_port()
             ctx = mp.get_context("spawn")
             for r in range(1, tp):
-                p = ctx.Process(target=_spawned_worker, args=(cfg, r, tp, port, self.ring_name),
-                                daemon=True)
+                p = ctx.Process(target=_spawned_worker,
+                                args=(cfg, r, tp, port, self.ring_name, os.getpid()), daemon=True)
                 p.start()
                 self.procs.append(p)
             os.environ.update(RANK="0", WORLD_SIZE=str(tp), LOCAL_RANK="0",
                               MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
-            if torch.cuda.is_available():
+            if cfg.device == "cuda" and torch.cuda.device_count() > 0:
                 torch.cuda.set_device(0)
             pstate.init_distributed(cfg.parallel.tensor_parallel_size,
                                     enable_expert_parallel=cfg.parallel.enable_expert_parallel,
                                     pp_size=cfg.parallel.pipeline_parallel_size)
+            self._start_monitor()
         self.runner = setup_runner(cfg)
         self.num_blocks = self.runner.num_blocks
 
-    def execute(self, bm, sched) -> StepOutput:
+    # ------------------------------------------------------------------ liveness
+    def dead_workers(self):
+        return [p for p in self.procs if not p.is_alive()]
+
+    def _start_monitor(self) -> None:
+        import threading
+
+        def watch():
+            while not self._closed:
+                dead = self.dead_workers()
+                if dead and not self._closed:
+                    logger.critical("TP worker(s) %s died (exit codes %s); aborting the driver",
+                                    [p.pid for p in dead], [p.exitcode for p in dead])
+                    os._exit(70)
+                time.sleep(0.5)
+
+        threading.Thread(target=watch, name="eia-tp-monitor", daemon=True).start()
+
+    def _publish(self, msg: bytes) -> None:
+        while not self.ring.put(msg, 1.0):
+            dead = self.dead_workers()
+            if dead:
+                raise RuntimeError(f"TP worker(s) {[p.pid for p in dead]} died")
+
+    # ------------------------------------------------------------------ steps
+    def launch(self, bm, sched, overlap: bool):
         r = self.runner
-        sample_items = sched.decodes + [p for p in sched.prefills if p.samples]
         plan = r.prepare(bm, sched)
-        self.ring.put(pickle.dumps((plan, r.plan_payload(plan)), protocol=5), -1.0)
-        with torch.no_grad():
-            logits = r.run(plan)
-            if not sample_items:
-                return StepOutput([], None)
-            return r.sample(logits, sample_items)
+        return r.launch_plan(plan, sched, overlap,
+                             publish=lambda pl: self._publish(r.encode_plan(pl)))
+
+    def execute(self, bm, sched) -> StepOutput:
+        return self.launch(bm, sched, overlap=False).result()
 
     def shutdown(self) -> None:
+        self._closed = True
         try:
-            self.ring.put(pickle.dumps(None), 5.0)
+            self.ring.put(b"", 5.0)
         except Exception:   # noqa: BLE001
             pass
         for p in self.procs:

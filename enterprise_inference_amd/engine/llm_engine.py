@@ -185,12 +185,8 @@ class LLMEngine:
     # ------------------------------------------------------------------ step
     @staticmethod
     def _needs_host_tokens(seq: Sequence) -> bool:
-        """Rows whose sampling needs the host (penalties over the output, logits processors,
-        guided decoding, logprobs): their step is read back before the next is planned."""
-        p = seq.params
-        return (p.needs_penalties or p.needs_logit_processing or p.logprobs is not None
-                or p.prompt_logprobs is not None or seq.guided_state is not None
-                or p.best_of > p.n)
+        from .sequence import needs_host_processing
+        return needs_host_processing(seq)
 
     def step(self) -> List[RequestOutput]:
         if not self._overlap:

@@ -27,6 +27,7 @@ from ..ops import sampling as sampling_ops
 from ..parallel import state as pstate
 from .block_manager import BlockManager
 from .scheduler import ScheduledSeq, SchedulerOutput
+from .sequence import needs_host_processing
 
 logger = logging.getLogger(__name__)
 
@@ -52,6 +53,53 @@ class StepOutput:
 
 
 _TOKEN_WAIT = __import__("os").environ.get("EIA_TOKEN_WAIT", "event")
+
+_O_NAMES = ("ids", "pos", "slot", "src", "dbt", "dlen", "pbt", "plen", "cu", "work", "lidx")
+_PLAN_MAGIC = 0x45504C31      # "EPL1"
+_HDR_WORDS = 32
+
+
+class StepPlan:
+    """Everything a rank needs to replay one step, besides the staging bytes: the launch
+    shape (graph bucket or eager token layout), offsets into the packed eager buffer and
+    the sampling set-up.  TP workers receive it as a fixed 32-word int32 header in front of
+    the staging bytes (``ModelRunner.encode_plan``) -- no pickling on the step path."""
+
+    __slots__ = ("kind", "Bp", "nd", "T", "npf", "mb_d", "mb_p", "n_work", "n_lidx", "P", "off",
+                 "src", "n_sample", "unfiltered", "sharded", "o")
+
+    def __init__(self, kind: str, **kw):
+        self.kind = kind
+        for k in self.__slots__[1:]:
+            setattr(self, k, kw.get(k, {} if k == "o" else 0))
+
+    def __getitem__(self, k):           # plan["nd"] style access
+        return getattr(self, k)
+
+    def get(self, k, default=None):
+        return getattr(self, k, default)
+
+    def header(self, payload_words: int) -> np.ndarray:
+        h = np.zeros(_HDR_WORDS, dtype=np.int32)
+        h[0:16] = (_PLAN_MAGIC, 0 if self.kind == "graph" else 1, self.Bp, self.nd, self.T,
+                   self.npf, self.mb_d, self.mb_p, self.n_work, self.n_lidx, self.P, self.off,
+                   int(bool(self.src)), self.n_sample, int(bool(self.unfiltered)), payload_words)
+        for i, n in enumerate(_O_NAMES):
+            h[16 + i] = self.o.get(n, -1)
+        h[27] = int(bool(self.sharded))
+        return h
+
+    @classmethod
+    def from_header(cls, h: np.ndarray) -> Tuple["StepPlan", int]:
+        if int(h[0]) != _PLAN_MAGIC:
+            raise RuntimeError("corrupt step plan header")
+        p = cls("graph" if int(h[1]) == 0 else "eager", Bp=int(h[2]), nd=int(h[3]), T=int(h[4]),
+                npf=int(h[5]), mb_d=int(h[6]), mb_p=int(h[7]), n_work=int(h[8]),
+                n_lidx=int(h[9]), P=int(h[10]), off=int(h[11]), src=bool(h[12]),
+                n_sample=int(h[13]), unfiltered=bool(h[14]), sharded=bool(h[27]))
+        if p.kind == "eager":
+            p.o = {n: int(h[16 + i]) for i, n in enumerate(_O_NAMES)}
+        return p, int(h[15])
 
 
 class StepHandle:
@@ -116,6 +164,14 @@ class ModelRunner:
         self.graph_pool = None
         self.vocab = m.vocab_size
         self.num_heads = m.num_attention_heads // pstate.tp_size()
+        # TP>1: the LM head stays vocab-sharded; unfiltered rows are sampled per shard and only
+        # B (value, id) pairs cross xGMI instead of B x V logits
+        self.sharded_lm = (pstate.tp_size() > 1 and self.pp == 1 and
+                           hasattr(self.model, "compute_logits_local") and
+                           __import__("os").environ.get("EIA_TP_SHARDED_SAMPLING", "1") != "0")
+        if self.sharded_lm:
+            self.lm_offset = self.model.lm_head.start
+            self.lm_valid = self.model.lm_head.valid_local
         self._alloc_staging()
 
     # ------------------------------------------------------------------ buffers
@@ -137,6 +193,9 @@ class ModelRunner:
         # while step k's H2D copies may still be queued behind step k-1 on the stream.
         self._pin = [self._pinned_set(pin) for _ in range(2)]
         self._par = 0
+        # event recorded after the last device read of each pinned set (H2D copies are async):
+        # a set is rewritten only after its previous step's copies completed
+        self._staging_ev: List[Optional[torch.cuda.Event]] = [None, None]
         self._use_pinned(0)
         dev = self.device
         self.d_g_hdr = torch.zeros(self.hdr_len, dtype=torch.int32, device=dev)
@@ -175,7 +234,18 @@ class ModelRunner:
 
     def _flip_staging(self) -> None:
         self._par ^= 1
+        ev = self._staging_ev[self._par]
+        if ev is not None:
+            ev.synchronize()            # that set's uploads (two steps ago) have landed
+            self._staging_ev[self._par] = None
         self._use_pinned(self._par)
+
+    def finish_step(self) -> None:
+        """Mark the current staging set as read by everything enqueued so far."""
+        if self.is_gpu:
+            ev = torch.cuda.Event()
+            ev.record()
+            self._staging_ev[self._par] = ev
 
     def _fill_decode_inputs(self, decodes: List[ScheduledSeq], ids: np.ndarray,
                             src: np.ndarray) -> bool:
@@ -301,9 +371,9 @@ class ModelRunner:
             hdr[so + n:so + Bp] = -1
         max_len = int(hdr[3 * S:3 * S + n].max()) if n else 1
         hdr[4 * S] = min(self._decode_partitions(Bp, max_len), self.graph_P.get(Bp, 1))
-        return {"kind": "graph", "Bp": Bp, "nd": n}
+        return StepPlan("graph", Bp=Bp, nd=n)
 
-    def _upload_graph(self, Bp: int) -> None:
+    def _upload_graph(self, Bp: int) -> None:  # noqa: D401 - H2D of the graph header
         self.d_g_hdr.copy_(self.g_hdr, non_blocking=True)
         self.d_g_bt[:Bp * self.maxb].copy_(self.g_bt[:Bp * self.maxb], non_blocking=True)
 
@@ -322,7 +392,17 @@ class ModelRunner:
         ids, md = self._graph_metadata(Bp, P)
         sampling_ops.fill_ids(ids, self.d_g_hdr[self.src_off:self.src_off + Bp], self.d_tok)
         h = self.model(ids, md, self.kv_caches)
+        return self._logits(h)
+
+    def _logits(self, h: torch.Tensor) -> torch.Tensor:
+        """Full fp32 logits, or this rank's vocab shard (model dtype) when ``sharded_lm``."""
+        if self.sharded_lm:
+            return self.model.compute_logits_local(h)
         return self.model.compute_logits(h)
+
+    def gather_logits(self, local: torch.Tensor) -> torch.Tensor:
+        """Vocab shards -> full fp32 logits (a collective: every TP rank calls it)."""
+        return self.model.lm_head.gather(local).float()
 
     def _prepare_eager(self, bm: BlockManager, out: SchedulerOutput) -> dict:
         """Pack the step's metadata into the eager staging buffer; returns the plan."""
@@ -390,11 +470,10 @@ class ModelRunner:
             buf[o["lidx"]:o["lidx"] + len(sample_rows)] = sample_rows
         max_len = max([it.start + it.num_tokens for it in out.decodes], default=1)
         P = self._decode_partitions(nd, max_len) if nd else 1
-        return {"kind": "eager", "T": T, "nd": nd, "npf": npf, "mb_d": mb_d, "mb_p": mb_p,
-                "o": o, "n_work": len(work) // 2, "n_lidx": len(sample_rows), "P": P, "off": off,
-                "src": has_src}
+        return StepPlan("eager", T=T, nd=nd, npf=npf, mb_d=mb_d, mb_p=mb_p, o=o,
+                        n_work=len(work) // 2, n_lidx=len(sample_rows), P=P, off=off, src=has_src)
 
-    def _eager_inputs(self, plan: dict):
+    def _eager_inputs(self, plan: StepPlan):
         d = self.d_e_buf
         o, T, nd, npf = plan["o"], plan["T"], plan["nd"], plan["npf"]
         mb_d, mb_p, nw = plan["mb_d"], plan["mb_p"], plan["n_work"]
@@ -415,32 +494,55 @@ class ModelRunner:
             sampling_ops.fill_ids(ids[:nd], d[o["src"]:o["src"] + nd], self.d_tok)
         return ids, md, lidx
 
-    def prepare(self, bm: BlockManager, out: SchedulerOutput) -> dict:
-        """Host side of a step (driver only): fill the pinned staging buffers."""
+    def prepare(self, bm: BlockManager, out: SchedulerOutput) -> StepPlan:
+        """Host side of a step (driver only): fill the pinned staging buffers (inputs and the
+        sampling parameters of the rows that emit a token)."""
         self._flip_staging()
         nd = len(out.decodes)
         if not out.prefills and self.graphs and nd <= max(self.graphs):
             Bp = min(b for b in self.graphs if b >= nd)
-            return self._prepare_graph(bm, out.decodes, Bp)
-        return self._prepare_eager(bm, out)
-
-    def plan_payload(self, plan: dict) -> bytes:
-        """Staging bytes a TP worker needs to replay `plan` (sent over the shm ring)."""
-        if plan["kind"] == "graph":
-            Bp = plan["Bp"]
-            return self.g_hdr.numpy().tobytes() + self.g_bt.numpy()[:Bp * self.maxb].tobytes()
-        return self.e_buf.numpy()[:plan["off"]].tobytes()
-
-    def load_payload(self, plan: dict, payload: bytes) -> None:
-        a = np.frombuffer(payload, dtype=np.int32)
-        if plan["kind"] == "graph":
-            hl = self.hdr_len
-            self.g_hdr.numpy()[:] = a[:hl]
-            self.g_bt.numpy()[:len(a) - hl] = a[hl:]
+            plan = self._prepare_graph(bm, out.decodes, Bp)
         else:
-            self.e_buf.numpy()[:len(a)] = a
+            plan = self._prepare_eager(bm, out)
+        items = out.decodes + [p for p in out.prefills if p.samples]
+        plan.n_sample = len(items)
+        if items:
+            plan.unfiltered = self._fill_sampling(items)
+            plan.sharded = self.sharded_lm and plan.unfiltered and not any(
+                needs_host_processing(it.seq) for it in items)
+        return plan
 
-    def run(self, plan: dict) -> Optional[torch.Tensor]:
+    def _staging_words(self, plan: StepPlan):
+        """int32 views of the staging regions `plan` reads, in wire order."""
+        if plan.kind == "graph":
+            views = [self.g_hdr.numpy(), self.g_bt.numpy()[:plan.Bp * self.maxb]]
+        else:
+            views = [self.e_buf.numpy()[:plan.off]]
+        if plan.n_sample:
+            views += [self.s_f32.numpy().view(np.int32), self.s_i32.numpy(),
+                      self.s_i64.numpy().view(np.int32)]
+        return views
+
+    def encode_plan(self, plan: StepPlan) -> bytes:
+        """Wire message for TP workers: 32-word header + staging bytes (one copy)."""
+        views = self._staging_words(plan)
+        return b"".join([plan.header(sum(v.size for v in views)).tobytes()] +
+                        [v.tobytes() for v in views])
+
+    def load_message(self, msg: bytes) -> StepPlan:
+        """TP worker: decode a driver message into this rank's (flipped) staging buffers."""
+        a = np.frombuffer(msg, dtype=np.int32)
+        plan, nwords = StepPlan.from_header(a[:_HDR_WORDS])
+        self._flip_staging()
+        pos = _HDR_WORDS
+        for v in self._staging_words(plan):
+            v[:] = a[pos:pos + v.size]
+            pos += v.size
+        if pos != _HDR_WORDS + nwords:
+            raise RuntimeError("step plan payload size mismatch")
+        return plan
+
+    def run(self, plan: StepPlan) -> Optional[torch.Tensor]:
         """Device side of a step (every TP rank): returns logits of the sampling rows."""
         if plan["kind"] == "graph":
             Bp = plan["Bp"]
@@ -455,7 +557,7 @@ class ModelRunner:
         h = self.model(ids, md, self.kv_caches)
         if plan["n_lidx"] == 0:
             return None
-        return self.model.compute_logits(h.index_select(0, lidx))
+        return self._logits(h.index_select(0, lidx))
 
     def _forward(self, ids, md, kv_caches, intermediate=None):
         if self.pp > 1:
@@ -496,8 +598,9 @@ class ModelRunner:
         return logits
 
     # ------------------------------------------------------------------ sampling
-    def _sampling_tensors(self, items: List[ScheduledSeq]):
-        n = len(items)
+    def _fill_sampling(self, items: List[ScheduledSeq]) -> bool:
+        """Host staging of the per-row sampling parameters; returns True when no row filters
+        (top-k / top-p / min-p), i.e. the split-row sampler applies."""
         f = self.s_f32.numpy()
         S = self.max_num_seqs
         k = self.s_i32.numpy()
@@ -515,7 +618,10 @@ class ModelRunner:
                 unfiltered = False
             # index of the token being sampled (in-flight samples included)
             sd[i] = sampling_ops.row_seed(seq.seed, len(seq.output_token_ids) + seq.num_pending)
-        self._unfiltered = unfiltered
+        return unfiltered
+
+    def _sampling_tensors(self, n: int):
+        S = self.max_num_seqs
         if self.is_gpu:
             self.d_s_f32.copy_(self.s_f32, non_blocking=True)
             self.d_s_i32[:n].copy_(self.s_i32[:n], non_blocking=True)
@@ -525,20 +631,44 @@ class ModelRunner:
             F_, K_, SD = self.s_f32, self.s_i32, self.s_i64
         return F_[:n], K_[:n], F_[S:S + n], F_[2 * S:2 * S + n], SD[:n]
 
-    def _sample_tokens(self, logits: torch.Tensor, items: List[ScheduledSeq]) -> torch.Tensor:
+    def sample_device(self, logits: torch.Tensor, plan: StepPlan,
+                      full: bool = False) -> torch.Tensor:
+        """Sample the plan's rows into d_tok[:n] from the staged parameters.  Every TP rank
+        runs this (same collectives, same inputs), so all ranks hold the same tokens on the
+        device -- what the next step's in-graph ``fill_ids`` of each rank reads.
+        ``full``: ``logits`` are already gathered (driver-side logits processing)."""
+        n = plan.n_sample
+        temp, top_k, top_p, min_p, seeds = self._sampling_tensors(n)
+        if self.sharded_lm and not full:
+            if plan.sharded:
+                local = logits[:, :self.lm_valid].float()
+                v, i = sampling_ops.sample_shard(local, temp, seeds, self.lm_offset)
+                from ..parallel import comm
+                pair = torch.cat([v, i.view(torch.float32)])[None, :]
+                g = comm.all_gather(pair, 0)                     # [W, 2n]
+                toks = sampling_ops.merge_shard_winners(g[:, :n],
+                                                        g[:, n:].contiguous().view(torch.int32))
+                self.d_tok[:n].copy_(toks)
+                return self.d_tok[:n]
+            logits = self.gather_logits(logits)
+        return sampling_ops.sample(logits, temp, top_k, top_p, min_p, seeds, out=self.d_tok[:n],
+                                   unfiltered=plan.unfiltered)
+
+    def _sample_tokens(self, logits: torch.Tensor, items: List[ScheduledSeq],
+                       plan: StepPlan, full: bool = False) -> torch.Tensor:
         """Sample into d_tok[:n] (device); also records which seq owns which row."""
-        temp, top_k, top_p, min_p, seeds = self._sampling_tensors(items)
-        n = len(items)
-        toks = sampling_ops.sample(logits, temp, top_k, top_p, min_p, seeds, out=self.d_tok[:n],
-                                   unfiltered=self._unfiltered)
+        toks = self.sample_device(logits, plan, full)
         self.last_rows = {it.seq.seq_id: r for r, it in enumerate(items)}
         return toks
 
-    def sample(self, logits: torch.Tensor, items: List[ScheduledSeq]) -> StepOutput:
+    def sample(self, logits: torch.Tensor, items: List[ScheduledSeq],
+               plan: StepPlan) -> StepOutput:
         from .logits_process import apply_logits_processors
 
+        if self.sharded_lm and not plan.sharded:
+            logits = self.gather_logits(logits)
         logits = apply_logits_processors(logits, items)
-        toks = self._sample_tokens(logits, items)
+        toks = self._sample_tokens(logits, items, plan, full=True)
         lp = None
         want = [it.seq.params.logprobs for it in items]
         if any(w is not None for w in want):
@@ -568,32 +698,49 @@ class ModelRunner:
         """Enqueue a step.  ``overlap``: leave the sampled tokens on the device (the next step
         reads them there) and copy them to pinned memory behind an event instead of
         synchronising; the caller guarantees no row needs host-side logits processing."""
-        sample_items = out.decodes + [p for p in out.prefills if p.samples]
         plan = self.prepare(bm, out)
-        logits = self.run(plan)
-        if not sample_items:
-            self.last_rows = {}
-            return StepHandle([], StepOutput([], None))
-        if not overlap:
-            return StepHandle(sample_items, self.sample(logits, sample_items))
-        toks = self._sample_tokens(logits, sample_items)
-        host = self.h_tok[self._par][:len(sample_items)]
-        if self.is_gpu:
-            host.copy_(toks, non_blocking=True)
-            ev = torch.cuda.Event(blocking=_TOKEN_WAIT == "blocking")
-            ev.record()
-            return StepHandle(sample_items, host=host, event=ev)
-        host.copy_(toks)
-        return StepHandle(sample_items, host=host)
+        return self.launch_plan(plan, out, overlap)
+
+    def launch_plan(self, plan: StepPlan, out: SchedulerOutput, overlap: bool,
+                    publish=None) -> StepHandle:
+        """Device side of a prepared step on the driver (``publish`` hands the plan to the TP
+        workers first, so every rank enqueues the same work)."""
+        sample_items = out.decodes + [p for p in out.prefills if p.samples]
+        if publish is not None:
+            publish(plan)
+        try:
+            logits = self.run(plan)
+            if not sample_items:
+                self.last_rows = {}
+                return StepHandle([], StepOutput([], None))
+            if not overlap:
+                return StepHandle(sample_items, self.sample(logits, sample_items, plan))
+            toks = self._sample_tokens(logits, sample_items, plan)
+            host = self.h_tok[self._par][:len(sample_items)]
+            if self.is_gpu:
+                host.copy_(toks, non_blocking=True)
+                ev = torch.cuda.Event(blocking=_TOKEN_WAIT == "blocking")
+                ev.record()
+                return StepHandle(sample_items, host=host, event=ev)
+            host.copy_(toks)
+            return StepHandle(sample_items, host=host)
+        finally:
+            self.finish_step()
 
     @torch.no_grad()
     def execute(self, bm: BlockManager, out: SchedulerOutput) -> StepOutput:
-        sample_items = out.decodes + [p for p in out.prefills if p.samples]
-        plan = self.prepare(bm, out)
-        logits = self.run(plan)
-        if not sample_items:
-            return StepOutput([], None)
-        return self.sample(logits, sample_items)
+        return self.launch(bm, out, overlap=False).result()
+
+    @torch.no_grad()
+    def replay(self, plan: StepPlan) -> None:
+        """TP worker side of a step: same forward (the collectives pair it with the other
+        ranks) and the same sampling, into this rank's d_tok."""
+        try:
+            logits = self.run(plan)
+            if plan.n_sample and logits is not None:
+                self.sample_device(logits, plan)
+        finally:
+            self.finish_step()
 
     # ------------------------------------------------------------------ graphs
     @torch.no_grad()

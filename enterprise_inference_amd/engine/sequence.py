@@ -12,6 +12,16 @@ from .sampling_params import SamplingParams
 _seq_counter = itertools.count(1)
 
 
+def needs_host_processing(seq: "Sequence") -> bool:
+    """Rows whose sampling needs the host (penalties over the output, logits processors,
+    guided decoding, logprobs, best_of ranking): their logits are gathered in full and their
+    step is read back before the next one is planned."""
+    p = seq.params
+    return (p.needs_penalties or p.needs_logit_processing or p.logprobs is not None
+            or p.prompt_logprobs is not None or seq.guided_state is not None
+            or p.best_of > p.n)
+
+
 class SeqStatus(enum.Enum):
     WAITING = 0
     RUNNING = 1

@@ -141,6 +141,19 @@ class QKVParallelLinear(ColumnParallelLinear):
             param.data.narrow(0, off, kvn).copy_(src)
 
 
+class PendingAllReduce:
+    """Row-parallel partial sums whose TP all-reduce is deferred to the consumer: an
+    add+RMSNorm fuses it (``comm.all_reduce_add_rmsnorm``), anything else materialises."""
+
+    __slots__ = ("partial",)
+
+    def __init__(self, partial: torch.Tensor):
+        self.partial = partial
+
+    def materialize(self) -> torch.Tensor:
+        return comm.all_reduce(self.partial)
+
+
 class RowParallelLinear(nn.Module):
     """y = x W^T (+b), W split along the input dim; all-reduce of the partial sums."""
 
@@ -161,11 +174,14 @@ class RowParallelLinear(nn.Module):
         param.data.copy_(_shard(loaded, 1, state.tp_rank(), state.tp_size()))
 
     def forward(self, x, defer_reduce: bool = False):
-        """With ``defer_reduce`` (TP=1 decode) the result may be a ``gemm.SplitK``
-        whose split-K reduction (+bias) is fused into the consumer's add+RMSNorm."""
+        """With ``defer_reduce`` the consumer's add+RMSNorm absorbs the reduction: at TP=1 the
+        result may be a ``gemm.SplitK`` (split-K partials summed in the norm kernel), at TP>1
+        a ``PendingAllReduce`` (all-reduce + add + norm in one xGMI kernel)."""
         if defer_reduce and (state.tp_size() == 1 or not self.reduce_results):
             return gemm.linear(x, self.weight, self.bias, defer_reduce=True)
         y = gemm.linear(x, self.weight)
+        if defer_reduce and self.bias is None and y.dim() == 2:
+            return PendingAllReduce(y)
         if self.reduce_results:
             y = comm.all_reduce(y)
         if self.bias is not None:
@@ -232,11 +248,22 @@ class ParallelLMHead(nn.Module):
             self.weight = _param((self.per_rank, dim), dtype, device)
             self.weight.weight_loader = VocabParallelEmbedding._load.__get__(self)
 
-    def forward(self, h: torch.Tensor) -> torch.Tensor:
-        logits = gemm.linear(h, self.weight)
+    @property
+    def valid_local(self) -> int:
+        """Columns of this rank's shard that are real vocabulary (the rest is padding)."""
+        return max(0, min(self.per_rank, self.vocab - self.start))
+
+    def forward_local(self, h: torch.Tensor) -> torch.Tensor:
+        """This rank's vocab shard of the logits (no collective)."""
+        return gemm.linear(h, self.weight)
+
+    def gather(self, local: torch.Tensor) -> torch.Tensor:
         if state.tp_size() > 1:
-            logits = comm.all_gather(logits, -1)
-        return logits[..., :self.vocab]
+            local = comm.all_gather(local, -1)
+        return local[..., :self.vocab]
+
+    def forward(self, h: torch.Tensor) -> torch.Tensor:
+        return self.gather(self.forward_local(h))
 
 
 class RMSNorm(nn.Module):
@@ -248,6 +275,10 @@ class RMSNorm(nn.Module):
 
     def forward(self, x, residual=None):
         from ..ops import norm
+        if isinstance(x, PendingAllReduce):
+            if residual is not None:
+                return comm.all_reduce_add_rmsnorm(x.partial, residual, self.weight, self.eps)
+            x = x.materialize()
         if isinstance(x, gemm.SplitK):
             if residual is not None:
                 return gemm.splitk_add_rmsnorm(x, residual, self.weight, self.eps)

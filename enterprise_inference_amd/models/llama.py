@@ -147,7 +147,7 @@ class LlamaForCausalLM(nn.Module):
         for i in range(self.start_layer, self.end_layer):
             h, residual = self.layers[i](h, residual, md, kv_caches[i])
         if not self.last:
-            if isinstance(h, SplitK):
+            if hasattr(h, "materialize"):      # SplitK / PendingAllReduce
                 h = h.materialize()
             return h, residual
         h, _ = self.norm(h, residual)
@@ -155,6 +155,10 @@ class LlamaForCausalLM(nn.Module):
 
     def compute_logits(self, h: torch.Tensor) -> torch.Tensor:
         return self.lm_head(h).float()
+
+    def compute_logits_local(self, h: torch.Tensor) -> torch.Tensor:
+        """TP: this rank's vocab shard of the logits (model dtype, no gather)."""
+        return self.lm_head.forward_local(h)
 
     # ------------------------------------------------------------------ weights
     _STACKED = [

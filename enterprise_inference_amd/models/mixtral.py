@@ -27,7 +27,13 @@ import torch.nn as nn
 from ..config import ModelConfig
 from ..ops import moe as moe_ops
 from ..parallel import comm, state
-from .layers import MergedColumnParallelLinear, ReplicatedLinear, RowParallelLinear, _param
+from .layers import (MergedColumnParallelLinear, PendingAllReduce, ReplicatedLinear,
+                     RowParallelLinear, _param)
+
+
+def _deferred_reduce(out: torch.Tensor):
+    """TP>1: hand the MoE partial sums to the next add+RMSNorm (fused xGMI all-reduce)."""
+    return PendingAllReduce(out) if state.tp_size() > 1 else out
 from .llama import LlamaAttention, LlamaDecoderLayer, LlamaForCausalLM, LlamaMLP
 
 
@@ -119,14 +125,12 @@ class MixtralMoE(nn.Module):
             self.shared_expert_gate = ReplicatedLinear(H, 1, dtype=dtype, device=device)
 
     def forward(self, x):
-        out = self.experts(x, self.gate(x), reduce=self.shared_expert is None)
+        out = self.experts(x, self.gate(x), reduce=False)
         if self.shared_expert is not None:
             s = self.shared_expert(x)
             s = s.materialize() if hasattr(s, "materialize") else s
             out = out + torch.sigmoid(self.shared_expert_gate(x).float()).to(x.dtype) * s
-            if state.tp_size() > 1:
-                out = comm.all_reduce(out)
-        return out
+        return _deferred_reduce(out)
 
 
 class MixtralForCausalLM(LlamaForCausalLM):
@@ -238,10 +242,7 @@ class Llama4MoE(nn.Module):
     def forward(self, x):
         routed = self.experts(x, self.router(x), reduce=False)
         s = self.shared_expert.down_proj(self.shared_expert.gate_up_proj.forward_act_and_mul(x))
-        out = routed + s
-        if state.tp_size() > 1:
-            out = comm.all_reduce(out)
-        return out
+        return _deferred_reduce(routed + s)
 
 
 class Llama4ForCausalLM(LlamaForCausalLM):

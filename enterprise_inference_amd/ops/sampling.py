@@ -50,9 +50,10 @@ def row_seed(request_seed: int, step: int) -> int:
     return _s64(splitmix64_int((request_seed & _M64) ^ (step * 0x2545F4914F6CDD1D & _M64)))
 
 
-def uniform_t(seeds: torch.Tensor, V: int) -> torch.Tensor:
-    """[B, V] float32 uniforms in (0,1), bit-identical to rng_uniform() in the kernel."""
-    idx = torch.arange(1, V + 1, dtype=torch.int64, device=seeds.device)
+def uniform_t(seeds: torch.Tensor, V: int, offset: int = 0) -> torch.Tensor:
+    """[B, V] float32 uniforms in (0,1) for global token ids offset..offset+V-1, bit-identical
+    to rng_uniform() in the kernel."""
+    idx = torch.arange(offset + 1, offset + V + 1, dtype=torch.int64, device=seeds.device)
     h = splitmix64_t(seeds.to(torch.int64)[:, None] ^ (idx[None, :] * _CI))
     return (_lsr(h, 40).to(torch.float32) + 0.5) * (1.0 / 16777216.0)
 
@@ -73,6 +74,39 @@ def sample_reference(logits: torch.Tensor, temperature: torch.Tensor, top_k: tor
 
 
 SPLIT_CHUNK = 4096     # tokens per workgroup of the split-row sampler
+
+
+def sample_shard(logits: torch.Tensor, temperature: torch.Tensor, seeds: torch.Tensor,
+                 vocab_offset: int):
+    """Unfiltered sampling restricted to one tensor-parallel vocab shard.
+
+    logits fp32 [B, V_shard] hold global ids vocab_offset..; returns (value fp32 [B], global
+    id int32 [B]) of the shard's Gumbel-max winner (greedy rows: the plain max).  The max over
+    shards (lowest id on ties) equals ``sample(full_logits, ..., unfiltered=True)``."""
+    B, V = logits.shape
+    if not use_hip(logits):
+        l = logits.float()
+        t = temperature.float()
+        tt = torch.where(t > 0, t, torch.ones_like(t))
+        g = l / tt[:, None] - torch.log(-torch.log(uniform_t(seeds, V, vocab_offset)))
+        v = torch.where((t > 0)[:, None], g, l)
+        best_v, best_i = v.max(-1)          # first max = lowest id on ties
+        return best_v, (best_i + vocab_offset).to(torch.int32)
+    require(logits.dtype == torch.float32 and logits.stride(-1) == 1, "sample_shard: fp32")
+    C = (V + SPLIT_CHUNK - 1) // SPLIT_CHUNK
+    ws = torch.empty(2 * B * C, dtype=torch.int32, device=logits.device)
+    out_v = torch.empty(B, dtype=torch.float32, device=logits.device)
+    out_i = torch.empty(B, dtype=torch.int32, device=logits.device)
+    check(lib().eia_sample_shard(ptr(logits), logits.stride(0), B, V, SPLIT_CHUNK, vocab_offset,
+                                 ptr(temperature), ptr(seeds), ptr(ws), ws.data_ptr() + 4 * B * C,
+                                 ptr(out_v), ptr(out_i), stream(logits)), "sample_shard")
+    return out_v, out_i
+
+
+def merge_shard_winners(vals: torch.Tensor, ids: torch.Tensor) -> torch.Tensor:
+    """[W, B] shard winners (rank order = vocab order) -> [B] int32 global token ids."""
+    best = vals.argmax(0)                   # first max = lowest rank = lowest id on ties
+    return ids.gather(0, best[None, :])[0].to(torch.int32)
 
 
 def sample(logits: torch.Tensor, temperature: torch.Tensor, top_k: torch.Tensor,

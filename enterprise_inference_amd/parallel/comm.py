@@ -37,6 +37,20 @@ def all_reduce(x: torch.Tensor) -> torch.Tensor:
     return x
 
 
+def all_reduce_add_rmsnorm(x: torch.Tensor, residual: torch.Tensor, weight: torch.Tensor,
+                           eps: float):
+    """(rmsnorm(residual + allreduce(x)) * w, residual) with residual updated in place.
+
+    Decode-sized messages run the fused xGMI kernel (one launch, no HBM round trip of the
+    reduced tensor); otherwise RCCL all-reduce followed by the fused add+RMSNorm kernel."""
+    from ..ops import norm
+    ar = _CUSTOM_AR
+    if state.tp_size() > 1 and ar is not None and ar.can_fuse_norm(x) and \
+            residual.is_contiguous() and residual.dtype == x.dtype:
+        return ar.add_rmsnorm(x, residual, weight, eps), residual
+    return norm.fused_add_rms_norm(all_reduce(x), residual, weight, eps)
+
+
 def all_gather(x: torch.Tensor, dim: int = -1) -> torch.Tensor:
     ws = state.tp_size()
     if ws == 1:

@@ -89,15 +89,27 @@ class CustomAllReduce:
         dist.all_gather_object(handles, mine, group=self.cpu_group)
         self._opened = []
         sigs, datas = [], []
+        err = None
         for r, (hs, hd) in enumerate(handles):
             if r == self.rank:
                 sigs.append(sig)
                 datas.append(data)
-            else:
+                continue
+            try:
                 ps, pd = ipc_open(hs), ipc_open(hd)
-                self._opened += [ps, pd]
-                sigs.append(ps)
-                datas.append(pd)
+            except Exception as e:   # noqa: BLE001 - agreed on below, never one-sided
+                err = e
+                break
+            self._opened += [ps, pd]
+            sigs.append(ps)
+            datas.append(pd)
+        # every rank must agree before any of them switches: a rank on RCCL while its peers
+        # spin in the custom kernel would hang (or corrupt) the group
+        ok = torch.tensor([0 if err else 1], dtype=torch.int32)
+        dist.all_reduce(ok, op=dist.ReduceOp.MIN, group=self.cpu_group)
+        if int(ok.item()) == 0:
+            self.close()
+            raise RuntimeError(f"custom all-reduce unavailable on some rank ({err!r} here)")
         self._sig_arr = (ctypes.c_void_p * self.world)(*sigs)
         self._data_arr = (ctypes.c_void_p * self.world)(*datas)
         self.own_sig = sig
@@ -131,6 +143,34 @@ class CustomAllReduce:
         _native.check(rc, "custom_allreduce")
         return out
 
+    def can_fuse_norm(self, x: torch.Tensor) -> bool:
+        return (self.should_use(x) and x.dim() == 2 and x.shape[1] % 8 == 0
+                and x.shape[1] <= 16384)
+
+    def add_rmsnorm(self, x: torch.Tensor, residual: torch.Tensor, weight: torch.Tensor,
+                    eps: float, twoshot: Optional[bool] = None) -> torch.Tensor:
+        """One kernel: all-reduce x over the TP group, residual += sum (in place), returns
+        rmsnorm(residual) * weight.  Bit-identical to all_reduce + fused_add_rms_norm."""
+        T, H = x.shape
+        out = torch.empty_like(x)
+        if twoshot is None:
+            twoshot = T * H * 2 > self.oneshot_max and T >= self.world
+        rc = self.lib.eia_ar_add_rmsnorm(ctypes.cast(self._sig_arr, ctypes.c_void_p),
+                                         ctypes.cast(self._data_arr, ctypes.c_void_p), self.rank,
+                                         self.world, x.data_ptr(), residual.data_ptr(),
+                                         weight.data_ptr(), out.data_ptr(), float(eps), T, H,
+                                         self.max_bytes, int(bool(twoshot)), self.nblocks,
+                                         torch.cuda.current_stream().cuda_stream)
+        _native.check(rc, "custom_allreduce_add_rmsnorm")
+        return out
+
+    def raise_on_error(self) -> None:
+        """A barrier spin that hit its bound means a peer stalled and this rank summed stale
+        buffers: the activations are wrong from then on -- fail instead of serving them."""
+        if self.error_flag():
+            raise RuntimeError("custom all-reduce barrier timed out (a TP peer stalled); "
+                               "results since then are invalid")
+
     def error_flag(self) -> int:
         v = ctypes.c_int(0)
         _native.check(self.lib.eia_ar_read_err(ctypes.c_void_p(self.own_sig), ctypes.byref(v)),
@@ -139,6 +179,8 @@ class CustomAllReduce:
 
     def close(self) -> None:
         hip = _hiprt()
+        if hip is None:
+            return
         for p in self._opened:
             hip.hipIpcCloseMemHandle(ctypes.c_void_p(p))
         for p in self._own:

@@ -158,3 +158,85 @@ def test_allreduce_kernel_multistream(tmp_path, world):
     out = r.stdout + r.stderr
     assert r.returncode == 0, out[-3000:]
     assert "NO_SPIN_ERR BAD 0" in out, out[-3000:]
+
+
+FUSED = textwrap.dedent('''
+    import ctypes, os, sys, torch
+    sys.path.insert(0, os.environ["EIA_ROOT"])
+    from enterprise_inference_amd import _native
+    world = int(sys.argv[1])
+    lib = _native.kernels()
+    max_bytes, nblocks = 8 << 20, 16
+    own = []
+    def alloc(nb):
+        p = ctypes.c_void_p()
+        assert lib.eia_ar_alloc(ctypes.byref(p), ctypes.c_long(nb)) == 0
+        own.append(p.value)
+        return p.value
+    sigs = [alloc(lib.eia_ar_signal_bytes()) for _ in range(world)]
+    datas = [alloc(2 * max_bytes) for _ in range(world)]
+    sig_arr = (ctypes.c_void_p * world)(*sigs)
+    data_arr = (ctypes.c_void_p * world)(*datas)
+    streams = [torch.cuda.Stream() for _ in range(world)]
+    bad = 0
+    it = 0
+    for H in (4096, 5120, 8192, 16384):
+        for T in (1, 7, 65, 130):
+            for twoshot in (0, 1):
+                it += 1
+                g = torch.Generator(device="cuda").manual_seed(it)
+                base = torch.randn(world, T, H, device="cuda", generator=g).to(torch.bfloat16)
+                res0 = torch.randn(T, H, device="cuda", generator=g).to(torch.bfloat16)
+                w = (1.0 + 0.1 * torch.randn(H, device="cuda", generator=g)).to(torch.bfloat16)
+                xs = [base[r].clone() for r in range(world)]
+                rs = [res0.clone() for _ in range(world)]
+                outs = [torch.empty(T, H, device="cuda", dtype=torch.bfloat16) for _ in range(world)]
+                torch.cuda.synchronize()
+                for r in range(world):
+                    assert lib.eia_ar_add_rmsnorm(
+                        ctypes.cast(sig_arr, ctypes.c_void_p), ctypes.cast(data_arr, ctypes.c_void_p),
+                        r, world, xs[r].data_ptr(), rs[r].data_ptr(), w.data_ptr(),
+                        outs[r].data_ptr(), 1e-5, T, H, max_bytes, twoshot, nblocks,
+                        streams[r].cuda_stream) == 0
+                torch.cuda.synchronize()
+                # fp32 reference of all_reduce -> bf16 -> + residual -> bf16 -> rmsnorm
+                s = base.float().sum(0).to(torch.bfloat16).float()
+                resid = (s + res0.float()).to(torch.bfloat16).float()
+                ref = resid * torch.rsqrt(resid.pow(2).mean(-1, keepdim=True) + 1e-5) * w.float()
+                for r in range(world):
+                    e1 = (rs[r].float() - resid).abs().max().item()
+                    e2 = (outs[r].float() - ref).abs().max().item()
+                    if e1 > 0.07 * world or e2 > 0.08:
+                        print("MISMATCH", H, T, twoshot, r, e1, e2, flush=True)
+                        bad += 1
+                    if not (torch.equal(rs[r], rs[0]) and torch.equal(outs[r], outs[0])):
+                        print("RANKS DIFFER", H, T, twoshot, r, flush=True)
+                        bad += 1
+    errs = []
+    for sp in sigs:
+        v = ctypes.c_int(0)
+        assert lib.eia_ar_read_err(ctypes.c_void_p(sp), ctypes.byref(v)) == 0
+        errs.append(v.value)
+    for p in own:
+        lib.eia_ar_free(ctypes.c_void_p(p))
+    print("SPIN_ERR" if any(errs) else "NO_SPIN_ERR", "BAD", bad, flush=True)
+''')
+
+
+@pytest.mark.parametrize("world", [2, 4, 8])
+def test_allreduce_add_rmsnorm_multistream(tmp_path, world):
+    """Fused all-reduce + residual add + RMSNorm (the TP>1 o_proj/down_proj epilogue), one-shot
+    and two-shot, T x H over decode/prefill-chunk rows and 4096..16384 hidden sizes, W ranks on
+    W streams of one GPU (as the kernel test above).  Every rank must produce bit-identical
+    residual/normed rows (fixed summation order) that match the fp32 reference of the unfused
+    all_reduce -> fused_add_rms_norm pair."""
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    f = tmp_path / "fused.py"
+    f.write_text(FUSED)
+    # one hardware queue per rank stream plus the default stream: W=8 needs more than 8
+    env = dict(os.environ, EIA_ROOT=root, GPU_MAX_HW_QUEUES=str(max(8, 2 * world)))
+    r = subprocess.run([sys.executable, str(f), str(world)], env=env, capture_output=True,
+                       text=True, timeout=150)
+    out = r.stdout + r.stderr
+    assert r.returncode == 0, out[-3000:]
+    assert "NO_SPIN_ERR BAD 0" in out, out[-3000:]

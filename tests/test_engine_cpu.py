@@ -43,7 +43,8 @@ def test_parity_with_transformers(arch):
     cap = []
     r = eng.executor.runner
     orig = r._sample_tokens      # every sampling path (sync and overlapped) goes through it
-    r._sample_tokens = lambda logits, items: (cap.append(logits.clone()), orig(logits, items))[1]
+    r._sample_tokens = lambda logits, items, plan, **kw: (cap.append(logits.clone()),
+                                                          orig(logits, items, plan, **kw))[1]
     prompts = [[5, 6, 7, 8, 9] * 10, [3, 4, 5], list(range(10, 100))]
     eng.generate(prompt_token_ids=prompts, params=SamplingParams(max_tokens=1, temperature=0))
     with torch.no_grad():

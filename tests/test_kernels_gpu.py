@@ -348,6 +348,34 @@ def test_sample_split_matches_full_kernel(B, V):
     assert split.cpu().tolist() == ref.tolist()
 
 
+@pytest.mark.parametrize("B,V,W", [(65, 128256, 8), (7, 32000, 4), (300, 4097, 2)])
+def test_sample_shard_merge_equals_full_row(B, V, W):
+    """TP LM head: per-shard sampling (global-id RNG) + merge of the W (value, id) winners ==
+    the full-row split sampler; shard winners also match the CPU oracle bit for bit."""
+    from enterprise_inference_amd.ops import sampling
+    torch.manual_seed(V)
+    logits = torch.randn(B, V, device=DEV) * 4
+    temp = torch.rand(B, device=DEV) * 1.5
+    temp[::4] = 0.0
+    seeds = torch.tensor([sampling.row_seed(7 + i, 3 * i) for i in range(B)], dtype=torch.int64,
+                         device=DEV)
+    zk = torch.zeros(B, dtype=torch.int32, device=DEV)
+    ones = torch.ones(B, device=DEV)
+    zp = torch.zeros(B, device=DEV)
+    full = sampling.sample(logits, temp, zk, ones, zp, seeds, unfiltered=True)
+    per = (V + W - 1) // W
+    vals, ids = [], []
+    for r in range(W):
+        lo, hi = r * per, min(V, (r + 1) * per)
+        v, i = sampling.sample_shard(logits[:, lo:hi].contiguous(), temp, seeds, lo)
+        rv, ri = sampling.sample_shard(logits[:, lo:hi].cpu(), temp.cpu(), seeds.cpu(), lo)
+        assert i.cpu().tolist() == ri.tolist()
+        vals.append(v)
+        ids.append(i)
+    got = sampling.merge_shard_winners(torch.stack(vals), torch.stack(ids))
+    assert got.cpu().tolist() == full.cpu().tolist()
+
+
 def test_fill_ids():
     from enterprise_inference_amd.ops import sampling
     ids = torch.tensor([5, 6, 7, 8, 9], dtype=torch.int32, device=DEV)

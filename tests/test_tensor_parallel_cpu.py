@@ -30,7 +30,7 @@ def _ckpt(tmp_path, d):
     return str(tmp_path)
 
 
-def _run(path, d, tp, ep=False, pp=1):
+def _run(path, d, tp, ep=False, pp=1, temperature=0.0):
     cfg = EngineConfig(model=ModelConfig.from_hf_dict(d), model_path=path,
                        cache=CacheConfig(block_size=16, num_gpu_blocks=64),
                        scheduler=SchedulerConfig(max_num_seqs=4, max_num_batched_tokens=40,
@@ -41,8 +41,8 @@ def _run(path, d, tp, ep=False, pp=1):
     eng = LLMEngine(cfg)
     try:
         prompts = [[5, 6, 7, 8, 9, 10] * 8, [11, 12, 13], list(range(40, 90))]
-        outs = eng.generate(prompt_token_ids=prompts,
-                            params=SamplingParams(max_tokens=6, temperature=0, ignore_eos=True))
+        params = SamplingParams(max_tokens=6, temperature=temperature, ignore_eos=True, seed=11)
+        outs = eng.generate(prompt_token_ids=prompts, params=params)
         return [o.outputs[0].token_ids for o in outs]
     finally:
         eng.shutdown()
@@ -58,6 +58,28 @@ def test_tp2_matches_tp1(tmp_path, arch, ep):
     ref = _run(path, d, 1)
     got = _run(path, d, 2, ep)
     assert got == ref
+
+
+@pytest.mark.parametrize("arch,tp,ep", [("LlamaForCausalLM", 4, False), ("LlamaForCausalLM", 8, False),
+                                        ("Qwen2ForCausalLM", 4, False),
+                                        ("MixtralForCausalLM", 4, True),
+                                        ("MixtralForCausalLM", 8, True)])
+def test_tp4_tp8_match_tp1(tmp_path, arch, tp, ep):
+    """BASELINE config #3 runs TP=8: 8 heads / 2 KV heads (KV heads replicated over ranks),
+    vocab-sharded embedding + LM head, 8 experts spread over the EP group."""
+    d = tiny_config(arch, num_local_experts=8) if arch.startswith("Mixtral") else tiny_config(arch)
+    path = _ckpt(tmp_path, d)
+    assert _run(path, d, tp, ep) == _run(path, d, 1)
+
+
+def test_tp_sharded_sampling_matches_full_row(tmp_path):
+    """Seeded temperature sampling at TP=2 samples each vocab shard (global-id-keyed RNG) and
+    exchanges only (value, id) pairs: the tokens equal the TP=1 full-row sampler's."""
+    d = tiny_config("LlamaForCausalLM")
+    path = _ckpt(tmp_path, d)
+    ref = _run(path, d, 1, temperature=0.8)
+    assert _run(path, d, 2, temperature=0.8) == ref
+    assert len(set(map(tuple, ref))) > 1
 
 
 @pytest.mark.parametrize("arch,tp,pp,layers", [("LlamaForCausalLM", 1, 2, 3),
