@@ -191,9 +191,13 @@ def _visible_devices(first: int, n: int) -> str:
 
 
 def start_server(args, local_rank: int, port: int, log_path: str) -> subprocess.Popen:
+    # the server runs its own process groups: drop every torchrun / elastic-agent variable
+    # (TORCHELASTIC_USE_AGENT_STORE would make its rank 0 wait for an agent-hosted store)
     env = {k: v for k, v in os.environ.items()
            if k not in ("RANK", "LOCAL_RANK", "WORLD_SIZE", "LOCAL_WORLD_SIZE", "GROUP_RANK",
-                        "ROLE_RANK", "MASTER_ADDR", "MASTER_PORT", "TORCHELASTIC_RUN_ID")}
+                        "GROUP_WORLD_SIZE", "ROLE_RANK", "ROLE_NAME", "ROLE_WORLD_SIZE",
+                        "MASTER_ADDR", "MASTER_PORT")
+           and not k.startswith("TORCHELASTIC_")}
     env["HIP_VISIBLE_DEVICES"] = _visible_devices(local_rank, args.tp)
     env.pop("CUDA_VISIBLE_DEVICES", None)
     env["PYTHONPATH"] = ROOT + os.pathsep + env.get("PYTHONPATH", "")

@@ -109,6 +109,7 @@ def _spawned_worker(cfg: EngineConfig, rank: int, world: int, port: int, ring_na
                     driver_pid: int) -> None:
     os.environ.update(RANK=str(rank), WORLD_SIZE=str(world), LOCAL_RANK=str(rank),
                       MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    os.environ.pop("TORCHELASTIC_USE_AGENT_STORE", None)
     if cfg.device == "cuda" and torch.cuda.device_count() > 0:
         torch.cuda.set_device(rank)
     pstate.init_distributed(cfg.parallel.tensor_parallel_size,
@@ -148,6 +149,7 @@ class TPExecutor:
                 self.procs.append(p)
             os.environ.update(RANK="0", WORLD_SIZE=str(tp), LOCAL_RANK="0",
                               MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+            os.environ.pop("TORCHELASTIC_USE_AGENT_STORE", None)   # this rank hosts the store
             if cfg.device == "cuda" and torch.cuda.device_count() > 0:
                 torch.cuda.set_device(0)
             pstate.init_distributed(cfg.parallel.tensor_parallel_size,

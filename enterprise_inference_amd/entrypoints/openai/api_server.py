@@ -210,7 +210,8 @@ def build_from_args(args, engine_mode: Optional[str] = None, wait_ready: bool = 
     if mode == "process":
         from ...engine.core_proc import MPEngineClient
         env = {k: v for k, v in os.environ.items()
-               if k not in ("RANK", "LOCAL_RANK", "WORLD_SIZE", "MASTER_ADDR", "MASTER_PORT")}
+               if k not in ("RANK", "LOCAL_RANK", "WORLD_SIZE", "MASTER_ADDR", "MASTER_PORT")
+               and not k.startswith("TORCHELASTIC_")}
         aengine = MPEngineClient(cfg, metrics, log_requests=not args.disable_log_requests,
                                  env=env)
     else:
