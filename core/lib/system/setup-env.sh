@@ -26,9 +26,13 @@ setup_initial_env() {
     mkdir -p "$KUBESPRAYDIR/config/vars"
     cp "$CORE_DIR"/inventory/metadata/vars/*.yml "$KUBESPRAYDIR/config/vars/"
     local vault="$KUBESPRAYDIR/config/vault.yml"
+    # the reference's mandatory keys (its setup-env.sh:108-129) plus this stack's additions
     local required=(litellm_master_key litellm_salt_key redis_password langfuse_secret_key \
-                    langfuse_public_key postgresql_password clickhouse_password minio_secret \
-                    grafana_admin_password)
+                    langfuse_public_key postgresql_username postgresql_password \
+                    clickhouse_username clickhouse_password langfuse_login langfuse_user \
+                    langfuse_password minio_secret minio_user postgres_user postgres_password \
+                    grafana_admin_password langfuse_salt langfuse_nextauth_secret \
+                    langfuse_encryption_key valkey_password keycloak_db_password)
     local regenerate=false
     for k in "${required[@]}"; do
         grep -q "^${k}:" "$vault" 2>/dev/null || regenerate=true

@@ -183,3 +183,151 @@ def test_multi_node_example():
                 if "=" in l}
     ex_keys = {l.split("=")[0] for l in open(os.path.join(d, "inference-config.cfg")) if "=" in l}
     assert ex_keys == cfg_keys
+
+
+# --------------------------------------------------------------------------- variable wiring
+
+def _checker():
+    sys.path.insert(0, os.path.join(os.path.dirname(ROOT), "scripts"))
+    import check_playbook_vars
+    return check_playbook_vars
+
+
+def test_every_playbook_renders_with_strict_undefined():
+    """Every play's Jinja (tasks, included task files, roles, role templates, the Langfuse
+    values template) renders against group vars + vars files + the GENERATED vault + the
+    --extra-vars the CLI passes that playbook, with StrictUndefined."""
+    ch = _checker().Checker(ROOT)
+    for pb in sorted(glob.glob(os.path.join(ROOT, "playbooks/*.yml"))):
+        ch.check_playbook(pb)
+    assert ch.errors == [], "\n".join(ch.errors)
+
+
+def test_strict_render_catches_a_missing_vault(tmp_path):
+    """The round-1 bug: the gateway play used vault secrets without loading the vault."""
+    core = tmp_path / "core"
+    shutil.copytree(ROOT, core)
+    pb = core / "playbooks/deploy-genai-gateway.yml"
+    pb.write_text(pb.read_text().replace("    - ../config/vault.yml\n", ""))
+    ch = _checker().Checker(str(core))
+    ch.check_playbook(str(pb))
+    assert any("litellm_master_key" in e for e in ch.errors), ch.errors
+
+
+def _keys(d, prefix=""):
+    out = set()
+    for k, v in d.items():
+        out.add(prefix + k)
+        if isinstance(v, dict):
+            out |= _keys(v, prefix + k + ".")
+    return out
+
+
+def test_gateway_play_values_exist_in_chart():
+    """Every value the play passes to the genai-gateway chart is a key the chart defines
+    (round 1 passed masterKey / postgres.password to a chart reading masterkey / postgresql)."""
+    chart = yaml.safe_load(open(os.path.join(ROOT, "helm-charts/genai-gateway/values.yaml")))
+    play = yaml.safe_load(open(os.path.join(ROOT, "playbooks/deploy-genai-gateway.yml")))[0]
+    task = next(t for t in play["tasks"] if t.get("name") == "Gateway chart")
+    passed = _keys(task["kubernetes.core.helm"]["values"])
+    missing = sorted(k for k in passed if k not in _keys(chart))
+    assert missing == [], missing
+    tmpl = open(os.path.join(ROOT, "helm-charts/genai-gateway/templates/deployment.yaml")).read()
+    assert "wait-for-postgres-restore" in tmpl and "kubectl" in tmpl
+    restore = open(os.path.join(ROOT, "helm-charts/genai-gateway/templates/postgres-restore-job.yaml")).read()
+    assert "n_live_tup" in restore       # restores only into an empty database
+
+
+def test_vault_generator_has_reference_keys(tmp_path):
+    out = tmp_path / "vault.yml"
+    subprocess.run(["bash", os.path.join(ROOT, "scripts/generate-vault-secrets.sh"), str(out)],
+                   check=True, capture_output=True)
+    v = yaml.safe_load(out.read_text())
+    ref = ["litellm_master_key", "litellm_salt_key", "redis_password", "langfuse_secret_key",
+           "langfuse_public_key", "postgresql_username", "postgresql_password",
+           "clickhouse_username", "clickhouse_password", "langfuse_login", "langfuse_user",
+           "langfuse_password", "minio_secret", "minio_user", "postgres_user", "postgres_password",
+           "grafana_admin_password"]
+    assert all(v.get(k) for k in ref), [k for k in ref if not v.get(k)]
+    assert oct(out.stat().st_mode & 0o777) == "0o600"
+
+
+def _topology_mod():
+    import importlib.util
+    spec = importlib.util.spec_from_file_location(
+        "topology", os.path.join(ROOT, "roles/utils/get_optimized_cpu_topology/files/topology.py"))
+    m = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(m)
+    return m
+
+
+def _topo(sockets, numa_per_socket, cpus_per_numa, free_gb_per_numa, amx=False):
+    numa, c = [], 0
+    for s in range(sockets):
+        for j in range(numa_per_socket):
+            numa.append({"node": s * numa_per_socket + j, "socket": s,
+                         "cpus": list(range(c, c + cpus_per_numa)),
+                         "mem_total_kb": int(free_gb_per_numa * 1.2 * 1048576),
+                         "mem_free_kb": int(free_gb_per_numa * 1048576), "gpus": []})
+            c += cpus_per_numa
+    return {"numa": numa, "sockets": sockets, "amx": amx, "avx512": True, "avx2": True}
+
+
+@pytest.mark.parametrize("sockets,nps,want_tp,want_pp", [(2, 2, 2, 2), (2, 3, 2, 2), (1, 4, 4, 1),
+                                                          (2, 6, 4, 2), (1, 1, 1, 1), (2, 1, 1, 2)])
+def test_cpu_topology_plan_rules(sockets, nps, want_tp, want_pp):
+    """Reference rules (get_optimized_cpu_topology.yaml:407-420, :503-521): TP from NUMA nodes
+    per socket, 18 % of a socket's CPUs reserved (>= 2, <= half), 82 % of free memory."""
+    t = _topology_mod()
+    p = t.plan(_topo(sockets, nps, 24, 100.0, amx=True))
+    cps = 24 * nps
+    assert p["tensor_parallel_size"] == want_tp and p["pipeline_parallel_size"] == want_pp
+    reserved = max(2, min(-(-cps * 18 // 100), cps // 2))
+    assert p["reserved_cpus_per_socket"] == reserved
+    expect_balloon = (cps - reserved) // 2 if (sockets == 1 and nps == 1) else cps - reserved
+    assert p["balloon_cpus"] == expect_balloon
+    assert p["memory_gi"] == int(100.0 * nps * 0.82)
+    assert p["isa"] == "amx"
+    assert len(p["reserved_cpuset"].split(",")) == reserved * sockets
+
+
+def test_topology_probe_reads_sysfs(tmp_path):
+    """probe() on a synthetic /sys + /proc tree (2 NUMA nodes, one MI355X on node 1)."""
+    t = _topology_mod()
+    for n, cpus in ((0, "0-3"), (1, "4-7")):
+        d = tmp_path / f"sys/devices/system/node/node{n}"
+        d.mkdir(parents=True)
+        (d / "cpulist").write_text(cpus)
+        (d / "meminfo").write_text(f"Node {n} MemTotal: 1048576 kB\nNode {n} MemFree: 524288 kB\n")
+    for c in range(8):
+        d = tmp_path / f"sys/devices/system/cpu/cpu{c}/topology"
+        d.mkdir(parents=True)
+        (d / "physical_package_id").write_text("0")
+        (d / "thread_siblings_list").write_text(str(c))
+    g = tmp_path / "sys/bus/pci/devices/0000:05:00.0"
+    g.mkdir(parents=True)
+    (g / "vendor").write_text("0x1002")
+    (g / "class").write_text("0x120000")
+    (g / "numa_node").write_text("1")
+    (tmp_path / "proc").mkdir()
+    (tmp_path / "proc/cpuinfo").write_text("flags : fpu avx2 avx512f\n")
+    topo = t.probe(str(tmp_path))
+    assert [len(n["cpus"]) for n in topo["numa"]] == [4, 4]
+    assert topo["numa"][1]["gpus"] == ["0000:05:00.0"] and topo["avx512"]
+    p = t.plan(topo)
+    assert p["tensor_parallel_size"] == 2 and p["gpu_numa"] == {"1": ["0000:05:00.0"]}
+
+
+def test_nri_balloon_matches_vllm_pods():
+    import jinja2
+    tmpl = open(os.path.join(ROOT, "roles/nri_cpu_balloons/templates/balloons-values.yaml.j2")).read()
+    d = yaml.safe_load(open(os.path.join(ROOT, "roles/nri_cpu_balloons/defaults/main.yml")))
+    out = jinja2.Environment(undefined=jinja2.StrictUndefined).from_string(tmpl).render(
+        cpu_parallelism={"balloon_cpus": 40, "reserved_cpuset": "0,1,2,3"}, **d)
+    cfg = yaml.safe_load(out)["config"]
+    bt = cfg["balloonTypes"][0]
+    assert bt["name"] == "vllm-balloon" and bt["minCPUs"] == 40
+    assert bt["matchExpressions"] == [{"key": "name", "operator": "In", "values": ["vllm"]}]
+    assert cfg["reservedResources"]["cpu"] == "cpuset:0,1,2,3"
+    dep = open(os.path.join(ROOT, "helm-charts/vllm/templates/deployment.yaml")).read()
+    assert "name: vllm" in dep           # the pod label the balloon matches
