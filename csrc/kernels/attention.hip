@@ -16,6 +16,7 @@
 #include <cstdlib>
 
 #include "eia_common.h"
+#include "eia_rope.h"
 
 #define NEG_INF (-INFINITY)
 #ifndef EIA_LEAN_OCC
@@ -246,14 +247,23 @@ EIA_DEV void compute_unit(WaveAcc<D>& acc, const bf16x8 (&qf)[D / 32], const KVF
 // bases are wave-uniform (one scalar block-table read) and each lane adds a CONSTANT 32-bit
 // byte offset, so the loads take the SGPR-base + VGPR-offset form -- no per-unit 64-bit
 // per-lane pointers held in VGPRs.
-template <int D>
+// `pre` runs once per wave between the first unit's loads and the loop (every wave calls it,
+// also those without units): the fused decode prologue (RoPE, KV write, q -> LDS, barrier)
+// then overlaps the first K/V fetch.  Token `tnew` (this step's, -1: none) is taken from
+// knew / vnew in LDS instead of the cache: its K/V stores may still be in flight when the unit
+// holding it is read, so those lanes' fragments are patched after the loads land.
+template <int D, typename Pre>
 EIA_DEV void attn_units_lean(WaveAcc<D>& acc, const bf16x8 (&qs)[D / 32][64],
                              const bf16_t* __restrict__ kc, const bf16_t* __restrict__ vc,
                              const int* __restrict__ bt, int ub, int ue, int w, int L, int kvh,
-                             int Hkv, int bs, float scale_log2, int kv_lo, int NW) {
+                             int Hkv, int bs, float scale_log2, int kv_lo, int NW, Pre&& pre,
+                             int tnew, const bf16_t* knew, const bf16_t* vnew) {
   // the unit index is wave-uniform; say so, or the per-unit bases become 64-bit VGPR pointers
   int u = __builtin_amdgcn_readfirstlane(ub + w);
-  if (u >= ue) return;
+  if (u >= ue) {
+    pre();
+    return;
+  }
   const int lane = threadIdx.x & 63;
   const int c = lane & 15, g = lane >> 4;
   const long hk = (long)bs * D;
@@ -288,11 +298,35 @@ EIA_DEV void attn_units_lean(WaveAcc<D>& acc, const bf16x8 (&qs)[D / 32][64],
     ldk(ka0, ka1, kbp);
     ldv(va, vbp);
   }
+  pre();
+  // lanes holding token tnew of unit uc take it from LDS (wave-uniform test)
+  auto patch = [&](bf16x8 (&k0)[D / 32], bf16x8 (&k1)[D / 32], bf16x8 (&v)[D / 16], int uc) {
+    const int o = tnew - 32 * uc;
+    if (o < 0 || o >= 32) return;
+    const int tr0 = 8 * (c >> 2) + (c & 3);
+    if (tr0 == o || tr0 + 4 == o) {
+#pragma unroll
+      for (int s2 = 0; s2 < D / 32; ++s2) {
+        const bf16x8 kn = *reinterpret_cast<const bf16x8*>(knew + 8 * g + 32 * s2);
+        if (tr0 == o) k0[s2] = kn; else k1[s2] = kn;
+      }
+    }
+    if (g == (o >> 3)) {
+#pragma unroll
+      for (int dt = 0; dt < D / 16; ++dt) {
+        const bf16_t x = vnew[16 * dt + c];
+#pragma unroll
+        for (int j = 0; j < 8; ++j)
+          if (j == (o & 7)) v[dt][j] = x;
+      }
+    }
+  };
   // one unit: K(next) -> QK(cur) -> V(next) -> softmax + PV(cur); named sets a/b alternate
   auto step = [&](bf16x8 (&kc0)[D / 32], bf16x8 (&kc1)[D / 32], bf16x8 (&vcur)[D / 16],
                   bf16x8 (&kn0)[D / 32], bf16x8 (&kn1)[D / 32], bf16x8 (&vn)[D / 16], int uc) {
     const char *kbp, *vbp;
     bases(min(uc + NW, ue - 1), kbp, vbp);
+    patch(kc0, kc1, vcur, uc);
     f32x4 s0, s1;
     {
       bf16x8 qf[D / 32];
@@ -358,17 +392,33 @@ EIA_DEV void attn_units_pipelined(WaveAcc<D>& acc, const bf16x8 (&qf)[D / 32],
 // 4 waves per workgroup.  LEAN: the attn_units_lean pipeline at 3 workgroups per CU (D <= 128);
 // otherwise two full K/V fragment sets at 2 per CU.  (A 2-wave form with 4 per CU measured
 // 1.9-2.2x slower at B = 16..65: each wave walks twice the units.)
-template <int D, bool LEAN>
+//
+// FUSED (LEAN only, G <= 16): the K4 prologue runs here instead of in rope_qkv_cache_kernel --
+// the workgroup reduces its own q heads and its KV head's k / v from the QKV GEMM's split-K
+// slabs (or bf16 rows), applies bias / qk-norm / RoPE, keeps q in LDS (never written to HBM)
+// and, in the partition that owns the last unit, writes this step's k / v into the paged cache
+// for later steps while its own unit loop takes the token from LDS (no wait for the stores;
+// the first K/V units are already in flight during the prologue).  This removes one launch and
+// the q round trip per layer (profiles/rocprof_r2_kernel_stats.md).
+struct DecodeRope {
+  QkvSrc src;
+  const int* positions;
+  const float* cos_sin;
+  const int* slot_mapping;
+};
+
+template <int D, bool LEAN, bool FUSED, bool SPLIT, bool QK_NORM, bool HAS_BIAS>
 __global__ void __launch_bounds__(256, D <= 128 ? (LEAN ? EIA_LEAN_OCC : 2) : 1)
 paged_decode_kernel(const bf16_t* __restrict__ q, long q_stride,
-                    const bf16_t* __restrict__ kc, const bf16_t* __restrict__ vc,
+                    const bf16_t* kc, const bf16_t* vc,
                     const int* __restrict__ block_tables, int bt_stride,
                     const int* __restrict__ seq_lens,
                     bf16_t* __restrict__ out, long out_stride,
                     float* __restrict__ part_o, float* __restrict__ part_ml,
                     int* __restrict__ part_cnt,
                     float scale_log2, int Hq, int Hkv, int bs, int Pmax, int NQG,
-                    int sliding_window, int chunk_size, const int* __restrict__ p_dyn) {
+                    int sliding_window, int chunk_size, const int* __restrict__ p_dyn,
+                    DecodeRope rope) {
   constexpr int NW = 4;
   __shared__ int s_last;
   __shared__ float sm[NW][16];
@@ -392,7 +442,7 @@ paged_decode_kernel(const bf16_t* __restrict__ q, long q_stride,
   const int c = lane & 15, g = lane >> 4;
 
   bf16x8 qf[D / 32];
-  {
+  if constexpr (!FUSED) {
     const bool cval = c < nq;
     const bf16_t* qp = q + (long)b * q_stride + (long)(hq0 + (cval ? c : 0)) * D + 8 * g;
 #pragma unroll
@@ -411,19 +461,65 @@ paged_decode_kernel(const bf16_t* __restrict__ q, long q_stride,
   int kv_lo = 0;
   if (L > 0 && sliding_window > 0) kv_lo = max(kv_lo, L - sliding_window);
   if (L > 0 && chunk_size > 0) kv_lo = max(kv_lo, ((L - 1) / chunk_size) * chunk_size);
+  // units [U0, U0 + U), split over the P partitions at even (64-token) unit boundaries
   const int U0 = kv_lo / 32;
   const int U = (L + 31) / 32 - U0;
-  const int ub = U0 + (int)(((long)p * U) / P), ue = U0 + (int)(((long)(p + 1) * U) / P);
+  const int A0 = U0 & ~1;
+  const int npair = (U0 + U - A0 + 1) / 2;
+  const int ub = max(U0, A0 + 2 * (int)(((long)p * npair) / P));
+  const int ue = min(U0 + U, A0 + 2 * (int)(((long)(p + 1) * npair) / P));
   const int* bt = block_tables + (long)b * bt_stride;
   if constexpr (LEAN) {
-    // Q fragments through LDS (one copy, re-read per unit): 16 fewer live VGPRs outside QK
+    // Q fragments through LDS (one copy, re-read per unit): 16 fewer live VGPRs outside QK.
+    // qs[s][16 g + c] = q head c, dims [32 s + 8 g, +8)
     __shared__ bf16x8 qs[D / 32][64];
-    if (w == 0) {
+    if constexpr (FUSED) {
+      constexpr int TPH = D / 16;
+      const int hs = threadIdx.x / TPH, sub = threadIdx.x % TPH;
+      const bool act = hs < nq + 2;
+      const int h = hs < nq ? hq0 + hs : (hs == nq ? Hq + kvh : Hq + Hkv + kvh);
+      const bool writer = p == P - 1 && qg == 0;
+      __shared__ __align__(16) bf16_t knew[D], vnew[D];
+      auto prologue = [&]() {
+        // zero the unused query columns (c >= nq); the RoPE lanes write the others
+        for (int i = threadIdx.x; i < (D / 32) * 64; i += 256)
+          if ((i & 15) >= nq) qs[i >> 6][i & 63] = bf16x8{};
+        float a[8], bv[8];
+        rope_lane_values<D, true, QK_NORM, HAS_BIAS, SPLIT>(rope.src, b, act ? h : 0, act, sub,
+                                                           Hq, Hkv, rope.cos_sin,
+                                                           rope.positions[b], a, bv);
+        if (act) {
+          bf16x8 oa, ob;
 #pragma unroll
-      for (int s = 0; s < D / 32; ++s) qs[s][lane] = qf[s];
+          for (int j = 0; j < 8; ++j) { oa[j] = f2bf(a[j]); ob[j] = f2bf(bv[j]); }
+          int e0, e1;
+          rope_lane_offsets<D, true>(sub, e0, e1);
+          if (hs < nq) {
+            qs[e0 / 32][16 * ((e0 % 32) / 8) + hs] = oa;
+            qs[e1 / 32][16 * ((e1 % 32) / 8) + hs] = ob;
+          } else if (writer) {
+            bf16_t* nw = hs == nq ? knew : vnew;
+            *reinterpret_cast<bf16x8*>(nw + e0) = oa;
+            *reinterpret_cast<bf16x8*>(nw + e1) = ob;
+            const int slot = rope.slot_mapping[b];
+            if (slot >= 0)   // for later steps; this one reads the token from LDS
+              rope_lane_store_kv<D, true>(const_cast<bf16_t*>(kc), const_cast<bf16_t*>(vc), slot,
+                                          bs, Hkv, kvh, hs == nq + 1, sub, oa, ob);
+          }
+        }
+        __syncthreads();
+      };
+      attn_units_lean<D>(acc, qs, kc, vc, bt, ub, ue, w, L, kvh, Hkv, bs, scale_log2, kv_lo, NW,
+                         prologue, writer && L > 0 ? L - 1 : -1, knew, vnew);
+    } else {
+      if (w == 0) {
+#pragma unroll
+        for (int s = 0; s < D / 32; ++s) qs[s][lane] = qf[s];
+      }
+      __syncthreads();
+      attn_units_lean<D>(acc, qs, kc, vc, bt, ub, ue, w, L, kvh, Hkv, bs, scale_log2, kv_lo, NW,
+                         [] {}, -1, nullptr, nullptr);
     }
-    __syncthreads();
-    attn_units_lean<D>(acc, qs, kc, vc, bt, ub, ue, w, L, kvh, Hkv, bs, scale_log2, kv_lo, NW);
   } else
     attn_units_pipelined<D>(acc, qf, kc, vc, bt, ub, ue, w, L, kvh, Hkv, bs, scale_log2, kv_lo, NW);
 
@@ -855,6 +951,14 @@ paged_prefill_lds_kernel(const bf16_t* __restrict__ q, long q_stride,
 
 // ---------------------------------------------------------------------------------- launchers
 
+static int decode_lean_env() {
+  static const int v = [] {
+    const char* e = getenv("EIA_DECODE_LEAN");
+    return e != nullptr ? atoi(e) : -1;
+  }();
+  return v;
+}
+
 EIA_API int eia_paged_decode(const void* q, long q_stride, const void* k_cache, const void* v_cache,
                              const int* block_tables, int bt_stride, const int* seq_lens,
                              void* out, long out_stride, float* part_o, float* part_ml,
@@ -867,18 +971,17 @@ EIA_API int eia_paged_decode(const void* q, long q_stride, const void* k_cache, 
   const int G = Hq / Hkv;
   const int NQG = (G + 15) / 16;
   const float sl2 = scale * 1.4426950408889634f;
-  static const int lean_env = [] {
-    const char* e = getenv("EIA_DECODE_LEAN");
-    return e != nullptr ? atoi(e) : -1;
-  }();
+  const int lean_env = decode_lean_env();
   // lean form: whole 32-token units inside a block (bs % 32 == 0), uniform per-unit bases
   const bool lean = (lean_env >= 0 ? lean_env != 0 : true) && bs % 32 == 0 && D <= 128;
   dim3 grid(B, Hkv * NQG, P);
+  const DecodeRope none{};
 #define DEC_V(DD, LEAN_)                                                                     \
-  hipLaunchKernelGGL((paged_decode_kernel<DD, LEAN_>), grid, dim3(256), 0, st, (const bf16_t*)q, \
-                     q_stride, (const bf16_t*)k_cache, (const bf16_t*)v_cache, block_tables,      \
-                     bt_stride, seq_lens, (bf16_t*)out, out_stride, part_o, part_ml, part_cnt, sl2, \
-                     Hq, Hkv, bs, P, NQG, sliding_window, chunk_size, p_dyn);
+  hipLaunchKernelGGL((paged_decode_kernel<DD, LEAN_, false, false, false, false>), grid, dim3(256), \
+                     0, st, (const bf16_t*)q, q_stride, (const bf16_t*)k_cache,                \
+                     (const bf16_t*)v_cache, block_tables, bt_stride, seq_lens, (bf16_t*)out,     \
+                     out_stride, part_o, part_ml, part_cnt, sl2, Hq, Hkv, bs, P, NQG,             \
+                     sliding_window, chunk_size, p_dyn, none);
 #define DEC(DD)                                                                             \
   if (lean) { DEC_V(DD, true) } else { DEC_V(DD, false) }                                  \
   if (P > 1 && part_cnt == nullptr)                                                         \
@@ -892,6 +995,56 @@ EIA_API int eia_paged_decode(const void* q, long q_stride, const void* k_cache, 
   }
 #undef DEC
 #undef DEC_V
+  EIA_LAUNCH_CHECK();
+}
+
+// Fused K4 + K1 for pure-decode steps (see paged_decode_kernel FUSED): q/k/v come from the QKV
+// GEMM output of T >= B rows (split-K slabs `part` [sk][T][(Hq+2Hkv)*D], or bf16 rows `qkv`),
+// this step's k/v land in the cache, out [B][Hq*D] receives the attention.  NEOX RoPE only.
+// Returns EIA_UNSUPPORTED for shapes the fused form does not cover (the caller then runs the
+// two kernels).
+EIA_API int eia_paged_decode_rope(const void* qkv, long qkv_stride, const float* part, int sk,
+                                  const void* bias, const void* q_norm_w, const void* k_norm_w,
+                                  float eps, const int* positions, const float* cos_sin,
+                                  const int* slot_mapping, int T, void* k_cache, void* v_cache,
+                                  const int* block_tables, int bt_stride, const int* seq_lens,
+                                  void* out, long out_stride, float* part_o, float* part_ml,
+                                  int* part_cnt, float scale, int B, int Hq, int Hkv, int D, int bs,
+                                  int P, int sliding_window, int chunk_size, const int* p_dyn,
+                                  hipStream_t st) {
+  if (B < 0 || B > T || Hkv <= 0 || Hq % Hkv != 0 || P < 1) return EIA_BAD_SHAPE;
+  if (P > 1 && (part_o == nullptr || part_ml == nullptr)) return EIA_BAD_SHAPE;
+  if ((q_norm_w == nullptr) != (k_norm_w == nullptr)) return EIA_BAD_SHAPE;
+  if ((part == nullptr) == (qkv == nullptr) || (part != nullptr && sk < 1)) return EIA_BAD_SHAPE;
+  const int G = Hq / Hkv;
+  const int lean_env = decode_lean_env();
+  if (G > 16 || bs % 32 != 0 || !(D == 64 || D == 128) || cos_sin == nullptr ||
+      positions == nullptr || slot_mapping == nullptr || lean_env == 0)
+    return EIA_UNSUPPORTED;
+  if (B == 0) return EIA_OK;
+  const float sl2 = scale * 1.4426950408889634f;
+  const DecodeRope rope{QkvSrc{(const bf16_t*)qkv, qkv_stride, part, sk,
+                               (long)T * (Hq + 2 * Hkv) * D, (const bf16_t*)bias,
+                               (const bf16_t*)q_norm_w, (const bf16_t*)k_norm_w, eps},
+                        positions, cos_sin, slot_mapping};
+  dim3 grid(B, Hkv, P);
+#define DEC_F(DD, SP, QN, HB)                                                                    \
+  hipLaunchKernelGGL((paged_decode_kernel<DD, true, true, SP, QN, HB>), grid, dim3(256), 0, st,  \
+                     nullptr, 0L, (const bf16_t*)k_cache, (const bf16_t*)v_cache, block_tables,  \
+                     bt_stride, seq_lens, (bf16_t*)out, out_stride, part_o, part_ml, part_cnt,    \
+                     sl2, Hq, Hkv, bs, P, 1, sliding_window, chunk_size, p_dyn, rope);
+#define DEC_FQ(DD, SP)                                                                           \
+  if (q_norm_w) { if (bias) { DEC_F(DD, SP, true, true) } else { DEC_F(DD, SP, true, false) } }  \
+  else { if (bias) { DEC_F(DD, SP, false, true) } else { DEC_F(DD, SP, false, false) } }
+#define DEC_FD(DD)                                                                               \
+  if (part != nullptr) { DEC_FQ(DD, true) } else { DEC_FQ(DD, false) }                          \
+  if (P > 1 && part_cnt == nullptr)                                                              \
+    hipLaunchKernelGGL((paged_decode_reduce_kernel<DD>), dim3(B, Hq), dim3(DD), 0, st, part_o,    \
+                       part_ml, (bf16_t*)out, out_stride, Hq, P, p_dyn);
+  if (D == 128) { DEC_FD(128) } else { DEC_FD(64) }
+#undef DEC_FD
+#undef DEC_FQ
+#undef DEC_F
   EIA_LAUNCH_CHECK();
 }
 

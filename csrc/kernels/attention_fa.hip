@@ -1,0 +1,241 @@
+// K2 (long prompts): paged flash-attention prefill on v_mfma_f32_32x32x16_bf16, D = 128.
+//
+// Work split: a workgroup of 8 waves owns one 64-query block of one sequence for FOUR query
+// heads of one KV group (wave w: head 4*hg + (w & 3), queries q0 + 32*(w >> 2) + [0, 32)), so
+// every 64-key K/V tile staged in LDS feeds 256 query rows (the GQA group shares it).
+//
+// Per wave and tile (swapped products, guide §3 "An accumulator tile as the next MFMA's
+// operand"):
+//   S^T[key, q] = K Q^T   : A = K rows from LDS, B = Q^T fragments held in registers,
+//                           2 x 8 MFMAs (two 32-key halves x 8 k-steps of 16 dims)
+//   O^T[d, q]  += V^T P^T : A = V^T rows from LDS, B = P^T taken straight from the S^T
+//                           accumulators (no LDS round trip, no lane movement), 4 x 4 MFMAs
+// Each lane owns ONE query column q = lane & 31 of S^T and O^T, so the online softmax (max,
+// exp2, running sum, O rescale) is lane-local but for one xor-32 shuffle per tile.
+// Key order: accumulator element j of lane half h in k-step s is S^T row 16s+8(j>>2)+4h+(j&3);
+// feeding K row pi(R) (bits 2 and 3 of R swapped) into A-row R makes that element the
+// PHYSICAL key 16s + 8h + j, so the V^T operand of the same k-step is 8 consecutive keys --
+// one 16-B LDS read per lane.
+//
+// LDS (64 KiB): two buffers of [K 64 x 128 | V^T 128 x 64] bf16.  Bank-conflict-free 16-B
+// reads: K row r keeps chunk c at slot c ^ (r & 15) (the rows a 16-lane read group touches are
+// distinct mod 16 under pi), V^T row d keeps chunk c at slot c ^ ((d >> 1) & 7) (two 128-B rows
+// per 256-B bank row; the group's (d & 1, (d >> 1) & 7) pairs are distinct).  Tile i+1 is
+// fetched to registers before tile i is multiplied and written to the other buffer after it;
+// one barrier per tile.
+#include "eia_common.h"
+
+namespace {
+
+typedef __attribute__((ext_vector_type(16))) float f32x16_t;
+
+constexpr int FD = 128;        // head dim
+constexpr int FKB = 64;        // keys per tile
+constexpr int FQB = 64;        // queries per workgroup and head
+constexpr int FTHREADS = 512;  // 8 waves
+constexpr int KT_ELEMS = FKB * FD;   // K tile elements (= V^T tile elements)
+
+EIA_DEV int k_slot(int r, int c) { return r * FD + ((c ^ (r & 15)) << 3); }
+EIA_DEV int v_slot(int d, int c) { return d * FKB + ((c ^ ((d >> 1) & 7)) << 3); }
+EIA_DEV int perm_row(int R) { return (R & ~12) | ((R & 4) << 1) | ((R & 8) >> 1); }
+
+__global__ void __launch_bounds__(FTHREADS, 1)
+paged_prefill_fa_kernel(const bf16_t* __restrict__ q, long q_stride, bf16_t* __restrict__ out,
+                        long out_stride, const bf16_t* __restrict__ kc,
+                        const bf16_t* __restrict__ vc, const int* __restrict__ block_tables,
+                        int bt_stride, const int* __restrict__ seq_lens,
+                        const int* __restrict__ cu_q, const int* __restrict__ work,
+                        float scale_log2, int Hq, int Hkv, int bs, int causal, int sliding_window,
+                        int chunk_size) {
+  __shared__ __align__(16) bf16_t lds[2 * 2 * KT_ELEMS];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int r32 = lane & 31, h = lane >> 5;
+  const int s = work[2 * blockIdx.x], q0 = work[2 * blockIdx.x + 1];
+  const int G = Hq / Hkv, NHG = G / 4;
+  const int kvh = blockIdx.y / NHG, hg = blockIdx.y % NHG;
+  const int hq = kvh * G + hg * 4 + (w & 3);
+  const int qsub = w >> 2;
+  const int qbeg = cu_q[s], qlen = cu_q[s + 1] - qbeg;
+  if (q0 >= qlen) return;                                  // workgroup-uniform
+  const int L = seq_lens[s], ctx = L - qlen;
+  const bool window = sliding_window > 0 || chunk_size > 0;
+  auto lo_of = [&](int qa) {
+    int lo = 0;
+    if (sliding_window > 0) lo = max(lo, qa - sliding_window + 1);
+    if (chunk_size > 0) lo = max(lo, (qa / chunk_size) * chunk_size);
+    return lo;
+  };
+
+  // this lane's query column
+  const int qi = q0 + 32 * qsub + r32;
+  const bool qvalid = qi < qlen;
+  const int qe = min(qi, qlen - 1);
+  const long tok = qbeg + qe;
+  const int qa = ctx + qe;
+  const int q_lo = lo_of(qa);
+  // Q^T fragments (B operand): k-step t = dims [16t, 16t+16), lane half h holds 16t+8h..+8
+  bf16x8 qf[FD / 16];
+  {
+    const bf16_t* qp = q + tok * q_stride + (long)hq * FD + 8 * h;
+#pragma unroll
+    for (int t = 0; t < FD / 16; ++t) qf[t] = *reinterpret_cast<const bf16x8*>(qp + 16 * t);
+  }
+
+  // workgroup key range [lo, hi) (tiles of 64 from a 64-aligned lo) and this wave's range
+  const int qlast = min(q0 + FQB, qlen) - 1;
+  const int hi = causal ? min(L, ctx + qlast + 1) : L;
+  const int lo = lo_of(ctx + q0) & ~(FKB - 1);
+  const int ntile = (hi - lo + FKB - 1) / FKB;
+  const int wq0 = q0 + 32 * qsub;                          // wave's first query
+  const bool wave_live = wq0 < qlen;
+  const int wq1 = min(wq0 + 32, qlen) - 1;                 // wave's last valid query
+  const int w_hi = !wave_live ? 0 : (causal ? min(L, ctx + wq1 + 1) : L);
+  const int w_lo = wave_live ? lo_of(ctx + wq0) : 0;      // no query of the wave sees below
+
+  const int* bt = block_tables + (long)s * bt_stride;
+  auto fetch = [&](int kb, bf16x8 (&st)[4]) {
+    const int blk = bt[kb / bs];
+    const long base = ((long)blk * Hkv + kvh) * (long)bs * FD;
+    const int o = kb % bs;
+    const bf16_t* kp = kc + base + (long)o * FD;          // 64 rows x 128, contiguous
+    const bf16_t* vp = vc + base + o;                     // 128 rows x 64 keys, row stride bs
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int id = tid + FTHREADS * i;
+      st[i] = *reinterpret_cast<const bf16x8*>(kp + 8 * id);
+      st[2 + i] = *reinterpret_cast<const bf16x8*>(vp + (long)(id >> 3) * bs + 8 * (id & 7));
+    }
+  };
+  auto stash = [&](int buf, const bf16x8 (&st)[4]) {
+    bf16_t* kl = lds + buf * 2 * KT_ELEMS;
+    bf16_t* vl = kl + KT_ELEMS;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int id = tid + FTHREADS * i;
+      *reinterpret_cast<bf16x8*>(kl + k_slot(id >> 4, id & 15)) = st[i];
+      *reinterpret_cast<bf16x8*>(vl + v_slot(id >> 3, id & 7)) = st[2 + i];
+    }
+  };
+
+  f32x16_t oacc[FD / 32];
+#pragma unroll
+  for (int dt = 0; dt < FD / 32; ++dt)
+#pragma unroll
+    for (int i = 0; i < 16; ++i) oacc[dt][i] = 0.f;
+  float m_run = (-INFINITY), l_run = 0.f;
+  const int krow0 = perm_row(r32);
+
+  auto compute = [&](int buf, int kb) {
+    const bf16_t* kl = lds + buf * 2 * KT_ELEMS;
+    const bf16_t* vl = kl + KT_ELEMS;
+    f32x16_t sacc[2];
+#pragma unroll
+    for (int sh = 0; sh < 2; ++sh) {
+#pragma unroll
+      for (int i = 0; i < 16; ++i) sacc[sh][i] = 0.f;
+      const int kr = 32 * sh + krow0;
+#pragma unroll
+      for (int t = 0; t < FD / 16; ++t) {
+        const bf16x8 kf = *reinterpret_cast<const bf16x8*>(kl + k_slot(kr, 2 * t + h));
+        sacc[sh] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf, qf[t], sacc[sh], 0, 0, 0);
+      }
+    }
+    // element i of half sh is key kb + 32 sh + 16 (i >> 3) + 8 h + (i & 7)
+    const bool whole = !window && kb + FKB <= L && (!causal || kb + FKB - 1 <= ctx + wq0);
+    if (!whole) {
+#pragma unroll
+      for (int sh = 0; sh < 2; ++sh)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+          const int kp = kb + 32 * sh + 16 * (i >> 3) + 8 * h + (i & 7);
+          const bool ok = kp < L && (!causal || kp <= qa) && kp >= q_lo;
+          if (!ok) sacc[sh][i] = (-INFINITY);
+        }
+    }
+    float mx = sacc[0][0];
+#pragma unroll
+    for (int sh = 0; sh < 2; ++sh)
+#pragma unroll
+      for (int i = 0; i < 16; ++i) mx = fmaxf(mx, sacc[sh][i]);
+    mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+    const float m_new = fmaxf(m_run, mx * scale_log2);
+    const float muse = m_new == (-INFINITY) ? 0.f : m_new;
+    const float alpha = exp2f(m_run - muse);
+    bf16x8 pb[4];
+    float psum = 0.f;
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const float p = exp2f(fmaf(sacc[ks >> 1][8 * (ks & 1) + j], scale_log2, -muse));
+        pb[ks][j] = f2bf(p);
+        psum += p;
+      }
+    l_run = fmaf(l_run, alpha, psum);
+    m_run = m_new;
+    if (!__all(alpha == 1.f)) {
+#pragma unroll
+      for (int dt = 0; dt < FD / 32; ++dt) oacc[dt] *= alpha;
+    }
+#pragma unroll
+    for (int dt = 0; dt < FD / 32; ++dt) {
+      const int d = 32 * dt + r32;
+#pragma unroll
+      for (int ks = 0; ks < 4; ++ks) {
+        const bf16x8 vf = *reinterpret_cast<const bf16x8*>(vl + v_slot(d, 2 * ks + h));
+        oacc[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf, pb[ks], oacc[dt], 0, 0, 0);
+      }
+    }
+  };
+
+  bf16x8 st[4];
+  if (ntile > 0) {
+    fetch(lo, st);
+    stash(0, st);
+  }
+  __syncthreads();
+  for (int it = 0; it < ntile; ++it) {
+    const int kb = lo + FKB * it;
+    const bool more = it + 1 < ntile;
+    if (more) fetch(kb + FKB, st);
+    // wave-uniform: does any of this wave's queries see a key of the tile?
+    if (kb < w_hi && kb + FKB > w_lo) compute(it & 1, kb);
+    if (more) stash((it + 1) & 1, st);
+    __syncthreads();
+  }
+
+  float lt = l_run + __shfl_xor(l_run, 32, 64);
+  if (!qvalid) return;
+  const float inv = lt > 0.f ? 1.f / lt : 0.f;
+  bf16_t* op = out + tok * out_stride + (long)hq * FD + 4 * h;
+#pragma unroll
+  for (int dt = 0; dt < FD / 32; ++dt)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      bf16x4 o4;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) o4[r] = f2bf(oacc[dt][4 * j + r] * inv);
+      *reinterpret_cast<bf16x4*>(op + 32 * dt + 8 * j) = o4;
+    }
+}
+
+}  // namespace
+
+// work = [seq, first query] pairs with 64-query blocks (attention.prefill_query_block);
+// grid (n_work, Hkv * G/4).  Requires D = 128, G % 4 == 0, block size % 64 == 0.
+EIA_API int eia_paged_prefill_fa(const void* q, long q_stride, void* out, long out_stride,
+                                 const void* k_cache, const void* v_cache,
+                                 const int* block_tables, int bt_stride, const int* seq_lens,
+                                 const int* cu_q, const int* work, int n_work, float scale, int Hq,
+                                 int Hkv, int D, int bs, int causal, int sliding_window,
+                                 int chunk_size, hipStream_t st) {
+  if (Hkv <= 0 || Hq % Hkv != 0) return EIA_BAD_SHAPE;
+  if (D != FD || (Hq / Hkv) % 4 != 0 || bs % FKB != 0) return EIA_UNSUPPORTED;
+  if (n_work == 0) return EIA_OK;
+  dim3 grid(n_work, Hkv * ((Hq / Hkv) / 4));
+  hipLaunchKernelGGL(paged_prefill_fa_kernel, grid, dim3(FTHREADS), 0, st, (const bf16_t*)q,
+                     q_stride, (bf16_t*)out, out_stride, (const bf16_t*)k_cache,
+                     (const bf16_t*)v_cache, block_tables, bt_stride, seq_lens, cu_q, work,
+                     scale * 1.4426950408889634f, Hq, Hkv, bs, causal, sliding_window, chunk_size);
+  EIA_LAUNCH_CHECK();
+}

@@ -19,7 +19,7 @@ import torch.nn.functional as F
 
 from ..config import ModelConfig
 from ..ops import activation, gemm  # noqa: F401
-from ..ops.attention import AttentionMetadata, attention
+from ..ops.attention import AttentionMetadata, attention, decode_rope_attention
 from ..ops.rotary import RotaryCache, rope_qkv_cache
 from ..parallel import state
 from ..ops.gemm import SplitK
@@ -60,14 +60,20 @@ class LlamaAttention(nn.Module):
     def forward(self, h: torch.Tensor, md: AttentionMetadata, kv: KVCache) -> torch.Tensor:
         T = h.shape[0]
         qkv = gemm.linear(h, self.qkv_proj.weight, defer_reduce=True)   # split-K summed in K4
-        q = rope_qkv_cache(qkv, md.positions, self.rotary, md.slot_mapping, kv[0], kv[1],
-                           self.num_heads, self.num_kv_heads, self.head_dim,
-                           bias=self.qkv_proj.bias,
-                           q_norm_w=None if self.q_norm is None else self.q_norm.weight,
-                           k_norm_w=None if self.k_norm is None else self.k_norm.weight,
-                           norm_eps=self.cfg.rms_norm_eps)
-        o = attention(q, kv[0], kv[1], md, self.scale, self.sliding_window, self.chunk_size)
-        return self.o_proj(o.view(T, self.num_heads * self.head_dim), defer_reduce=True)
+        qn = None if self.q_norm is None else self.q_norm.weight
+        kn = None if self.k_norm is None else self.k_norm.weight
+        # pure decode: K4 (reduce/bias/qk-norm/RoPE/KV write) runs inside the attention kernel
+        o = decode_rope_attention(qkv, md, kv[0], kv[1], self.rotary, self.num_heads,
+                                  self.num_kv_heads, self.head_dim, self.scale,
+                                  self.qkv_proj.bias, qn, kn, self.cfg.rms_norm_eps,
+                                  self.sliding_window, self.chunk_size)
+        if o is None:
+            q = rope_qkv_cache(qkv, md.positions, self.rotary, md.slot_mapping, kv[0], kv[1],
+                               self.num_heads, self.num_kv_heads, self.head_dim,
+                               bias=self.qkv_proj.bias, q_norm_w=qn, k_norm_w=kn,
+                               norm_eps=self.cfg.rms_norm_eps)
+            o = attention(q, kv[0], kv[1], md, self.scale, self.sliding_window, self.chunk_size)
+        return self.o_proj(o.view(-1, self.num_heads * self.head_dim)[:T], defer_reduce=True)
 
 
 class LlamaMLP(nn.Module):

@@ -10,12 +10,15 @@ from __future__ import annotations
 
 import dataclasses
 import math
+import os
 from typing import List, Optional, Sequence
 
 import torch
 
 from . import reference as ref
 from ._dispatch import check, lib, ptr, require, stream, use_hip
+
+EIA_UNSUPPORTED = 1002       # csrc/include/eia_common.h EiaStatus
 
 
 def heads_per_workgroup(num_heads: int, num_kv_heads: int) -> int:
@@ -46,10 +49,27 @@ PREFILL_LDS = 16          # kernel variant flag: K/V units shared by the workgro
 PREFILL_LDS_QT = {64: 1, 128: 2}
 
 
+# Flash-attention form (csrc/kernels/attention_fa.hip): 8 waves, 64 queries x 4 heads of one KV
+# group per workgroup, 64-key K/V tiles in swizzled LDS, v_mfma_f32_32x32x16_bf16 with P^T fed
+# from the S^T accumulators.  D = 128, G % 4 == 0, block size % 64 == 0.
+PREFILL_FA = 32
+PREFILL_FA_QB = 64
+_FA_ENV = os.environ.get("EIA_PREFILL_FA", "1") != "0"
+
+
+def fa_supported(num_heads: int, num_kv_heads: int, head_dim: int,
+                 block_size: Optional[int]) -> bool:
+    return (_FA_ENV and head_dim == 128 and (num_heads // num_kv_heads) % 4 == 0
+            and block_size is not None and block_size % 64 == 0)
+
+
 def prefill_variant(num_heads: int, num_kv_heads: int, head_dim: int,
                     block_size: Optional[int] = None) -> int:
-    """Kernel variant code: tiles per wave, | PREFILL_LDS for the LDS-shared form (the four
-    waves of a workgroup are four query heads of one KV group; needs 32 | block size)."""
+    """Kernel variant code: PREFILL_FA for the flash form where it applies; else tiles per
+    wave, | PREFILL_LDS for the LDS-shared form (the four waves of a workgroup are four query
+    heads of one KV group; needs 32 | block size)."""
+    if fa_supported(num_heads, num_kv_heads, head_dim, block_size):
+        return PREFILL_FA
     if (heads_per_workgroup(num_heads, num_kv_heads) == 4 and block_size is not None
             and block_size % 32 == 0 and head_dim in PREFILL_LDS_QT):
         return PREFILL_LDS | PREFILL_LDS_QT[head_dim]
@@ -58,8 +78,11 @@ def prefill_variant(num_heads: int, num_kv_heads: int, head_dim: int,
 
 def prefill_query_block(num_heads: int, num_kv_heads: int, head_dim: int = 128,
                         qt: Optional[int] = None, block_size: Optional[int] = None) -> int:
-    """Queries covered by one prefill workgroup (4 waves x QT x 16 columns / heads-per-WG)."""
+    """Queries covered by one prefill workgroup (4 waves x QT x 16 columns / heads-per-WG;
+    64 for the flash form)."""
     code = qt or prefill_variant(num_heads, num_kv_heads, head_dim, block_size)
+    if code & PREFILL_FA:
+        return PREFILL_FA_QB
     return 16 * (code & 15) * (4 // heads_per_workgroup(num_heads, num_kv_heads))
 
 
@@ -196,12 +219,91 @@ def paged_prefill(q: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tensor,
     require(block_tables.stride(1) == 1, "block_tables rows must be contiguous")
     o = torch.empty_like(q) if out is None else out
     hpw = heads_per_workgroup(Hq, Hkv)
+    code = qt or prefill_variant(Hq, Hkv, D, bs)
+    if code & PREFILL_FA:
+        rc = lib().eia_paged_prefill_fa(
+            ptr(q), q.stride(0), ptr(o), o.stride(0), ptr(k_cache), ptr(v_cache),
+            ptr(block_tables), block_tables.stride(0), ptr(seq_lens), ptr(cu_q), ptr(work), n_work,
+            float(scale), Hq, Hkv, D, bs, 1 if causal else 0, sliding_window or 0, chunk_size or 0,
+            stream(q))
+        if rc != EIA_UNSUPPORTED:
+            check(rc, "paged_prefill_fa")
+            return o
+        code = PREFILL_LDS | 4          # same 64-query blocks (HPW 4 x QT 4 x 16)
+        require(hpw == 4, "paged_prefill: flash work list needs 4 heads per workgroup")
     check(lib().eia_paged_prefill(
         ptr(q), q.stride(0), ptr(o), o.stride(0), ptr(k_cache), ptr(v_cache), ptr(block_tables),
         block_tables.stride(0), ptr(seq_lens), ptr(cu_q), ptr(work), n_work, float(scale), Hq, Hkv,
-        D, bs, hpw, 1 if causal else 0, sliding_window or 0, chunk_size or 0, qt or prefill_variant(Hq, Hkv, D, bs),
-        stream(q)),
+        D, bs, hpw, 1 if causal else 0, sliding_window or 0, chunk_size or 0, code, stream(q)),
         "paged_prefill")
+    return o
+
+
+_FUSED_ENV = os.environ.get("EIA_DECODE_FUSED_ROPE", "1") != "0"
+
+
+def decode_rope_attention(qkv, md: AttentionMetadata, k_cache: torch.Tensor,
+                          v_cache: torch.Tensor, rotary, num_heads: int, num_kv_heads: int,
+                          head_dim: int, scale: float, bias: Optional[torch.Tensor] = None,
+                          q_norm_w: Optional[torch.Tensor] = None,
+                          k_norm_w: Optional[torch.Tensor] = None, norm_eps: float = 1e-6,
+                          sliding_window: Optional[int] = None,
+                          chunk_size: Optional[int] = None) -> Optional[torch.Tensor]:
+    """Pure-decode step: QKV reduce + bias + qk-norm + RoPE + KV write + attention in ONE
+    kernel (csrc/kernels/attention.hip eia_paged_decode_rope) -> out [B, Hq, D].
+
+    Returns None when the fused form does not apply (CPU, prefill tokens in the step, GPT-J
+    rotary, G > 16, D not 64/128, block size not a multiple of 32, EIA_DECODE_FUSED_ROPE=0);
+    the caller then runs rope_qkv_cache + attention.  Same bits as the two-kernel path."""
+    from .gemm import SplitK
+    if not _FUSED_ENV or md.num_prefill_tokens != 0 or md.num_decode == 0 or rotary is None:
+        return None
+    if not rotary.is_neox or head_dim not in (64, 128) or num_heads // num_kv_heads > 16:
+        return None
+    if k_cache.shape[2] % 32 != 0 or md.positions is None:
+        return None
+    split = isinstance(qkv, SplitK)
+    src = qkv.part if split else qkv
+    if not (use_hip(src, k_cache) and k_cache.dtype == torch.bfloat16):
+        return None
+    if split:
+        if qkv.bias is not None:
+            require(bias is None, "decode_rope_attention: bias given twice")
+            bias = qkv.bias
+        if not qkv.part.is_contiguous():
+            return None
+        T = qkv.M
+    else:
+        if qkv.dtype != torch.bfloat16 or qkv.stride(-1) != 1:
+            return None
+        T = qkv.shape[0]
+    require((qkv.N if split else qkv.shape[1]) == (num_heads + 2 * num_kv_heads) * head_dim,
+            "decode_rope_attention: qkv width")
+    B = md.num_decode
+    bt, sl = md.decode_block_tables, md.decode_seq_lens
+    require(bt.dtype == torch.int32 and sl.dtype == torch.int32 and bt.stride(1) == 1,
+            "int32 decode metadata")
+    require(md.slot_mapping.dtype == torch.int32 and md.positions.dtype == torch.int32,
+            "int32 slot_mapping / positions")
+    P = md.decode_partitions
+    if P > 1:
+        require(md.decode_part_o is not None and md.decode_part_ml is not None and
+                md.decode_part_o.numel() >= B * num_heads * P * head_dim, "decode workspace")
+    o = torch.empty((B, num_heads, head_dim), dtype=torch.bfloat16, device=k_cache.device)
+    rc = lib().eia_paged_decode_rope(
+        None if split else ptr(qkv), 0 if split else qkv.stride(0),
+        ptr(qkv.part) if split else None, qkv.sk if split else 0,
+        ptr(bias), ptr(q_norm_w), ptr(k_norm_w), float(norm_eps), ptr(md.positions),
+        ptr(rotary.cos_sin), ptr(md.slot_mapping), T, ptr(k_cache), ptr(v_cache), ptr(bt),
+        bt.stride(0), ptr(sl), ptr(o), o.stride(0),
+        ptr(md.decode_part_o) if P > 1 else None, ptr(md.decode_part_ml) if P > 1 else None,
+        ptr(md.decode_part_cnt) if (P > 1 and md.decode_part_cnt is not None) else None,
+        float(scale), B, num_heads, num_kv_heads, head_dim, k_cache.shape[2], P,
+        sliding_window or 0, chunk_size or 0,
+        ptr(md.decode_p_dyn) if (P > 1 and md.decode_p_dyn is not None) else None, stream(o))
+    if rc == EIA_UNSUPPORTED:
+        return None
+    check(rc, "paged_decode_rope")
     return o
 
 

@@ -25,9 +25,12 @@ def main():
     ap.add_argument("--bs", type=int, default=128)
     ap.add_argument("--qt", type=int, nargs="*", default=None)
     ap.add_argument("--iters", type=int, default=10)
+    ap.add_argument("--noncausal", action="store_true")
     a = ap.parse_args()
     dev, bf = "cuda", torch.bfloat16
-    qts = a.qt or sorted({1, 2, attention.prefill_tiles(a.d)})
+    qts = a.qt or sorted({1, 2, attention.prefill_tiles(a.d),
+                          attention.prefill_variant(a.hq, a.hkv, a.d, a.bs)} |
+                         ({attention.PREFILL_LDS | 2} if a.hq % (4 * a.hkv) == 0 else set()))
     for shp in a.shapes:
         B, L = (int(x) for x in shp.split("x"))
         nb = B * ((L + a.bs - 1) // a.bs)
@@ -37,17 +40,18 @@ def main():
         sl = torch.full((B,), L, dtype=torch.int32, device=dev)
         cu = torch.arange(0, (B + 1) * L, L, dtype=torch.int32, device=dev)
         q = torch.randn(B * L, a.hq, a.d, device=dev, dtype=bf)
-        flops = 4.0 * B * a.hq * a.d * L * (L + 1) / 2          # QK^T + PV under the causal mask
+        causal = not a.noncausal
+        flops = 4.0 * B * a.hq * a.d * L * ((L + 1) / 2 if causal else L)   # QK^T + PV
         ref = None
         for qt in qts:
-            qb = attention.prefill_query_block(a.hq, a.hkv, a.d, qt)
+            qb = attention.prefill_query_block(a.hq, a.hkv, a.d, qt, block_size=a.bs)
             work = torch.tensor(attention.build_prefill_work([L] * B, qb), dtype=torch.int32,
                                 device=dev)
             n = work.numel() // 2
 
             def fn():
-                return attention.paged_prefill(q, kc, vc, bt, sl, cu, work, n, a.d ** -0.5, True,
-                                               qt=qt)
+                return attention.paged_prefill(q, kc, vc, bt, sl, cu, work, n, a.d ** -0.5,
+                                               causal, qt=qt)
             o = fn()
             torch.cuda.synchronize()
             if ref is None:
@@ -60,7 +64,7 @@ def main():
             e1.record()
             torch.cuda.synchronize()
             us = e0.elapsed_time(e1) / a.iters * 1e3
-            print(json.dumps({"shape": shp, "hq": a.hq, "hkv": a.hkv, "d": a.d, "qt": qt,
+            print(json.dumps({"shape": shp, "causal": causal, "hq": a.hq, "hkv": a.hkv, "d": a.d, "qt": qt,
                               "us": round(us, 1), "tflops": round(flops / us / 1e6, 1),
                               "max_diff_vs_qt%d" % qts[0]: err}), flush=True)
 

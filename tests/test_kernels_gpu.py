@@ -178,7 +178,7 @@ def test_paged_decode_zero_len_rows():
 
 
 @pytest.mark.parametrize("Hq,Hkv,D,bs", [(32, 8, 128, 128), (12, 12, 64, 16), (40, 8, 128, 32),
-                                         (12, 4, 256, 16), (8, 2, 128, 64)])
+                                         (12, 4, 256, 16), (8, 2, 128, 64), (64, 8, 128, 128)])
 @pytest.mark.parametrize("causal", [True, False])
 def test_paged_prefill(Hq, Hkv, D, bs, causal):
     from enterprise_inference_amd.ops import attention
@@ -199,6 +199,8 @@ def test_paged_prefill(Hq, Hkv, D, bs, causal):
     qts = {1, attention.prefill_tiles(D)} | ({2, 3, 4} if D <= 128 else set())
     if attention.heads_per_workgroup(Hq, Hkv) == 4 and bs % 32 == 0 and D in (64, 128):
         qts |= {attention.PREFILL_LDS | t for t in (1, 2, 3, 4)}
+    if attention.fa_supported(Hq, Hkv, D, bs):
+        qts.add(attention.PREFILL_FA)
     for qt in sorted(qts):
         qb = attention.prefill_query_block(Hq, Hkv, D, qt)
         work = torch.tensor(attention.build_prefill_work(qlens, qb), dtype=torch.int32, device=DEV)
@@ -383,3 +385,81 @@ def test_fill_ids():
     tok = torch.tensor([100, 101, 102, 103], dtype=torch.int32, device=DEV)
     sampling.fill_ids(ids, src, tok)
     assert ids.cpu().tolist() == [5, 102, 7, 100, 103]
+
+
+@pytest.mark.parametrize("Hq,Hkv,D,bs,bias,qkn,split", [
+    (32, 8, 128, 128, False, False, True),      # Llama-3-8B decode (split-K QKV)
+    (32, 8, 128, 128, False, False, False),
+    (28, 4, 128, 64, True, False, True),        # Qwen2 (bias)
+    (16, 8, 128, 32, False, True, True),        # Qwen3 (qk-norm)
+    (12, 12, 64, 32, True, True, False),
+    (64, 8, 128, 128, False, False, True)])     # 70B-like G = 8
+@pytest.mark.parametrize("P,dyn", [(1, None), (4, None), (8, 3)])
+def test_decode_rope_fused_matches_two_kernels(Hq, Hkv, D, bs, bias, qkn, split, P, dyn):
+    """eia_paged_decode_rope == rope_qkv_cache + paged_decode, bit for bit (q, out, K/V cache)."""
+    from enterprise_inference_amd.ops import attention, rotary
+    from enterprise_inference_amd.ops.gemm import SplitK
+    torch.manual_seed(Hq + D + P)
+    B = 13
+    lens = [random.Random(i * 3 + P).randint(1, 900) for i in range(B)]
+    lens[0], lens[1], lens[2] = 1, 64, 65
+    lens[5] = 0                                                   # graph padding row
+    nbt = sum(math.ceil(max(l, 1) / bs) for l in lens) + 2
+    k1, v1 = _make_cache(nbt, Hkv, bs, D, fill=True)
+    bt = _random_tables([max(l, 1) for l in lens], bs, nbt).to(DEV)
+    sl = torch.tensor(lens, dtype=torch.int32, device=DEV)
+    pos = torch.tensor([max(l - 1, 0) for l in lens], dtype=torch.int32, device=DEV)
+    slots = torch.tensor([int(bt[i, (l - 1) // bs]) * bs + (l - 1) % bs if l > 0 else -1
+                          for i, l in enumerate(lens)], dtype=torch.int32, device=DEV)
+    N = (Hq + 2 * Hkv) * D
+    if split:
+        qkv = SplitK(torch.randn(4, B, N, device=DEV) * 0.5, 4, B, N, None)
+    else:
+        qkv = torch.randn(B, N, device=DEV, dtype=BF)
+    b = torch.randn(N, device=DEV, dtype=BF) if bias else None
+    qn = (torch.rand(D, device=DEV) + 0.5).to(BF) if qkn else None
+    kn = (torch.rand(D, device=DEV) + 0.5).to(BF) if qkn else None
+    rc = rotary.RotaryCache(D, 4096, 500000.0, None, DEV)
+    k2, v2 = k1.clone(), v1.clone()
+    Pw = P
+    po = torch.empty(B * Hq * Pw * D, device=DEV)
+    pml = torch.empty(B * Hq * Pw * 2, device=DEV)
+    cnt = torch.zeros(B * Hkv, dtype=torch.int32, device=DEV)
+    pd = torch.tensor([dyn], dtype=torch.int32, device=DEV) if dyn else None
+    md = attention.AttentionMetadata(num_decode=B, num_prefill_tokens=0, slot_mapping=slots,
+                                     positions=pos, decode_block_tables=bt, decode_seq_lens=sl,
+                                     decode_partitions=P, decode_part_o=po, decode_part_ml=pml,
+                                     decode_part_cnt=cnt, decode_p_dyn=pd)
+    o1 = attention.decode_rope_attention(qkv, md, k1, v1, rc, Hq, Hkv, D, D ** -0.5, b, qn, kn,
+                                         1e-6)
+    assert o1 is not None, "fused decode must apply to this shape"
+    q = rotary.rope_qkv_cache(qkv, pos, rc, slots, k2, v2, Hq, Hkv, D, b, qn, kn, 1e-6)
+    o2 = attention.attention(q, k2, v2, md, D ** -0.5)
+    assert torch.equal(k1, k2) and torch.equal(v1, v2), "K/V cache writes differ"
+    live = sl > 0
+    assert torch.equal(o1[live], o2[live]), (o1[live].float() - o2[live].float()).abs().max()
+    assert int(cnt.abs().sum()) == 0
+
+
+@pytest.mark.parametrize("sw,ch", [(None, None), (50, None), (None, 64), (200, None)])
+def test_paged_prefill_fa_long_and_windowed(sw, ch):
+    """Flash form (v_mfma_f32_32x32x16) on multi-tile prompts with cached context, ragged
+    lengths, sliding window and chunked attention vs the fp32 reference."""
+    from enterprise_inference_amd.ops import attention
+    Hq, Hkv, D, bs = 16, 4, 128, 64
+    torch.manual_seed(11)
+    qlens, ctxs = [333, 64, 1, 190, 65], [0, 129, 700, 3, 64]
+    lens = [c + q for c, q in zip(ctxs, qlens)]
+    nbt = sum(math.ceil(l / bs) for l in lens) + 2
+    k, v = _make_cache(nbt, Hkv, bs, D, fill=True)
+    bt = _random_tables(lens, bs, nbt).to(DEV)
+    sl = torch.tensor(lens, dtype=torch.int32, device=DEV)
+    cu = torch.tensor([0] + list(torch.tensor(qlens).cumsum(0)), dtype=torch.int32, device=DEV)
+    q = torch.randn(sum(qlens), Hq, D, device=DEV, dtype=BF)
+    work = torch.tensor(attention.build_prefill_work(qlens, attention.PREFILL_FA_QB),
+                        dtype=torch.int32, device=DEV)
+    o = attention.paged_prefill(q, k, v, bt, sl, cu, work, work.numel() // 2, D ** -0.5, True,
+                                sw, ch, qt=attention.PREFILL_FA)
+    r = ref.paged_attention_prefill(q.cpu().float(), k.cpu().float(), v.cpu().float(), bt.cpu(),
+                                    cu.cpu(), sl.cpu(), D ** -0.5, True, sw, ch)
+    _close(o, r, 2e-2, 2e-2, f"prefill fa sw={sw} chunk={ch}")
