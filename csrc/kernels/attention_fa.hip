@@ -17,12 +17,18 @@
 // PHYSICAL key 16s + 8h + j, so the V^T operand of the same k-step is 8 consecutive keys --
 // one 16-B LDS read per lane.
 //
-// LDS (64 KiB): two buffers of [K 64 x 128 | V^T 128 x 64] bf16.  Bank-conflict-free 16-B
-// reads: K row r keeps chunk c at slot c ^ (r & 15) (the rows a 16-lane read group touches are
-// distinct mod 16 under pi), V^T row d keeps chunk c at slot c ^ ((d >> 1) & 7) (two 128-B rows
-// per 256-B bank row; the group's (d & 1, (d >> 1) & 7) pairs are distinct).  Tile i+1 is
-// fetched to registers before tile i is multiplied and written to the other buffer after it;
-// one barrier per tile.
+// LDS (70 KiB, dynamic): two buffers of [K 64 x (128+8) | V^T 128 x (64+8)] bf16.  One 16-B
+// pad per row makes every ds_read_b128 group conflict-free (K slot = (row + chunk) mod 16,
+// V^T slot = (9 d + chunk) mod 16; a 16-lane read group touches rows distinct mod 16 under pi)
+// AND keeps a lane's fragment addresses one base register plus immediate offsets (an XOR
+// swizzle costs VALU address math on every read).  Tile i+1 is fetched to registers before
+// tile i is multiplied and written to the other buffer after it; one barrier per tile.
+// Softmax: deferred rescale (the running max moves only when a column's tile max exceeds it by
+// more than 2^8, guide T13), row max combined across the two lane halves by permlane32_swap.
+// Measured variants (profiles/prefill_attn_fa_r2.log): 4-wave workgroups (two per CU), other
+// MFMA / exp orders: all within 3 %; a software pipeline holding two tiles' S (QK(i+1) beside
+// the exp work of tile i) and two 32-query sub-blocks per wave (one wave per SIMD) both exceed
+// the register file and spill.
 #include "eia_common.h"
 
 namespace {
@@ -33,11 +39,21 @@ constexpr int FD = 128;        // head dim
 constexpr int FKB = 64;        // keys per tile
 constexpr int FQB = 64;        // queries per workgroup and head
 constexpr int FTHREADS = 512;  // 8 waves
-constexpr int KT_ELEMS = FKB * FD;   // K tile elements (= V^T tile elements)
+constexpr int KS = FD + 8;           // K row stride (elements)
+constexpr int VS = FKB + 8;          // V^T row stride (elements)
+constexpr int KBUF = FKB * KS, BUF = KBUF + FD * VS;
+constexpr int FA_LDS_BYTES = 2 * BUF * 2;
+constexpr float DEFER_LOG2 = 8.f;    // rescale only when the max grows by > 2^8
 
-EIA_DEV int k_slot(int r, int c) { return r * FD + ((c ^ (r & 15)) << 3); }
-EIA_DEV int v_slot(int d, int c) { return d * FKB + ((c ^ ((d >> 1) & 7)) << 3); }
 EIA_DEV int perm_row(int R) { return (R & ~12) | ((R & 4) << 1) | ((R & 8) >> 1); }
+EIA_DEV float pair_max(float v) {    // max with lane l ^ 32
+  const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return fmaxf(__uint_as_float(r[0]), __uint_as_float(r[1]));
+}
+EIA_DEV float pair_sum(float v) {
+  const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return __uint_as_float(r[0]) + __uint_as_float(r[1]);
+}
 
 __global__ void __launch_bounds__(FTHREADS, 1)
 paged_prefill_fa_kernel(const bf16_t* __restrict__ q, long q_stride, bf16_t* __restrict__ out,
@@ -47,7 +63,7 @@ paged_prefill_fa_kernel(const bf16_t* __restrict__ q, long q_stride, bf16_t* __r
                         const int* __restrict__ cu_q, const int* __restrict__ work,
                         float scale_log2, int Hq, int Hkv, int bs, int causal, int sliding_window,
                         int chunk_size) {
-  __shared__ __align__(16) bf16_t lds[2 * 2 * KT_ELEMS];
+  extern __shared__ __align__(16) bf16_t lds[];         // FA_LDS_BYTES
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int r32 = lane & 31, h = lane >> 5;
   const int s = work[2 * blockIdx.x], q0 = work[2 * blockIdx.x + 1];
@@ -107,13 +123,13 @@ paged_prefill_fa_kernel(const bf16_t* __restrict__ q, long q_stride, bf16_t* __r
     }
   };
   auto stash = [&](int buf, const bf16x8 (&st)[4]) {
-    bf16_t* kl = lds + buf * 2 * KT_ELEMS;
-    bf16_t* vl = kl + KT_ELEMS;
+    bf16_t* kl = lds + buf * BUF;
+    bf16_t* vl = kl + KBUF;
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
       const int id = tid + FTHREADS * i;
-      *reinterpret_cast<bf16x8*>(kl + k_slot(id >> 4, id & 15)) = st[i];
-      *reinterpret_cast<bf16x8*>(vl + v_slot(id >> 3, id & 7)) = st[2 + i];
+      *reinterpret_cast<bf16x8*>(kl + (id >> 4) * KS + 8 * (id & 15)) = st[i];
+      *reinterpret_cast<bf16x8*>(vl + (id >> 3) * VS + 8 * (id & 7)) = st[2 + i];
     }
   };
 
@@ -126,18 +142,18 @@ paged_prefill_fa_kernel(const bf16_t* __restrict__ q, long q_stride, bf16_t* __r
   const int krow0 = perm_row(r32);
 
   auto compute = [&](int buf, int kb) {
-    const bf16_t* kl = lds + buf * 2 * KT_ELEMS;
-    const bf16_t* vl = kl + KT_ELEMS;
+    // lane fragment bases: K row pi(lane) (+32 rows for the second half), chunk h; V^T row
+    // lane (+32 rows per d-tile), chunk h -- every read below is base + immediate
+    const bf16_t* kf0 = lds + buf * BUF + krow0 * KS + 8 * h;
+    const bf16_t* vf0 = lds + buf * BUF + KBUF + r32 * VS + 8 * h;
     f32x16_t sacc[2];
 #pragma unroll
     for (int sh = 0; sh < 2; ++sh) {
 #pragma unroll
-      for (int i = 0; i < 16; ++i) sacc[sh][i] = 0.f;
-      const int kr = 32 * sh + krow0;
-#pragma unroll
       for (int t = 0; t < FD / 16; ++t) {
-        const bf16x8 kf = *reinterpret_cast<const bf16x8*>(kl + k_slot(kr, 2 * t + h));
-        sacc[sh] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf, qf[t], sacc[sh], 0, 0, 0);
+        const bf16x8 kf = *reinterpret_cast<const bf16x8*>(kf0 + 32 * KS * sh + 16 * t);
+        sacc[sh] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf, qf[t], t == 0 ? f32x16_t{} : sacc[sh],
+                                                           0, 0, 0);
       }
     }
     // element i of half sh is key kb + 32 sh + 16 (i >> 3) + 8 h + (i & 7)
@@ -157,10 +173,17 @@ paged_prefill_fa_kernel(const bf16_t* __restrict__ q, long q_stride, bf16_t* __r
     for (int sh = 0; sh < 2; ++sh)
 #pragma unroll
       for (int i = 0; i < 16; ++i) mx = fmaxf(mx, sacc[sh][i]);
-    mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
-    const float m_new = fmaxf(m_run, mx * scale_log2);
-    const float muse = m_new == (-INFINITY) ? 0.f : m_new;
-    const float alpha = exp2f(m_run - muse);
+    const float mt = pair_max(mx) * scale_log2;
+    const bool grow = mt > m_run + DEFER_LOG2;
+    if (__any(grow)) {                                     // wave-uniform
+      const float m_new = grow ? mt : m_run;
+      const float alpha = grow ? exp2f(m_run - m_new) : 1.f;
+      m_run = m_new;
+      l_run *= alpha;
+#pragma unroll
+      for (int dt = 0; dt < FD / 32; ++dt) oacc[dt] *= alpha;
+    }
+    const float muse = m_run == (-INFINITY) ? 0.f : m_run;
     bf16x8 pb[4];
     float psum = 0.f;
 #pragma unroll
@@ -171,21 +194,14 @@ paged_prefill_fa_kernel(const bf16_t* __restrict__ q, long q_stride, bf16_t* __r
         pb[ks][j] = f2bf(p);
         psum += p;
       }
-    l_run = fmaf(l_run, alpha, psum);
-    m_run = m_new;
-    if (!__all(alpha == 1.f)) {
+    l_run += psum;
 #pragma unroll
-      for (int dt = 0; dt < FD / 32; ++dt) oacc[dt] *= alpha;
-    }
-#pragma unroll
-    for (int dt = 0; dt < FD / 32; ++dt) {
-      const int d = 32 * dt + r32;
+    for (int dt = 0; dt < FD / 32; ++dt)
 #pragma unroll
       for (int ks = 0; ks < 4; ++ks) {
-        const bf16x8 vf = *reinterpret_cast<const bf16x8*>(vl + v_slot(d, 2 * ks + h));
+        const bf16x8 vf = *reinterpret_cast<const bf16x8*>(vf0 + 32 * VS * dt + 16 * ks);
         oacc[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf, pb[ks], oacc[dt], 0, 0, 0);
       }
-    }
   };
 
   bf16x8 st[4];
@@ -204,7 +220,7 @@ paged_prefill_fa_kernel(const bf16_t* __restrict__ q, long q_stride, bf16_t* __r
     __syncthreads();
   }
 
-  float lt = l_run + __shfl_xor(l_run, 32, 64);
+  const float lt = pair_sum(l_run);
   if (!qvalid) return;
   const float inv = lt > 0.f ? 1.f / lt : 0.f;
   bf16_t* op = out + tok * out_stride + (long)hq * FD + 4 * h;
@@ -232,8 +248,14 @@ EIA_API int eia_paged_prefill_fa(const void* q, long q_stride, void* out, long o
   if (Hkv <= 0 || Hq % Hkv != 0) return EIA_BAD_SHAPE;
   if (D != FD || (Hq / Hkv) % 4 != 0 || bs % FKB != 0) return EIA_UNSUPPORTED;
   if (n_work == 0) return EIA_OK;
+  static bool attr = false;   // > 64 KiB of dynamic LDS must be opted into
+  if (!attr) {
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(paged_prefill_fa_kernel),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, FA_LDS_BYTES);
+    attr = true;
+  }
   dim3 grid(n_work, Hkv * ((Hq / Hkv) / 4));
-  hipLaunchKernelGGL(paged_prefill_fa_kernel, grid, dim3(FTHREADS), 0, st, (const bf16_t*)q,
+  hipLaunchKernelGGL(paged_prefill_fa_kernel, grid, dim3(FTHREADS), FA_LDS_BYTES, st, (const bf16_t*)q,
                      q_stride, (bf16_t*)out, out_stride, (const bf16_t*)k_cache,
                      (const bf16_t*)v_cache, block_tables, bt_stride, seq_lens, cu_q, work,
                      scale * 1.4426950408889634f, Hq, Hkv, bs, causal, sliding_window, chunk_size);

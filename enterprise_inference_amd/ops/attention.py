@@ -53,8 +53,8 @@ PREFILL_LDS_QT = {64: 1, 128: 2}
 # group per workgroup, 64-key K/V tiles in swizzled LDS, v_mfma_f32_32x32x16_bf16 with P^T fed
 # from the S^T accumulators.  D = 128, G % 4 == 0, block size % 64 == 0.
 PREFILL_FA = 32
-PREFILL_FA_QB = 64
 _FA_ENV = os.environ.get("EIA_PREFILL_FA", "1") != "0"
+PREFILL_FA_QB = 64
 
 
 def fa_supported(num_heads: int, num_kv_heads: int, head_dim: int,
@@ -229,7 +229,7 @@ def paged_prefill(q: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tensor,
         if rc != EIA_UNSUPPORTED:
             check(rc, "paged_prefill_fa")
             return o
-        code = PREFILL_LDS | 4          # same 64-query blocks (HPW 4 x QT 4 x 16)
+        code = PREFILL_LDS | (PREFILL_FA_QB // 16)   # same query blocks (HPW 4 x QT x 16)
         require(hpw == 4, "paged_prefill: flash work list needs 4 heads per workgroup")
     check(lib().eia_paged_prefill(
         ptr(q), q.stride(0), ptr(o), o.stride(0), ptr(k_cache), ptr(v_cache), ptr(block_tables),
