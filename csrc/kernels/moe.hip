@@ -13,20 +13,11 @@
 
 namespace {
 
-// One wave per token.  scoring 0: softmax over E then top-k (optionally renormalised);
-// scoring 1: top-k on raw logits, weight = sigmoid(logit) (Llama-4).
-template <int EMAX>
-__global__ void __launch_bounds__(256)
-topk_kernel(const void* __restrict__ logits, int is_bf16, int T, int E, int k, int renorm,
-            int scoring, float* __restrict__ w_out, int* __restrict__ id_out) {
-  const int wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
-  const int lane = threadIdx.x & 63;
-  if (wave >= T) return;
-  float v = -INFINITY;
-  if (lane < E) {
-    v = is_bf16 ? bf2f(static_cast<const bf16_t*>(logits)[(long)wave * E + lane])
-                : static_cast<const float*>(logits)[(long)wave * E + lane];
-  }
+// Top-k of one token whose router logit for expert `lane` is v (lanes >= E: -inf).
+// scoring 0: softmax over E then top-k (optionally renormalised); scoring 1: top-k on raw
+// logits, weight = sigmoid(logit) (Llama-4).
+EIA_DEV void topk_select(float v, int wave, int lane, int E, int k, int renorm, int scoring,
+                         float* __restrict__ w_out, int* __restrict__ id_out) {
   float p = v;
   if (scoring == 0) {
     const float mx = wave_max(v);
@@ -59,6 +50,61 @@ topk_kernel(const void* __restrict__ logits, int is_bf16, int T, int E, int k, i
     w_out[(long)wave * k + sel_slot] = wv;
     id_out[(long)wave * k + sel_slot] = lane;
   }
+}
+
+// One wave per token, logits from a preceding router GEMM.
+__global__ void __launch_bounds__(256)
+topk_kernel(const void* __restrict__ logits, int is_bf16, int T, int E, int k, int renorm,
+            int scoring, float* __restrict__ w_out, int* __restrict__ id_out) {
+  const int wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const int lane = threadIdx.x & 63;
+  if (wave >= T) return;
+  float v = -INFINITY;
+  if (lane < E) {
+    v = is_bf16 ? bf2f(static_cast<const bf16_t*>(logits)[(long)wave * E + lane])
+                : static_cast<const float*>(logits)[(long)wave * E + lane];
+  }
+  topk_select(v, wave, lane, E, k, renorm, scoring, w_out, id_out);
+}
+
+// Router GEMM fused into the top-k: one wave per token computes its E logits (x row . router
+// row e, fp32 accumulate, rounded to bf16 like the unfused bf16 Linear) from 16-B loads of x
+// and of the router weight (E x H, L2-resident), reduces them across the wave and selects.
+// Replaces a hipBLASLt launch for an N = 8 GEMM (13.7 us per layer on Mixtral decode,
+// profiles/rocprof_r2_mixtral.md) and the logits round trip.
+template <int EM>
+__global__ void __launch_bounds__(256)
+route_kernel(const bf16_t* __restrict__ x, long ldx, const bf16_t* __restrict__ wr, int H, int T,
+             int E, int k, int renorm, int scoring, float* __restrict__ w_out,
+             int* __restrict__ id_out) {
+  const int wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const int lane = threadIdx.x & 63;
+  if (wave >= T) return;
+  float acc[EM];
+#pragma unroll
+  for (int e = 0; e < EM; ++e) acc[e] = 0.f;
+  const bf16_t* xr = x + (long)wave * ldx;
+  for (int c = lane * 8; c < H; c += 512) {
+    const bf16x8 xv = *reinterpret_cast<const bf16x8*>(xr + c);
+    float xf[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) xf[j] = bf2f(xv[j]);
+#pragma unroll
+    for (int e = 0; e < EM; ++e) {
+      if (e < E) {
+        const bf16x8 wv = *reinterpret_cast<const bf16x8*>(wr + (long)e * H + c);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) acc[e] = fmaf(xf[j], bf2f(wv[j]), acc[e]);
+      }
+    }
+  }
+  float v = -INFINITY;
+#pragma unroll
+  for (int e = 0; e < EM; ++e) {
+    const float tot = wave_sum(acc[e]);
+    if (lane == e && e < E) v = bf2f(f2bf(tot));
+  }
+  topk_select(v, wave, lane, E, k, renorm, scoring, w_out, id_out);
 }
 
 // Single workgroup: counts per expert, exclusive scan, scatter.  n = T*k entries.
@@ -126,9 +172,26 @@ EIA_API int eia_moe_topk(const void* logits, int is_bf16, int T, int E, int k, i
   if (E < 1 || E > 64 || k < 1 || k > E) return EIA_BAD_SHAPE;
   if (T == 0) return EIA_OK;
   const int waves_per_block = 4;
-  hipLaunchKernelGGL(topk_kernel<64>, dim3((T + waves_per_block - 1) / waves_per_block),
+  hipLaunchKernelGGL(topk_kernel, dim3((T + waves_per_block - 1) / waves_per_block),
                      dim3(64 * waves_per_block), 0, st, logits, is_bf16, T, E, k, renorm, scoring,
                      w_out, id_out);
+  EIA_LAUNCH_CHECK();
+}
+
+// Fused router GEMM + top-k: x [T, H] bf16 (ldx), router weight [E, H] bf16.
+EIA_API int eia_moe_route(const void* x, long ldx, const void* wr, int H, int T, int E, int k,
+                          int renorm, int scoring, float* w_out, int* id_out, hipStream_t st) {
+  if (E < 1 || E > 64 || k < 1 || k > E || H % 8 != 0 || (ldx % 8)) return EIA_BAD_SHAPE;
+  if (T == 0) return EIA_OK;
+  const dim3 grid((T + 3) / 4), block(256);
+  const bf16_t* xp = static_cast<const bf16_t*>(x);
+  const bf16_t* wp = static_cast<const bf16_t*>(wr);
+  if (E <= 8)
+    hipLaunchKernelGGL(route_kernel<8>, grid, block, 0, st, xp, ldx, wp, H, T, E, k, renorm, scoring, w_out, id_out);
+  else if (E <= 16)
+    hipLaunchKernelGGL(route_kernel<16>, grid, block, 0, st, xp, ldx, wp, H, T, E, k, renorm, scoring, w_out, id_out);
+  else
+    hipLaunchKernelGGL(route_kernel<64>, grid, block, 0, st, xp, ldx, wp, H, T, E, k, renorm, scoring, w_out, id_out);
   EIA_LAUNCH_CHECK();
 }
 

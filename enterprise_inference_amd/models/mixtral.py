@@ -93,8 +93,12 @@ class FusedMoE(nn.Module):
         if e is not None:
             param.data[e].copy_(self._ishard(loaded, 1))
 
-    def forward(self, x: torch.Tensor, router_logits: torch.Tensor, reduce: bool = True):
-        w, ids = moe_ops.topk_route(router_logits, self.k, self.renormalize, self.scoring)
+    def forward(self, x: torch.Tensor, router_logits: Optional[torch.Tensor] = None,
+                reduce: bool = True, router_w: Optional[torch.Tensor] = None):
+        if router_logits is None:     # fused router GEMM + top-k
+            w, ids = moe_ops.route(x, router_w, self.k, self.renormalize, self.scoring)
+        else:
+            w, ids = moe_ops.topk_route(router_logits, self.k, self.renormalize, self.scoring)
         if self.scale_input:
             # Llama-4 applies the routing score to the expert input (k = 1)
             x = (x.float() * w[:, :1]).to(x.dtype)
@@ -125,7 +129,10 @@ class MixtralMoE(nn.Module):
             self.shared_expert_gate = ReplicatedLinear(H, 1, dtype=dtype, device=device)
 
     def forward(self, x):
-        out = self.experts(x, self.gate(x), reduce=False)
+        if self.gate.bias is None and x.dim() == 2:
+            out = self.experts(x, None, reduce=False, router_w=self.gate.weight)
+        else:
+            out = self.experts(x, self.gate(x), reduce=False)
         if self.shared_expert is not None:
             s = self.shared_expert(x)
             s = s.materialize() if hasattr(s, "materialize") else s

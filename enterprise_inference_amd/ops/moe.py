@@ -1,9 +1,17 @@
 """Fused MoE (K9) -> csrc/kernels/moe.hip + the grouped skinny GEMM (gemm_skinny.hip).
 
-Decode-sized batches (tokens per expert <= 128 on average) run entirely in HIP:
-top-k routing, on-device expert alignment, grouped gate_up GEMM with the SwiGLU
-epilogue, grouped down GEMM, weighted combine.  Prefill-sized batches run one
-hipBLASLt GEMM pair per expert on the gathered rows (MFMA-bound there).
+Both regimes run entirely on the device with no host synchronisation: top-k routing,
+on-device expert alignment (offsets + sorted token list), grouped gate_up GEMM with the
+SwiGLU epilogue, grouped down GEMM, weighted combine.  Decode-sized batches (<= 96 rows per
+expert on average) use the weight-streaming grouped skinny GEMM (gemm_skinny.hip); prefill-
+sized batches use the MFMA grouped GEMM (moe_gemm.hip), whose grid is an upper bound that
+each workgroup maps to (expert, M tile) from the device-side offsets (graph-capturable).  Past
+128 rows per expert hipBLASLt's tiles are faster (Mixtral-8x7B, profiles/moe_bench_r2.log:
+512 / 2048 / 8192 tokens = 0.98 / 1.89 / 5.19 ms against 1.08 / 2.42 / 8.13 ms for the
+grouped MFMA kernel), so that regime reads the E+1 offsets back once per layer and runs one
+GEMM pair per expert on contiguous slices of the sorted rows (the old path synchronised once
+per expert through nonzero() and scattered with fp32 index_add: 1.43 ms at 65 tokens,
+profiles/moe_bench_r2.log first run).
 
 Expert parallelism (``--enable-expert-parallel``, core/helm-charts/vllm/gaudi3-values.yaml:492):
 rank r owns experts [e_lo, e_hi); tokens routed elsewhere contribute zero locally
@@ -41,6 +49,24 @@ def topk_route(logits: torch.Tensor, k: int, renormalize: bool = True,
     return w, ids
 
 
+def route(x: torch.Tensor, router_w: torch.Tensor, k: int, renormalize: bool = True,
+          scoring: str = "softmax") -> Tuple[torch.Tensor, torch.Tensor]:
+    """Router GEMM + top-k.  On the GPU one kernel computes the E logits per token (bf16
+    rounded, like the Linear it replaces) and selects (moe.hip route_kernel)."""
+    T, H = x.shape
+    E = router_w.shape[0]
+    if (use_hip(x) and x.dtype == torch.bfloat16 and router_w.dtype == torch.bfloat16
+            and E <= 64 and H % 8 == 0 and x.stride(1) == 1 and x.stride(0) % 8 == 0
+            and router_w.is_contiguous()):
+        w = torch.empty(T, k, dtype=torch.float32, device=x.device)
+        ids = torch.empty(T, k, dtype=torch.int32, device=x.device)
+        check(lib().eia_moe_route(ptr(x), x.stride(0), ptr(router_w), H, T, E, k,
+                                  1 if renormalize else 0, SCORING[scoring], ptr(w), ptr(ids),
+                                  stream(x)), "moe_route")
+        return w, ids
+    return topk_route(F.linear(x, router_w), k, renormalize, scoring)
+
+
 def _grouped_ok(x, w13, w2) -> bool:
     return (x.dtype == torch.bfloat16 and x.shape[1] % 256 == 0 and w2.shape[2] % 256 == 0
             and (w13.shape[1] // 2) % 32 == 0 and w2.shape[1] % 64 == 0)
@@ -62,32 +88,85 @@ def fused_moe(x: torch.Tensor, w13: torch.Tensor, w2: torch.Tensor, topk_w: torc
     avg = T * k / max(1, El)
     if act == "silu" and avg <= 96 and _grouped_ok(x, w13, w2):
         return _fused_moe_grouped(x, w13, w2, topk_w, topk_ids, e_lo, e_hi)
+    if act == "silu" and _mfma_ok(x, w13, w2) and avg <= MFMA_MAX_ROWS:
+        return _fused_moe_grouped(x, w13, w2, topk_w, topk_ids, e_lo, e_hi, mfma=True)
+    if _grouped_ok(x, w13, w2):
+        return _fused_moe_sorted_blas(x, w13, w2, topk_w, topk_ids, e_lo, e_hi, act)
     return _fused_moe_per_expert(x, w13, w2, topk_w, topk_ids, e_lo, act)
 
 
-def _fused_moe_grouped(x, w13, w2, topk_w, topk_ids, e_lo, e_hi):
+MFMA_MAX_ROWS = 128      # rows per expert above which the per-expert hipBLASLt GEMMs win
+
+
+def _mfma_ok(x, w13, w2) -> bool:
+    H, I = x.shape[1], w13.shape[1] // 2
+    return (x.dtype == torch.bfloat16 and H % 128 == 0 and I % 64 == 0
+            and w13.is_contiguous() and w2.is_contiguous() and x.stride(1) == 1)
+
+
+def _fused_moe_grouped(x, w13, w2, topk_w, topk_ids, e_lo, e_hi, mfma: bool = False):
     T, H = x.shape
     El, I2, _ = w13.shape
     I = I2 // 2
     k = topk_ids.shape[1]
     n = T * k
     dev = x.device
+    st = stream(x)
+    offs, row_idx, inv = _align(topk_ids, El, e_lo, e_hi, n, dev, st)
+    h1 = torch.empty(max(1, n), I, dtype=x.dtype, device=dev)
+    h2 = torch.empty(max(1, n), H, dtype=x.dtype, device=dev)
+    if mfma:
+        check(lib().eia_moe_grouped_gemm(ptr(x), x.stride(0), ptr(row_idx), ptr(w13), I2, H, El,
+                                         ptr(offs), n, 1, ptr(h1), h1.stride(0), st),
+              "moe_grouped_gemm_gate_up")
+        check(lib().eia_moe_grouped_gemm(ptr(h1), h1.stride(0), None, ptr(w2), H, I, El,
+                                         ptr(offs), n, 0, ptr(h2), h2.stride(0), st),
+              "moe_grouped_gemm_down")
+    else:
+        mt = max(1, min(8, -(-int(1.5 * n / El + 1) // 16)))
+        check(lib().eia_moe_gemm(ptr(x), x.stride(0), ptr(w13), w13.stride(1), None, ptr(h1),
+                                 h1.stride(0), I2, H, El, ptr(offs), ptr(row_idx), mt, 2,
+                                 3 if (I % 64 == 0) else 1, st), "moe_gemm_gate_up")
+        check(lib().eia_moe_gemm(ptr(h1), h1.stride(0), ptr(w2), w2.stride(1), None, ptr(h2),
+                                 h2.stride(0), H, I, El, ptr(offs), None, mt, 0,
+                                 2 if H % 128 == 0 else 0, st), "moe_gemm_down")
+    out = torch.empty(T, H, dtype=x.dtype, device=dev)
+    check(lib().eia_moe_combine(ptr(h2), h2.stride(0), ptr(topk_w), ptr(inv), T, k, H, ptr(out),
+                                out.stride(0), st), "moe_combine")
+    return out
+
+
+def _align(topk_ids, El, e_lo, e_hi, n, dev, st):
     E_total = max(e_hi, int(El + e_lo))
     offs = torch.empty(El + 1, dtype=torch.int32, device=dev)
     row_idx = torch.empty(max(1, n), dtype=torch.int32, device=dev)
     inv = torch.empty(max(1, n), dtype=torch.int32, device=dev)
-    st = stream(x)
     check(lib().eia_moe_align(ptr(topk_ids), n, E_total, e_lo, e_hi, ptr(offs), ptr(row_idx),
-                              ptr(inv), k, st), "moe_align")
-    mt = max(1, min(8, -(-int(1.5 * n / El + 1) // 16)))
-    h1 = torch.empty(max(1, n), I, dtype=x.dtype, device=dev)
-    check(lib().eia_moe_gemm(ptr(x), x.stride(0), ptr(w13), w13.stride(1), None, ptr(h1),
-                             h1.stride(0), I2, H, El, ptr(offs), ptr(row_idx), mt, 2,
-                             3 if (I % 64 == 0) else 1, st), "moe_gemm_gate_up")
+                              ptr(inv), topk_ids.shape[1], st), "moe_align")
+    return offs, row_idx, inv
+
+
+def _fused_moe_sorted_blas(x, w13, w2, topk_w, topk_ids, e_lo, e_hi, act):
+    """Long-prompt regime: device-side alignment, ONE read-back of the expert offsets, one
+    hipBLASLt GEMM pair per expert on contiguous slices of the gathered rows, HIP combine."""
+    from . import activation
+
+    T, H = x.shape
+    El = w13.shape[0]
+    k = topk_ids.shape[1]
+    n = T * k
+    dev = x.device
+    st = stream(x)
+    offs, row_idx, inv = _align(topk_ids, El, e_lo, e_hi, n, dev, st)
+    xs = x.index_select(0, row_idx[:n].long())
+    bounds = offs.tolist()                     # the one host synchronisation of this layer
     h2 = torch.empty(max(1, n), H, dtype=x.dtype, device=dev)
-    check(lib().eia_moe_gemm(ptr(h1), h1.stride(0), ptr(w2), w2.stride(1), None, ptr(h2),
-                             h2.stride(0), H, I, El, ptr(offs), None, mt, 0,
-                             2 if H % 128 == 0 else 0, st), "moe_gemm_down")
+    for e in range(El):
+        a, b = bounds[e], bounds[e + 1]
+        if a == b:
+            continue
+        h = activation.act_and_mul(F.linear(xs[a:b], w13[e]), act)
+        torch.matmul(h, w2[e].t(), out=h2[a:b])
     out = torch.empty(T, H, dtype=x.dtype, device=dev)
     check(lib().eia_moe_combine(ptr(h2), h2.stride(0), ptr(topk_w), ptr(inv), T, k, H, ptr(out),
                                 out.stride(0), st), "moe_combine")
@@ -95,7 +174,8 @@ def _fused_moe_grouped(x, w13, w2, topk_w, topk_ids, e_lo, e_hi):
 
 
 def _fused_moe_per_expert(x, w13, w2, topk_w, topk_ids, e_lo, act):
-    """Prefill path: gather each expert's rows, two hipBLASLt GEMMs, weighted scatter-add."""
+    """Fallback for shapes / activations the grouped kernels do not cover (non-SiLU experts,
+    H % 128 or I % 64 != 0): per-expert hipBLASLt GEMMs on the gathered rows."""
     from . import activation
 
     T, H = x.shape

@@ -1,0 +1,62 @@
+#!/usr/bin/env python3
+"""Per-decode-step view of a rocprofv3 kernel trace (``*_kernel_trace.csv``).
+
+A decode step ends at the sampler's merge kernel; the last N complete steps are averaged:
+launches per step, kernel time per step, step span (first start -> last end) and the busy
+fraction (kernel time / span), then the per-kernel time per step.
+
+Usage: analyze_steps.py <kernel_trace.csv> [title] [steps] [end_kernel_substring]
+"""
+import collections
+import csv
+import re
+import sys
+
+
+def short(name: str) -> str:
+    m = re.search(r"MT(\d+x\d+x\d+)", name)
+    if name.startswith(("Cijk_", "Custom_Cijk")):
+        return f"hipBLASLt GEMM MT{m.group(1) if m else '?'}"
+    name = name.replace("void ", "").replace("(anonymous namespace)::", "")
+    return re.sub(r"\(.*", "", name)[:72]
+
+
+def main() -> int:
+    path = sys.argv[1]
+    title = sys.argv[2] if len(sys.argv) > 2 else path
+    nsteps = int(sys.argv[3]) if len(sys.argv) > 3 else 30
+    marker = sys.argv[4] if len(sys.argv) > 4 else "sample_merge"
+    rows = sorted(csv.DictReader(open(path)), key=lambda r: int(r["Start_Timestamp"]))
+    ends = [i for i, r in enumerate(rows) if marker in r["Kernel_Name"]]
+    if len(ends) < 2:
+        print(f"no steps found (marker {marker!r})")
+        return 1
+    nsteps = min(nsteps, len(ends) - 1)
+    pairs = list(zip(ends[-nsteps - 1:-1], ends[-nsteps:]))
+    agg = collections.defaultdict(list)
+    spans, busy, launches = [], [], []
+    for a, b in pairs:
+        ks = rows[a + 1:b + 1]
+        t0 = int(ks[0]["Start_Timestamp"])
+        t1 = int(ks[-1]["End_Timestamp"])
+        spans.append((t1 - t0) / 1e3)
+        k = sum(int(r["End_Timestamp"]) - int(r["Start_Timestamp"]) for r in ks) / 1e3
+        busy.append(k)
+        launches.append(len(ks))
+        for r in ks:
+            agg[short(r["Kernel_Name"])].append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3)
+    n = len(pairs)
+    span, kern = sum(spans) / n, sum(busy) / n
+    print(f"### {title}\n")
+    print(f"Last {n} decode steps: {sum(launches) / n:.0f} launches/step, kernel time "
+          f"{kern / 1e3:.3f} ms/step, span {span / 1e3:.3f} ms/step, busy {100 * kern / span:.1f} %\n")
+    print("| kernel | launches/step | µs/step | % of kernel time | avg µs |")
+    print("|---|---:|---:|---:|---:|")
+    for name, v in sorted(agg.items(), key=lambda kv: -sum(kv[1])):
+        per = sum(v) / n
+        print(f"| {name} | {len(v) / n:.1f} | {per:.1f} | {100 * per / kern:.1f} | {sum(v) / len(v):.2f} |")
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())
