@@ -2,15 +2,18 @@
 (docs/api-spec.yaml:479 onward; vLLM extras the reference exposes through its
 OpenAI surface) and chat ``response_format``.
 
-Each sequence carries a ``GuidedState`` that yields the allowed next-token ids
-(K13: applied as a -inf mask before the sampler kernel, engine/logits_process.py):
+Each sequence carries a ``GuidedState`` that yields the allowed next tokens as a device
+bool mask (K13: applied with one masked_fill before the sampler kernel,
+engine/logits_process.py):
 
-* choice -> token trie over the tokenised choices (exact, O(#choices));
-* regex  -> incremental partial-match of ``text + token_text`` with the
-  ``regex`` module (``partial=True``); candidate tokens are pre-filtered by their
-  first character class to keep the per-step scan cheap;
-* json   -> a JSON-schema subset compiled to a regex (objects with typed
-  properties, enums, arrays, nested objects; ``{}`` = any flat JSON object).
+* choice  -> token trie over the tokenised choices (exact, O(#choices));
+* regex   -> token-level FSM (engine/fsm.py): the pattern is compiled once into an NFA,
+  determinised lazily, and each DFA state's allowed-token set / mask is computed once per
+  process by walking the vocabulary trie -- shared by every request with the same pattern;
+* json    -> a JSON-schema subset compiled to a regex (objects with typed properties,
+  enums, arrays, nested objects; ``{}`` = any flat JSON object), then as regex;
+* grammar -> the regular subset of GBNF / Lark EBNF (``guided_grammar``) compiled to a
+  regex (engine/fsm.py grammar_to_regex); recursive grammars are rejected.
 """
 
 from __future__ import annotations
@@ -21,7 +24,7 @@ from typing import Dict, List, Optional
 try:
     import regex as _re
 except ImportError:  # pragma: no cover - regex ships in the image
-    _re = None
+    import re as _re
 
 # Whitespace between JSON tokens is capped: with an unbounded run a weakly-conditioned model
 # can spend its whole max_tokens budget on indentation and never close the document.
@@ -88,6 +91,16 @@ class GuidedState:
     def allowed_tokens(self) -> Optional[List[int]]:
         raise NotImplementedError
 
+    def allowed_mask(self, device, vocab: int):
+        """bool [vocab] on `device` (True = allowed)."""
+        import torch
+
+        m = torch.zeros(vocab, dtype=torch.bool)
+        ids = [t for t in (self.allowed_tokens() or []) if 0 <= t < vocab]
+        if ids:
+            m[torch.tensor(ids, dtype=torch.long)] = True
+        return m.to(device)
+
     def advance(self, token: int) -> None:
         raise NotImplementedError
 
@@ -122,50 +135,34 @@ class ChoiceState(GuidedState):
 
 
 class RegexState(GuidedState):
-    """Token-level constrained decoding by incremental partial regex matching."""
-
-    _vocab_cache: Dict[int, List[str]] = {}
+    """Token-level constrained decoding on a cached token FSM (engine/fsm.py)."""
 
     def __init__(self, pattern: str, tokenizer, vocab_size: int, eos_ids: List[int]):
-        if _re is None:
-            raise RuntimeError("guided_regex needs the `regex` module")
-        self.pat = _re.compile(pattern)
-        self.tok = tokenizer
-        self.eos = list(eos_ids)
-        key = id(tokenizer)
-        if key not in self._vocab_cache:
-            strs = []
-            for i in range(min(vocab_size, len(tokenizer))):
-                try:
-                    strs.append(tokenizer.decode([i], skip_special_tokens=True))
-                except Exception:   # noqa: BLE001
-                    strs.append("")
-            self._vocab_cache[key] = strs
-        self.strs = self._vocab_cache[key]
-        self.text = ""
+        from .fsm import token_fsm
+
+        self.fsm = token_fsm(pattern, tokenizer, vocab_size, eos_ids)
+        self.eos = set(self.fsm.eos)
+        self.sid = self.fsm.start
         self.done = False
 
     def allowed_tokens(self):
-        ok = []
-        for i, s in enumerate(self.strs):
-            if not s:
-                continue
-            if self.pat.fullmatch(self.text + s, partial=True) is not None:
-                ok.append(i)
-        if self.pat.fullmatch(self.text) is not None:
-            ok.extend(self.eos)
-        return ok if ok else list(self.eos)
+        return self.fsm.allowed_ids(self.sid).tolist()
+
+    def allowed_mask(self, device, vocab: int):
+        return self.fsm.mask(self.sid, device, vocab)
 
     def advance(self, token):
         if token in self.eos:
             self.done = True
             return
-        self.text += self.strs[token] if token < len(self.strs) else ""
-        m = self.pat.fullmatch(self.text)
-        if m is not None and self.pat.fullmatch(self.text + "￿", partial=True) is None:
-            # complete and cannot be extended: stop
-            self.done = not any(self.pat.fullmatch(self.text + s, partial=True) is not None
-                                for s in self.strs[:512] if s)
+        n = self.fsm.next_state(self.sid, token)
+        if n < 0:                  # not allowed (e.g. sampled from an unmasked fallback row)
+            self.done = True
+            return
+        self.sid = n
+        # complete and cannot be extended: stop
+        if self.fsm.char.accepting(n) and not self.fsm.can_continue(n):
+            self.done = True
 
     def is_done(self):
         return self.done
@@ -177,4 +174,7 @@ def make_guided_state(params, tokenizer, vocab_size: int) -> GuidedState:
         return ChoiceState(list(params.guided_choice), tokenizer, eos)
     if params.guided_regex:
         return RegexState(params.guided_regex, tokenizer, vocab_size, eos)
+    if getattr(params, "guided_grammar", None):
+        from .fsm import grammar_to_regex
+        return RegexState(grammar_to_regex(params.guided_grammar), tokenizer, vocab_size, eos)
     return RegexState(schema_to_regex(params.guided_json), tokenizer, vocab_size, eos)

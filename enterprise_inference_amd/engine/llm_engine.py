@@ -162,7 +162,8 @@ class LLMEngine:
             seed = (params.seed + i) if params.seed is not None else random.getrandbits(63)
             s = Sequence(request_id, prompt_token_ids, params, index=i, arrival_time=arrival,
                          seed=seed, priority=priority)
-            if params.guided_choice or params.guided_regex or params.guided_json is not None:
+            if (params.guided_choice or params.guided_regex or params.guided_json is not None
+                    or params.guided_grammar):
                 from .guided import make_guided_state
                 s.guided_state = make_guided_state(params, self.tokenizer, vocab)
             seqs.append(s)

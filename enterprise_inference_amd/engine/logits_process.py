@@ -71,9 +71,7 @@ def apply_logits_processors(logits: torch.Tensor, items: List) -> torch.Tensor:
             if stop_ids:
                 row[torch.tensor(stop_ids, device=row.device, dtype=torch.long)] = float("-inf")
         if s.guided_state is not None:
-            allowed = s.guided_state.allowed_tokens()
-            if allowed is not None:
-                mask = torch.full_like(row, float("-inf"))
-                mask[torch.tensor(allowed, device=row.device, dtype=torch.long)] = 0.0
-                row += mask
+            # cached device mask per FSM state: no per-step host->device copy of token lists
+            row.masked_fill_(~s.guided_state.allowed_mask(row.device, row.shape[0]),
+                             float("-inf"))
     return logits

@@ -30,10 +30,11 @@ class SamplingParams:
     include_stop_str_in_output: bool = False
     logit_bias: Optional[Dict[int, float]] = None
     allowed_token_ids: Optional[List[int]] = None
-    # guided decoding (choice / regex / json handled in engine/guided.py)
+    # guided decoding (choice / regex / json / grammar handled in engine/guided.py)
     guided_choice: Optional[List[str]] = None
     guided_regex: Optional[str] = None
     guided_json: Optional[object] = None
+    guided_grammar: Optional[str] = None
 
     def __post_init__(self) -> None:
         if isinstance(self.stop, str):
@@ -83,7 +84,7 @@ class SamplingParams:
     @property
     def needs_logit_processing(self) -> bool:
         return bool(self.logit_bias or self.allowed_token_ids or self.guided_choice
-                    or self.guided_regex or self.guided_json is not None
+                    or self.guided_regex or self.guided_json is not None or self.guided_grammar
                     or self.min_tokens > 0)
 
     def clone(self, **kw) -> "SamplingParams":

@@ -118,7 +118,8 @@ class _SamplingFields(OpenAIBase):
             elif guided_json is None:
                 guided_json = {}
         if self.guided_grammar:
-            raise ValueError("guided_grammar is not supported; use guided_json/guided_regex")
+            from ...engine.fsm import grammar_to_regex
+            grammar_to_regex(self.guided_grammar)      # reject unsupported grammars with a 400
         if self.use_beam_search:
             raise ValueError("use_beam_search is not supported; use best_of/n sampling")
         max_tokens = self.max_tokens if self.max_tokens is not None else default_max_tokens
@@ -138,6 +139,7 @@ class _SamplingFields(OpenAIBase):
             if self.logit_bias else None,
             allowed_token_ids=self.allowed_token_ids,
             guided_choice=self.guided_choice, guided_regex=self.guided_regex,
+            guided_grammar=self.guided_grammar,
             guided_json=guided_json)
 
 
