@@ -78,6 +78,9 @@ def make_parser(description: str = "MI355X OpenAI-compatible LLM server") -> arg
     a("--enable-auto-tool-choice", action="store_true")
     a("--trust-remote-code", action="store_true")
     a("--enable-expert-parallel", action="store_true")
+    a("--expert-parallel-dispatch", choices=["allreduce", "all_to_all"], default=None,
+      help="EP form: experts sharded + layer all-reduce (default) or all-to-all token "
+           "dispatch/combine (parallel/expert_parallel.py)")
     a("--override-generation-config", type=json.loads, default=None)
     a("--generation-config", default="auto")
     a("--tokenizer", default=None)
@@ -163,6 +166,9 @@ def engine_config_from_args(args: argparse.Namespace):
                         gpu_memory_utilization=args.gpu_memory_utilization,
                         cpu_kvcache_space_gb=float(os.environ.get("VLLM_CPU_KVCACHE_SPACE", 4)),
                         enable_prefix_caching=bool(args.enable_prefix_caching))
+    if getattr(args, "expert_parallel_dispatch", None):
+        # read by parallel/state.ep_dispatch() in this process and in spawned TP workers
+        os.environ["EIA_EP_DISPATCH"] = args.expert_parallel_dispatch
     par = ParallelConfig(tensor_parallel_size=args.tensor_parallel_size,
                          pipeline_parallel_size=args.pipeline_parallel_size,
                          enable_expert_parallel=args.enable_expert_parallel,

@@ -103,11 +103,22 @@ class FusedMoE(nn.Module):
             # Llama-4 applies the routing score to the expert input (k = 1)
             x = (x.float() * w[:, :1]).to(x.dtype)
             w = torch.ones_like(w)
+        if self.a2a:
+            from ..parallel.expert_parallel import moe_all_to_all_replicated
+            return moe_all_to_all_replicated(x, w, ids, self.w13, self.w2, self.e_lo,
+                                             self.e_per, state.tp_group())
         out = moe_ops.fused_moe(x, self.w13, self.w2, w, ids,
                                 (self.e_lo, self.e_lo + self.e_per) if self.ep else None)
         if reduce and state.tp_size() > 1:
             out = comm.all_reduce(out)
         return out
+
+    @property
+    def a2a(self) -> bool:
+        """All-to-all EP: the output comes back complete (no all-reduce follows).  Llama-4
+        (routing score applied to the expert input, shared expert summed before one
+        all-reduce) keeps the all-reduce form."""
+        return self.ep and not self.scale_input and state.ep_dispatch() == "all_to_all"
 
 
 class MixtralMoE(nn.Module):
@@ -133,10 +144,15 @@ class MixtralMoE(nn.Module):
             out = self.experts(x, None, reduce=False, router_w=self.gate.weight)
         else:
             out = self.experts(x, self.gate(x), reduce=False)
+        a2a = self.experts.a2a          # all-to-all EP: `out` is already complete
         if self.shared_expert is not None:
             s = self.shared_expert(x)
             s = s.materialize() if hasattr(s, "materialize") else s
+            if a2a:
+                s = comm.all_reduce(s)
             out = out + torch.sigmoid(self.shared_expert_gate(x).float()).to(x.dtype) * s
+        if a2a:
+            return out
         return _deferred_reduce(out)
 
 

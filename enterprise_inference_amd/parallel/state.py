@@ -139,6 +139,14 @@ def ep_enabled() -> bool:
     return _EP_ENABLED and _TP_SIZE > 1
 
 
+def ep_dispatch() -> str:
+    """EP form: "allreduce" (experts sharded, tokens replicated, the layer all-reduce sums)
+    or "all_to_all" (token slices dispatched to the expert owners,
+    parallel/expert_parallel.py).  --expert-parallel-dispatch / EIA_EP_DISPATCH."""
+    v = os.environ.get("EIA_EP_DISPATCH", "allreduce")
+    return v if v in ("allreduce", "all_to_all") else "allreduce"
+
+
 def is_driver() -> bool:
     """Rank 0 of its model replica (owns the scheduler)."""
     return _TP_RANK == 0 and _PP_RANK == 0
