@@ -193,6 +193,7 @@ class CacheConfig:
     gpu_memory_utilization: float = 0.90
     num_gpu_blocks: Optional[int] = None     # override (tests / bench)
     cpu_kvcache_space_gb: float = 4.0        # VLLM_CPU_KVCACHE_SPACE analogue
+    swap_space_gb: float = 4.0               # --swap-space: pinned host KV for preemption
     enable_prefix_caching: bool = True
     cache_dtype: Optional[torch.dtype] = None   # None -> model dtype
 

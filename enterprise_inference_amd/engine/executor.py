@@ -71,6 +71,20 @@ class UniprocExecutor:
     def launch(self, bm, sched, overlap: bool):
         return self.runner.launch(bm, sched, overlap)
 
+    # KV swap (K14): single-rank engines only -- TP/PP keep recompute preemption
+    def allocate_swap(self, swap_space_gb: float) -> int:
+        from .swap import swap_blocks_for
+        r = self.runner
+        if getattr(r, "kv_buf", None) is None:
+            return 0
+        return r.allocate_swap(swap_blocks_for(r.kv_bytes_per_block(), swap_space_gb))
+
+    def swap_out(self, gpu_blocks, cpu_blocks) -> None:
+        self.runner.swap_out(gpu_blocks, cpu_blocks)
+
+    def swap_in(self, cpu_blocks, gpu_blocks) -> None:
+        self.runner.swap_in(cpu_blocks, gpu_blocks)
+
     def shutdown(self) -> None:
         pass
 

@@ -99,6 +99,13 @@ class LLMEngine:
         self.executor = executor
         self.num_blocks = executor.num_blocks
         self.scheduler = Scheduler(cfg.scheduler, cfg.cache, self.num_blocks)
+        # K14 swap space (single-rank executors; TP/PP engines keep recompute preemption)
+        alloc = getattr(executor, "allocate_swap", None)
+        if alloc is not None and cfg.cache.swap_space_gb > 0:
+            from .swap import SwapSpace
+            n = alloc(cfg.cache.swap_space_gb)
+            if n > 0:
+                self.scheduler.swap = SwapSpace(n)
         m = cfg.model
         self.tokenizer = tokenizer or get_tokenizer(
             cfg.tokenizer or cfg.model_path, m.vocab_size, m.eos_token_id, m.bos_token_id,
@@ -194,6 +201,7 @@ class LLMEngine:
             return self._step_sync()
         t0 = time.time()
         sched = self.scheduler.schedule()
+        self._apply_swaps(sched)
         touched: Dict[str, _Request] = {}
         for s in self.scheduler.finished_since_last:
             r = self.requests.get(s.request_id)
@@ -269,6 +277,7 @@ class LLMEngine:
     def _step_sync(self) -> List[RequestOutput]:
         t0 = time.time()
         sched = self.scheduler.schedule()
+        self._apply_swaps(sched)
         touched: Dict[str, _Request] = {}
         for s in self.scheduler.finished_since_last:
             r = self.requests.get(s.request_id)
@@ -400,6 +409,18 @@ class LLMEngine:
 
     def kv_cache_usage(self) -> float:
         return self.scheduler.kv_usage()
+
+    def cpu_cache_usage(self) -> float:
+        return self.scheduler.cpu_usage()
+
+    def _apply_swaps(self, sched) -> None:
+        """K14: victims' blocks out to host memory, returning sequences' blocks back in --
+        on the step stream, before the step's kernels (out first: an in-swap may reuse a
+        block an out-swap just released)."""
+        for gpu, cpu in sched.swap_out:
+            self.executor.swap_out(gpu, cpu)
+        for cpu, gpu in sched.swap_in:
+            self.executor.swap_in(cpu, gpu)
 
     def shutdown(self) -> None:
         ex = getattr(self.executor, "shutdown", None)

@@ -346,6 +346,45 @@ class ModelRunner:
                     buf.numel() * buf.element_size() / 2**30)
         return nb
 
+    # ------------------------------------------------------------------ swap (K14)
+    def kv_bytes_per_block(self) -> int:
+        return 2 * self.num_local_layers * self.num_kv_heads * self.block_size * \
+            self.head_dim * self.kv_buf.element_size()
+
+    def allocate_swap(self, num_cpu_blocks: int) -> int:
+        """Pinned host mirror of the KV layout, [layers, 2, cpu_blocks, block elems]."""
+        self.num_cpu_blocks = int(num_cpu_blocks)
+        if self.num_cpu_blocks <= 0:
+            self.swap_buf = None
+            return 0
+        L, blk = self.num_local_layers, self.kv_buf.shape[2] // self.num_blocks
+        self.swap_buf = torch.empty(L, 2, self.num_cpu_blocks, blk, dtype=self.kv_buf.dtype,
+                                    pin_memory=self.is_gpu)
+        logger.info("KV swap space: %d blocks (%.1f GiB pinned)", self.num_cpu_blocks,
+                    self.swap_buf.numel() * self.swap_buf.element_size() / 2**30)
+        return self.num_cpu_blocks
+
+    def _kv_blocks(self) -> torch.Tensor:
+        return self.kv_buf.view(self.kv_buf.shape[0], 2, self.num_blocks, -1)
+
+    def swap_out(self, gpu_blocks: List[int], cpu_blocks: List[int]) -> None:
+        """Device blocks -> pinned host blocks (after the in-flight step on this stream)."""
+        if not gpu_blocks:
+            return
+        g = torch.tensor(gpu_blocks, dtype=torch.long, device=self.device)
+        data = self._kv_blocks().index_select(2, g).cpu()    # waits for the writers
+        self.swap_buf[:, :, torch.tensor(cpu_blocks, dtype=torch.long)] = data
+
+    def swap_in(self, cpu_blocks: List[int], gpu_blocks: List[int]) -> None:
+        """Pinned host blocks -> device blocks, ahead of the step that reads them."""
+        if not gpu_blocks:
+            return
+        data = self.swap_buf[:, :, torch.tensor(cpu_blocks, dtype=torch.long)]
+        if self.is_gpu:
+            data = data.pin_memory().to(self.device, non_blocking=True)
+        g = torch.tensor(gpu_blocks, dtype=torch.long, device=self.device)
+        self._kv_blocks().index_copy_(2, g, data)
+
     # ------------------------------------------------------------------ inputs
     def _decode_partitions(self, B: int, max_len: int) -> int:
         if not self.is_gpu:

@@ -6,8 +6,10 @@ Implements the knobs the reference passes to vLLM:
 xeon-values.yaml:80-83).  Policy per step:
   1. running sequences first (decodes, then unfinished prefill chunks), growing
      their block tables; on KV exhaustion the most recently admitted running
-     sequence is preempted (recompute mode) until the allocation fits;
-  2. then waiting sequences FCFS with prefix-cache lookup, chunked to the
+     sequence is preempted until the allocation fits -- swapped to pinned host memory
+     when the swap space (K14, --swap-space) can hold its blocks, else recompute;
+  2. swapped sequences come back first (FCFS) when their blocks fit again;
+  3. then waiting sequences FCFS with prefix-cache lookup, chunked to the
      remaining token budget when chunked prefill is enabled.
 Batch layout handed to the runner: [decode tokens | prefill chunks].
 """
@@ -17,7 +19,7 @@ from __future__ import annotations
 import collections
 import dataclasses
 import time
-from typing import Deque, Dict, List, Optional
+from typing import Deque, Dict, List, Optional, Tuple
 
 import numpy as np
 
@@ -43,6 +45,9 @@ class SchedulerOutput:
     prefills: List[ScheduledSeq]
     preempted: List[Sequence]
     num_batched_tokens: int
+    # KV swap copies to run before this step's kernels: (device blocks, host blocks)
+    swap_out: List[Tuple[List[int], List[int]]] = dataclasses.field(default_factory=list)
+    swap_in: List[Tuple[List[int], List[int]]] = dataclasses.field(default_factory=list)
 
     @property
     def empty(self) -> bool:
@@ -62,7 +67,11 @@ class Scheduler:
                                                 cache.enable_prefix_caching)
         self.waiting: Deque[Sequence] = collections.deque()
         self.running: List[Sequence] = []
+        self.swapped: Deque[Sequence] = collections.deque()
+        self.swap = None                  # engine.swap.SwapSpace when --swap-space > 0
+        self._swap_out: List[Tuple[List[int], List[int]]] = []
         self.num_preemptions = 0
+        self.num_swapouts = 0
         self.finished_since_last: List[Sequence] = []
 
     # ------------------------------------------------------------------ queue ops
@@ -71,7 +80,13 @@ class Scheduler:
         self.waiting.append(seq)
 
     def num_unfinished(self) -> int:
-        return len(self.waiting) + len(self.running)
+        return len(self.waiting) + len(self.running) + len(self.swapped)
+
+    def num_swapped(self) -> int:
+        return len(self.swapped)
+
+    def cpu_usage(self) -> float:
+        return self.swap.usage() if self.swap is not None else 0.0
 
     def finish(self, seq: Sequence, status: SeqStatus) -> None:
         if seq.finished:
@@ -80,6 +95,10 @@ class Scheduler:
         seq.finish_time = time.time()
         if seq in self.running:
             self.running.remove(seq)
+        elif seq in self.swapped:
+            self.swapped.remove(seq)
+            self.swap.free(seq.swap_blocks)
+            seq.swap_blocks = None
         else:
             try:
                 self.waiting.remove(seq)
@@ -88,7 +107,8 @@ class Scheduler:
         self.bm.free(seq)
 
     def abort_request(self, request_id: str) -> List[Sequence]:
-        out = [s for s in list(self.running) + list(self.waiting) if s.request_id == request_id]
+        out = [s for s in list(self.running) + list(self.waiting) + list(self.swapped)
+               if s.request_id == request_id]
         for s in out:
             self.finish(s, SeqStatus.FINISHED_ABORTED)
         return out
@@ -96,11 +116,22 @@ class Scheduler:
     # ------------------------------------------------------------------ scheduling
     def _preempt(self, seq: Sequence) -> None:
         self.running.remove(seq)
+        seq.num_preemptions += 1
+        self.num_preemptions += 1
+        nblk = -(-seq.num_computed_tokens // self.cache_cfg.block_size)
+        if self.swap is not None and nblk and self.swap.can_allocate(nblk):
+            gpu = list(self.bm.block_table(seq))[:nblk]
+            cpu = self.swap.allocate(nblk)
+            self._swap_out.append((gpu, cpu))
+            seq.swap_blocks = cpu
+            self.bm.free(seq)
+            seq.status = SeqStatus.SWAPPED
+            self.swapped.append(seq)
+            self.num_swapouts += 1
+            return
         self.bm.free(seq)
         seq.status = SeqStatus.PREEMPTED
         seq.num_computed_tokens = 0
-        seq.num_preemptions += 1
-        self.num_preemptions += 1
         self.waiting.appendleft(seq)
 
     def schedule(self) -> SchedulerOutput:
@@ -129,7 +160,7 @@ class Scheduler:
                 preempted.append(victim)
                 if victim is seq:
                     break
-            if seq.status == SeqStatus.PREEMPTED:
+            if seq.status in (SeqStatus.PREEMPTED, SeqStatus.SWAPPED):
                 continue          # seq itself was evicted; list shrank
             item = ScheduledSeq(seq, seq.num_computed_tokens, n)
             (decodes if remaining == 1 else prefills).append(item)
@@ -137,10 +168,37 @@ class Scheduler:
             budget -= n
             i += 1
 
-        # 2. waiting sequences, FCFS
+        # 2. swapped sequences back in, FCFS (not in a step that had to evict; not while a
+        # sampled token of theirs is still in flight)
+        swap_in: List[Tuple[List[int], List[int]]] = []
+        while (self.swapped and budget > 0 and not preempted
+               and len(self.running) < self.cfg.max_num_seqs):
+            seq = self.swapped[0]
+            if seq.num_pending:
+                break
+            remaining = seq.num_tokens - seq.num_computed_tokens
+            n = min(remaining, budget)
+            if n < remaining and not self.cfg.enable_chunked_prefill and remaining > 1:
+                break
+            if not self.bm.ensure(seq, seq.num_computed_tokens + n):
+                break
+            self.swapped.popleft()
+            nblk = len(seq.swap_blocks)
+            gpu = list(self.bm.block_table(seq))[:nblk]
+            swap_in.append((seq.swap_blocks, gpu))
+            self.swap.free(seq.swap_blocks)
+            seq.swap_blocks = None
+            seq.status = SeqStatus.RUNNING
+            self.running.append(seq)
+            item = ScheduledSeq(seq, seq.num_computed_tokens, n)
+            (decodes if remaining == 1 else prefills).append(item)
+            budget -= n
+
+        # 3. waiting sequences, FCFS
         n_prefill = len(prefills)
         while (self.waiting and budget > 0 and len(self.running) < self.cfg.max_num_seqs
-               and n_prefill < self.cfg.max_num_prefill_seqs and not preempted):
+               and n_prefill < self.cfg.max_num_prefill_seqs and not preempted
+               and not self.swapped):
             seq = self.waiting[0]
             if seq.num_tokens > self.cfg.max_model_len:
                 self.waiting.popleft()
@@ -168,7 +226,8 @@ class Scheduler:
             n_prefill += remaining > 1
 
         total = sum(s.num_tokens for s in decodes) + sum(s.num_tokens for s in prefills)
-        return SchedulerOutput(decodes, prefills, preempted, total)
+        swap_out, self._swap_out = self._swap_out, []
+        return SchedulerOutput(decodes, prefills, preempted, total, swap_out, swap_in)
 
     def update_after_step(self, out: SchedulerOutput) -> None:
         """Advance computed-token counters and register full blocks for prefix reuse."""

@@ -29,10 +29,11 @@ class SeqStatus(enum.Enum):
     FINISHED_STOPPED = 3
     FINISHED_LENGTH = 4
     FINISHED_ABORTED = 5
+    SWAPPED = 6                      # preempted with its KV parked in the host swap space
 
     @property
     def finished(self) -> bool:
-        return self.value >= 3
+        return 3 <= self.value <= 5
 
 
 FINISH_REASON = {
@@ -50,7 +51,7 @@ class Sequence:
                  "first_scheduled_time", "first_token_time", "last_token_time", "finish_time",
                  "stop_reason", "output_logprobs", "cumulative_logprob", "prompt_logprobs",
                  "detok_offset", "output_text", "prefix_offset", "read_offset", "lora",
-                 "num_preemptions", "seed", "guided_state", "token_times", "priority",
+                 "num_preemptions", "seed", "guided_state", "swap_blocks", "token_times", "priority",
                  "num_pending")
 
     def __init__(self, request_id: str, prompt_token_ids: List[int], params: SamplingParams,
@@ -82,6 +83,7 @@ class Sequence:
         self.num_preemptions = 0
         self.seed = seed
         self.guided_state = None
+        self.swap_blocks = None
         self.token_times: List[float] = []
         self.priority = priority
         # tokens sampled by a launched, not yet read-back step (overlapped scheduling): they

@@ -165,6 +165,7 @@ def engine_config_from_args(args: argparse.Namespace):
     cache = CacheConfig(block_size=args.block_size,
                         gpu_memory_utilization=args.gpu_memory_utilization,
                         cpu_kvcache_space_gb=float(os.environ.get("VLLM_CPU_KVCACHE_SPACE", 4)),
+                        swap_space_gb=float(args.swap_space),
                         enable_prefix_caching=bool(args.enable_prefix_caching))
     if getattr(args, "expert_parallel_dispatch", None):
         # read by parallel/state.ep_dispatch() in this process and in spawned TP workers
