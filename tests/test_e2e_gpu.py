@@ -122,25 +122,25 @@ def test_tei_encoders_gpu_match_cpu(cfgd):
         assert (a - b).abs().max().item() < 0.03 * (1 + b.abs().max().item()), (a, b)
 
 
-def test_kv_swap_under_pressure_matches_unpressured():
-    """K14 on the GPU path (HIP graphs, overlap): pinned-host swap-out/in of KV blocks."""
+def test_kv_swap_under_pressure_matches_fp32_oracle():
+    """K14 on the GPU path (HIP graphs, overlap): pinned-host swap-out/in of KV blocks.  Batch
+    compositions differ from an unpressured run (other GEMM buckets, other bf16 rounding), so
+    the check is teacher-forced against the fp32 oracle, which catches a corrupted block."""
     d = tiny_config("LlamaForCausalLM", **SHAPE)
-
-    def run(blocks, swap_gb):
-        cfg = EngineConfig(model=ModelConfig.from_hf_dict(d),
-                           cache=CacheConfig(block_size=128, num_gpu_blocks=blocks,
-                                             swap_space_gb=swap_gb, enable_prefix_caching=False),
-                           scheduler=SchedulerConfig(max_num_seqs=16, max_num_batched_tokens=512,
-                                                     max_model_len=2048),
-                           device="cuda", dtype=torch.bfloat16, load_format="dummy")
-        eng = LLMEngine(cfg)
-        gen = torch.Generator().manual_seed(4)
-        prompts = [torch.randint(3, 1000, (200 + 37 * i,), generator=gen).tolist() for i in range(6)]
-        params = SamplingParams(max_tokens=100, temperature=0, ignore_eos=True)
-        outs = eng.generate(prompt_token_ids=prompts, params=params)
-        return [o.outputs[0].token_ids for o in outs], eng.scheduler
-
-    ref, _ = run(64, 0)
-    got, sch = run(12, 1.0)        # 6 x ~400 tokens need ~18 blocks of 128
-    assert sch.num_swapouts > 0
-    assert got == ref
+    hf = hf_reference_model(d)
+    cfg = EngineConfig(model=ModelConfig.from_hf_dict(d),
+                       cache=CacheConfig(block_size=128, num_gpu_blocks=12, swap_space_gb=1.0,
+                                         enable_prefix_caching=False),
+                       scheduler=SchedulerConfig(max_num_seqs=16, max_num_batched_tokens=512,
+                                                 max_model_len=2048),
+                       device="cuda", dtype=torch.bfloat16, load_format="dummy")
+    eng = LLMEngine(cfg)
+    eng.executor.runner.model.load_weights(hf.state_dict().items())
+    gen = torch.Generator().manual_seed(4)
+    prompts = [torch.randint(3, 1000, (200 + 37 * i,), generator=gen).tolist() for i in range(6)]
+    params = SamplingParams(max_tokens=100, temperature=0, ignore_eos=True)
+    outs = eng.generate(prompt_token_ids=prompts, params=params)   # ~18 blocks needed, 12 here
+    assert eng.scheduler.num_swapouts > 0
+    toks = [o.outputs[0].token_ids for o in outs]
+    stats = check_greedy(hf, prompts, toks, tol=0.08)
+    assert stats["argmax_agreement"] > 0.8, stats
