@@ -8,6 +8,8 @@ loader serves TP=1..8 and the TP-vs-TP1 equivalence tests.
 
 from __future__ import annotations
 
+import os
+
 from typing import List, Optional, Sequence
 
 import torch
@@ -176,9 +178,14 @@ class RowParallelLinear(nn.Module):
     def forward(self, x, defer_reduce: bool = False):
         """With ``defer_reduce`` the consumer's add+RMSNorm absorbs the reduction: at TP=1 the
         result may be a ``gemm.SplitK`` (split-K partials summed in the norm kernel), at TP>1
-        a ``PendingAllReduce`` (all-reduce + add + norm in one xGMI kernel)."""
+        a ``PendingAllReduce`` (all-reduce + add + norm in one xGMI kernel).  Prefill-sized
+        inputs at TP>1 overlap the reduction with the GEMM instead (``_gemm_ar_overlapped``)."""
         if defer_reduce and (state.tp_size() == 1 or not self.reduce_results):
             return gemm.linear(x, self.weight, self.bias, defer_reduce=True)
+        if (self.reduce_results and state.tp_size() > 1 and x.dim() == 2
+                and x.shape[0] >= _overlap_min_tokens()):
+            y = self._gemm_ar_overlapped(x)
+            return y + self.bias if self.bias is not None else y
         y = gemm.linear(x, self.weight)
         if defer_reduce and self.bias is None and y.dim() == 2:
             return PendingAllReduce(y)
@@ -187,6 +194,35 @@ class RowParallelLinear(nn.Module):
         if self.bias is not None:
             y = y + self.bias
         return y
+
+
+    def _gemm_ar_overlapped(self, x: torch.Tensor) -> torch.Tensor:
+        """Token chunks: GEMM(chunk i+1) on the compute stream while RCCL all-reduces chunk i
+        on its own stream (async_op), so the xGMI reduction of a prefill step hides behind
+        the next chunk's MFMA work instead of following the whole GEMM."""
+        T = x.shape[0]
+        n = max(2, min(_OVERLAP_MAX_CHUNKS, T // _overlap_min_tokens() * 2))
+        y = torch.empty(T, self.out_features, dtype=x.dtype, device=x.device)
+        step = -(-T // n)
+        works = []
+        for a in range(0, T, step):
+            b = min(T, a + step)
+            torch.matmul(x[a:b], self.weight.t(), out=y[a:b])
+            works.append(comm.all_reduce_async(y[a:b]))
+        for w in works:
+            if w is not None:
+                w.wait()
+        return y
+
+
+_OVERLAP_MAX_CHUNKS = 4
+
+
+def _overlap_min_tokens() -> int:
+    """Read per call: every TP rank must take the same branch (EIA_TP_OVERLAP_MIN_TOKENS,
+    0 disables)."""
+    v = int(os.environ.get("EIA_TP_OVERLAP_MIN_TOKENS", "1024"))
+    return v if v > 0 else 1 << 62
 
 
 class ReplicatedLinear(nn.Module):

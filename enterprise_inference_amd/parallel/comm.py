@@ -37,6 +37,14 @@ def all_reduce(x: torch.Tensor) -> torch.Tensor:
     return x
 
 
+def all_reduce_async(x: torch.Tensor):
+    """RCCL all-reduce on the collective's own stream; returns the Work (wait() orders the
+    caller's stream after it) or None at TP=1."""
+    if state.tp_size() == 1:
+        return None
+    return dist.all_reduce(x, group=state.tp_group(), async_op=True)
+
+
 def all_reduce_add_rmsnorm(x: torch.Tensor, residual: torch.Tensor, weight: torch.Tensor,
                            eps: float):
     """(rmsnorm(residual + allreduce(x)) * w, residual) with residual updated in place.

@@ -94,3 +94,13 @@ def test_pipeline_parallel_matches_single(tmp_path, arch, tp, pp, layers):
     ref = _run(path, d, 1)
     got = _run(path, d, tp, pp=pp)
     assert got == ref
+
+
+def test_tp2_gemm_allreduce_overlap_matches_tp1(tmp_path, monkeypatch):
+    """Prefill chunks: GEMM of chunk i+1 overlapped with the async all-reduce of chunk i."""
+    d = tiny_config("LlamaForCausalLM")
+    path = _ckpt(tmp_path, d)
+    ref = _run(path, d, 1)
+    monkeypatch.setenv("EIA_TP_OVERLAP_MIN_TOKENS", "8")
+    got = _run(path, d, 2)
+    assert got == ref
