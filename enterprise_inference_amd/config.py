@@ -123,6 +123,7 @@ class ModelConfig:
     def from_hf_dict(cls, d: Dict[str, Any], name: str = "") -> "ModelConfig":
         arch = (d.get("architectures") or [d.get("model_type", "LlamaForCausalLM")])[0]
         text = d.get("text_config")
+        outer = d
         if text is not None and "hidden_size" not in d:   # Llama-4 style nesting
             merged = dict(text)
             merged.setdefault("architectures", [arch])
@@ -164,15 +165,23 @@ class ModelConfig:
         extra = {}
         L = d["num_hidden_layers"]
         if arch.startswith("Llama4"):
-            extra["no_rope_layers"] = d.get("no_rope_layers") or [
+            # an explicit empty list is a real value (e.g. all-dense layers), not "unset"
+            nrl = d.get("no_rope_layers")
+            extra["no_rope_layers"] = nrl if nrl else [
                 int((i + 1) % d.get("no_rope_layer_interval", 4) != 0) for i in range(L)]
             step = d.get("interleave_moe_layer_step", 1) or 1
-            extra["moe_layers"] = d.get("moe_layers") or [i for i in range(L) if (i + 1) % step == 0]
+            ml = d.get("moe_layers")
+            extra["moe_layers"] = list(ml) if ml is not None else [
+                i for i in range(L) if (i + 1) % step == 0]
             for key in ("use_qk_norm", "attn_temperature_tuning", "floor_scale", "attn_scale",
                         "intermediate_size_mlp"):
                 if key in d:
                     extra[key] = d[key]
             extra["rope_interleaved"] = True
+            if isinstance(outer.get("vision_config"), dict):    # multimodal checkpoint
+                extra["vision_config"] = dict(outer["vision_config"])
+                extra["image_token_id"] = outer.get("image_token_index",
+                                                    outer.get("image_token_id", 200092))
         kw["extra"] = extra
         if arch.startswith("OPT"):
             kw["position_offset"] = 2

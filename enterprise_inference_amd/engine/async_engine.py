@@ -76,13 +76,15 @@ class AsyncLLMEngine:
 
     # ------------------------------------------------------------------ API
     async def generate(self, request_id: str, prompt: Optional[str], params: SamplingParams,
-                       prompt_token_ids=None, priority: int = 0) -> AsyncIterator[RequestOutput]:
+                       prompt_token_ids=None, priority: int = 0,
+                       multi_modal_data=None) -> AsyncIterator[RequestOutput]:
         self.check_health()
         q: asyncio.Queue = asyncio.Queue()
         loop = asyncio.get_running_loop()
         self._streams[request_id] = q
         self._loops[request_id] = loop
-        self._cmds.put(("add", request_id, prompt, params, prompt_token_ids, time.time(), priority))
+        self._cmds.put(("add", request_id, prompt, params, prompt_token_ids, time.time(), priority,
+                        multi_modal_data))
         self._wake.set()
         try:
             while True:
@@ -140,10 +142,10 @@ class AsyncLLMEngine:
             except queue.Empty:
                 return
             if cmd[0] == "add":
-                _, rid, prompt, params, ids, arrival, prio = cmd
+                _, rid, prompt, params, ids, arrival, prio, mm = cmd
                 try:
                     self.engine.add_request(rid, prompt, params, ids, arrival_time=arrival,
-                                            priority=prio)
+                                            priority=prio, multi_modal_data=mm)
                     if self.log_requests:
                         logger.info("request %s added", rid)
                 except Exception as e:   # noqa: BLE001 - validation errors go to the client

@@ -25,7 +25,8 @@ class BlockManager:
         return self.native.has_seq(seq.seq_id)
 
     def allocate_prefix(self, seq: Sequence) -> int:
-        return self.native.allocate_prefix(seq.seq_id, self._toks(seq), 0)
+        return self.native.allocate_prefix(seq.seq_id, self._toks(seq),
+                                           getattr(seq, "cache_salt", 0) or 0)
 
     def ensure(self, seq: Sequence, num_tokens: int) -> bool:
         return self.native.ensure(seq.seq_id, num_tokens)
@@ -36,7 +37,8 @@ class BlockManager:
         nfull = seq.num_computed_tokens // self.block_size
         if nfull > self._committed.get(seq.seq_id, 0):
             toks = np.asarray(seq.all_token_ids[: nfull * self.block_size], dtype=np.int32)
-            self.native.commit(seq.seq_id, toks, nfull * self.block_size, 0)
+            self.native.commit(seq.seq_id, toks, nfull * self.block_size,
+                               getattr(seq, "cache_salt", 0) or 0)
             self._committed[seq.seq_id] = nfull
 
     def free(self, seq: Sequence) -> None:

@@ -173,10 +173,11 @@ def core_main(fd: int) -> int:
             for msg in reader.poll(0 if busy else 0.5):
                 k = msg[0]
                 if k == "add":
-                    _, rid, prompt, params, ids, arrival, prio = msg
+                    _, rid, prompt, params, ids, arrival, prio = msg[:7]
+                    mm = msg[7] if len(msg) > 7 else None
                     try:
                         engine.add_request(rid, prompt, params, ids, arrival_time=arrival,
-                                           priority=prio)
+                                           priority=prio, multi_modal_data=mm)
                         if log_requests:
                             logger.info("request %s added", rid)
                     except Exception as e:   # noqa: BLE001 - validation error -> the client
@@ -342,7 +343,7 @@ class MPEngineClient:
         self._writer.write(encode_frame(obj))
 
     async def generate(self, request_id: str, prompt: Optional[str], params,
-                       prompt_token_ids=None, priority: int = 0):
+                       prompt_token_ids=None, priority: int = 0, multi_modal_data=None):
         self.check_health()
         if self._writer is None:
             await self.start()
@@ -354,7 +355,8 @@ class MPEngineClient:
         if not self._reqs:
             self._last_msg = time.time()       # idle gap is not a stuck step
         self._reqs[request_id] = _ReqState(q, prompt, list(prompt_token_ids))
-        self._send(("add", request_id, prompt, params, prompt_token_ids, time.time(), priority))
+        self._send(("add", request_id, prompt, params, prompt_token_ids, time.time(), priority,
+                    multi_modal_data))
         finished = False
         try:
             while True:

@@ -82,6 +82,13 @@ class UniprocExecutor:
     def swap_out(self, gpu_blocks, cpu_blocks) -> None:
         self.runner.swap_out(gpu_blocks, cpu_blocks)
 
+    def encode_images(self, pixel_values):
+        """Vision tower + projector on this rank's device (multimodal prompts, TP=1)."""
+        enc = getattr(self.runner.model, "encode_images", None)
+        if enc is None:
+            raise ValueError("this model does not accept image inputs")
+        return enc(pixel_values)
+
     def swap_in(self, cpu_blocks, gpu_blocks) -> None:
         self.runner.swap_in(cpu_blocks, gpu_blocks)
 
@@ -161,14 +168,26 @@ class TPExecutor:
                                 args=(cfg, r, tp, port, self.ring_name, os.getpid()), daemon=True)
                 p.start()
                 self.procs.append(p)
+            keys = ("RANK", "WORLD_SIZE", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT",
+                    "TORCHELASTIC_USE_AGENT_STORE")
+            saved = {k: os.environ.get(k) for k in keys}
             os.environ.update(RANK="0", WORLD_SIZE=str(tp), LOCAL_RANK="0",
                               MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
             os.environ.pop("TORCHELASTIC_USE_AGENT_STORE", None)   # this rank hosts the store
             if cfg.device == "cuda" and torch.cuda.device_count() > 0:
                 torch.cuda.set_device(0)
-            pstate.init_distributed(cfg.parallel.tensor_parallel_size,
-                                    enable_expert_parallel=cfg.parallel.enable_expert_parallel,
-                                    pp_size=cfg.parallel.pipeline_parallel_size)
+            try:
+                pstate.init_distributed(cfg.parallel.tensor_parallel_size,
+                                        enable_expert_parallel=cfg.parallel.enable_expert_parallel,
+                                        pp_size=cfg.parallel.pipeline_parallel_size)
+            finally:
+                # the rendezvous env is only for init: leaving it behind would make a later
+                # engine in this process think it is a torchrun-launched rank
+                for k, v in saved.items():
+                    if v is None:
+                        os.environ.pop(k, None)
+                    else:
+                        os.environ[k] = v
             self._start_monitor()
         self.runner = setup_runner(cfg)
         self.num_blocks = self.runner.num_blocks

@@ -141,7 +141,8 @@ class LLMEngine:
     def add_request(self, request_id: str, prompt: Optional[str] = None,
                     params: Optional[SamplingParams] = None,
                     prompt_token_ids: Optional[List[int]] = None,
-                    arrival_time: Optional[float] = None, priority: int = 0) -> None:
+                    arrival_time: Optional[float] = None, priority: int = 0,
+                    multi_modal_data: Optional[dict] = None) -> None:
         if request_id in self.requests:
             raise ValueError(f"duplicate request id {request_id}")
         params = params or SamplingParams()
@@ -164,6 +165,7 @@ class LLMEngine:
             params = params.clone(logprobs=0)
             params.eos_ids = sorted(self.eos_ids)
         arrival = arrival_time if arrival_time is not None else time.time()
+        mm = self._encode_images(multi_modal_data, prompt_token_ids) if multi_modal_data else None
         seqs = []
         for i in range(params.best_of):
             seed = (params.seed + i) if params.seed is not None else random.getrandbits(63)
@@ -173,6 +175,8 @@ class LLMEngine:
                     or params.guided_grammar):
                 from .guided import make_guided_state
                 s.guided_state = make_guided_state(params, self.tokenizer, vocab)
+            if mm is not None:
+                s.mm_embeds, s.mm_positions, s.cache_salt = mm
             seqs.append(s)
             self.scheduler.add(s)
         self.requests[request_id] = _Request(request_id, prompt, list(prompt_token_ids), params,
@@ -391,14 +395,16 @@ class LLMEngine:
 
     # ------------------------------------------------------------------ helpers
     def generate(self, prompts: Optional[Seq[str]] = None, params=None,
-                 prompt_token_ids: Optional[Seq[List[int]]] = None) -> List[RequestOutput]:
+                 prompt_token_ids: Optional[Seq[List[int]]] = None,
+                 multi_modal_data: Optional[Seq[Optional[dict]]] = None) -> List[RequestOutput]:
         n = len(prompts) if prompts is not None else len(prompt_token_ids)
         plist = params if isinstance(params, list) else [params or SamplingParams()] * n
         ids = []
         for i in range(n):
             rid = f"gen-{time.time_ns()}-{i}"
             self.add_request(rid, prompts[i] if prompts is not None else None, plist[i],
-                             prompt_token_ids[i] if prompt_token_ids is not None else None)
+                             prompt_token_ids[i] if prompt_token_ids is not None else None,
+                             multi_modal_data=multi_modal_data[i] if multi_modal_data else None)
             ids.append(rid)
         done: Dict[str, RequestOutput] = {}
         while len(done) < n:
@@ -409,6 +415,43 @@ class LLMEngine:
 
     def kv_cache_usage(self) -> float:
         return self.scheduler.kv_usage()
+
+    def _encode_images(self, mm: dict, prompt_token_ids: List[int]):
+        """Vision tower at admission: -> (embeddings [n, hidden] on the device, prompt positions
+        of the n image-placeholder tokens, prefix-cache salt from the image bytes)."""
+        import hashlib
+
+        import numpy as np
+        import torch
+
+        images = mm.get("image") or []
+        if not isinstance(images, (list, tuple)):
+            images = [images]
+        if not images:
+            return None
+        enc = getattr(self.executor, "encode_images", None)
+        model = getattr(getattr(self.executor, "runner", None), "model", None)
+        tower = getattr(model, "vision", None)
+        if enc is None or tower is None:
+            raise ValueError("this deployment does not accept image inputs (needs a vision "
+                             "checkpoint served with tensor_parallel_size=1)")
+        from ..models.llama4_vision import preprocess
+        h = hashlib.blake2b(digest_size=8)
+        embeds = []
+        for img in images:
+            if isinstance(img, torch.Tensor):
+                pv = img
+                h.update(pv.float().numpy().tobytes())
+            else:
+                pv, _ = preprocess(img, tile=tower.image_size)
+                h.update(img if isinstance(img, (bytes, bytearray)) else str(img).encode())
+            embeds.append(enc(pv))
+        emb = torch.cat(embeds)
+        pos = np.flatnonzero(np.asarray(prompt_token_ids) == model.image_token_id).astype(np.int64)
+        if len(pos) != emb.shape[0]:
+            raise ValueError(f"prompt has {len(pos)} image placeholder tokens but the images "
+                             f"produce {emb.shape[0]} embeddings")
+        return emb, pos, int.from_bytes(h.digest(), "little") & ((1 << 63) - 1)
 
     def cpu_cache_usage(self) -> float:
         return self.scheduler.cpu_usage()

@@ -66,12 +66,12 @@ class StepPlan:
     the staging bytes (``ModelRunner.encode_plan``) -- no pickling on the step path."""
 
     __slots__ = ("kind", "Bp", "nd", "T", "npf", "mb_d", "mb_p", "n_work", "n_lidx", "P", "off",
-                 "src", "n_sample", "unfiltered", "sharded", "o")
+                 "src", "n_sample", "unfiltered", "sharded", "o", "mm")
 
     def __init__(self, kind: str, **kw):
         self.kind = kind
         for k in self.__slots__[1:]:
-            setattr(self, k, kw.get(k, {} if k == "o" else 0))
+            setattr(self, k, kw.get(k, {} if k == "o" else (None if k == "mm" else 0)))
 
     def __getitem__(self, k):           # plan["nd"] style access
         return getattr(self, k)
@@ -543,6 +543,7 @@ class ModelRunner:
             plan = self._prepare_graph(bm, out.decodes, Bp)
         else:
             plan = self._prepare_eager(bm, out)
+            plan.mm = self._mm_rows(out)
         items = out.decodes + [p for p in out.prefills if p.samples]
         plan.n_sample = len(items)
         if items:
@@ -550,6 +551,27 @@ class ModelRunner:
             plan.sharded = self.sharded_lm and plan.unfiltered and not any(
                 needs_host_processing(it.seq) for it in items)
         return plan
+
+    def _mm_rows(self, out: SchedulerOutput):
+        """(batch rows, embeddings) of the image-placeholder tokens in this step's prefill
+        chunks (single-rank engines; the embeddings were computed at admission)."""
+        rows, parts = [], []
+        acc = len(out.decodes)
+        for it in out.prefills:
+            seq = it.seq
+            emb = getattr(seq, "mm_embeds", None)
+            if emb is not None:
+                pos = seq.mm_positions
+                lo = int(np.searchsorted(pos, it.start))
+                hi = int(np.searchsorted(pos, it.start + it.num_tokens))
+                if hi > lo:
+                    rows.append(pos[lo:hi] - it.start + acc)
+                    parts.append(emb[lo:hi])
+            acc += it.num_tokens
+        if not rows:
+            return None
+        r = torch.from_numpy(np.concatenate(rows).astype(np.int64)).to(self.device)
+        return r, torch.cat(parts)
 
     def _staging_words(self, plan: StepPlan):
         """int32 views of the staging regions `plan` reads, in wire order."""
@@ -591,6 +613,8 @@ class ModelRunner:
         off = plan["off"]
         self.d_e_buf[:off].copy_(self.e_buf[:off], non_blocking=True)
         ids, md, lidx = self._eager_inputs(plan)
+        if plan.mm is not None:
+            md.mm_rows, md.mm_embeds = plan.mm
         if self.pp > 1:
             return self._run_stage(ids, md, lidx, plan["n_lidx"])
         h = self.model(ids, md, self.kv_caches)

@@ -51,7 +51,8 @@ class Sequence:
                  "first_scheduled_time", "first_token_time", "last_token_time", "finish_time",
                  "stop_reason", "output_logprobs", "cumulative_logprob", "prompt_logprobs",
                  "detok_offset", "output_text", "prefix_offset", "read_offset", "lora",
-                 "num_preemptions", "seed", "guided_state", "swap_blocks", "token_times", "priority",
+                 "num_preemptions", "seed", "guided_state", "swap_blocks", "mm_embeds",
+                 "mm_positions", "cache_salt", "token_times", "priority",
                  "num_pending")
 
     def __init__(self, request_id: str, prompt_token_ids: List[int], params: SamplingParams,
@@ -84,6 +85,9 @@ class Sequence:
         self.seed = seed
         self.guided_state = None
         self.swap_blocks = None
+        self.mm_embeds = None          # [n image tokens, hidden] on the device
+        self.mm_positions = None       # prompt positions of those tokens (sorted int64)
+        self.cache_salt = 0            # prefix-cache key salt (image content hash)
         self.token_times: List[float] = []
         self.priority = priority
         # tokens sampled by a launched, not yet read-back step (overlapped scheduling): they

@@ -13,7 +13,7 @@ from __future__ import annotations
 import functools
 import json
 import os
-from typing import Any, Dict, List, Optional
+from typing import Tuple, Any, Dict, List, Optional
 
 import jinja2
 from jinja2.sandbox import ImmutableSandboxedEnvironment
@@ -50,12 +50,38 @@ def _compile(template: str) -> jinja2.Template:
     return env.from_string(template)
 
 
+IMAGE_MARK = "\x00eia-image\x00"
+
+
+def extract_images(messages: List[Any]) -> Tuple[List[Dict[str, Any]], List[str]]:
+    """Replace image content parts (``image_url`` / ``image``) by a text marker, in order, and
+    return the image sources (data: URL, http(s) URL or path)."""
+    out, images = [], []
+    for m in messages:
+        m = dict(m) if isinstance(m, dict) else m.model_dump()
+        c = m.get("content")
+        if isinstance(c, list):
+            parts = []
+            for p in c:
+                p = p if isinstance(p, dict) else p.model_dump()
+                t = p.get("type", "text")
+                if t in ("image_url", "image"):
+                    iu = p.get("image_url") or p.get("image")
+                    images.append(iu.get("url") if isinstance(iu, dict) else iu)
+                    parts.append({"type": "text", "text": IMAGE_MARK})
+                else:
+                    parts.append(p)
+            m["content"] = parts
+        out.append(m)
+    return out, images
+
+
 def _normalise(messages: List[Dict[str, Any]]) -> List[Dict[str, Any]]:
     out = []
     for m in messages:
         m = dict(m)
         c = m.get("content")
-        if isinstance(c, list):   # content parts: keep text parts (vision parts are not served)
+        if isinstance(c, list):   # content parts: text (image parts became markers, extract_images)
             m["content"] = "".join(p.get("text", "") for p in c
                                    if isinstance(p, dict) and p.get("type", "text") == "text")
         if m.get("content") is None:

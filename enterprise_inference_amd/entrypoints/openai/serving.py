@@ -326,6 +326,75 @@ def _tools_for_request(req: ChatCompletionRequest, ctx: ServingContext):
     return tools, True, None
 
 
+def _vision_config(ctx) -> Optional[Dict]:
+    cfg = getattr(ctx.engine, "cfg", None) or getattr(getattr(ctx.engine, "engine", None),
+                                                       "cfg", None)
+    return None if cfg is None else cfg.model.extra.get("vision_config")
+
+
+def _special_id(tok, name: str) -> Optional[int]:
+    try:
+        i = tok.convert_tokens_to_ids(name)
+    except Exception:   # noqa: BLE001 - tokenizers without that vocabulary entry
+        return None
+    return i if isinstance(i, int) and i != getattr(tok, "unk_token_id", None) else None
+
+
+def _expand_images(ctx, prompt: str, images: List[str], add_special: bool):
+    """Chat prompt with image markers -> (text, token ids, multi_modal_data).  Every marker
+    becomes the Llama-4 image block for that image's tile grid (<|image_start|>, per-tile patch
+    runs with tile separators, the global tile, <|image_end|>); the patch token is the model's
+    image_token_id, so the ids are built here rather than by re-tokenising the expanded text.
+    The image bytes travel to the engine, which runs the vision tower at admission."""
+    from ...models.llama4_vision import expand_image_prompt, load_image, preprocess
+    from .chat_utils import IMAGE_MARK
+    vc = _vision_config(ctx)
+    if vc is None:
+        raise RequestError(f"model `{ctx.model}` does not accept image inputs")
+    cfg = getattr(ctx.engine, "cfg", None) or ctx.engine.engine.cfg
+    patch_id = int(cfg.model.extra["image_token_id"])
+    tile = vc.get("image_size", 336)
+    per_tile = int((tile // vc.get("patch_size", 14)) ** 2 * vc.get("pixel_shuffle_ratio", 0.5) ** 2)
+    tok = ctx.tokenizer
+    sp = {n: _special_id(tok, f"<|{n}|>") for n in ("image_start", "image_end", "image",
+                                                    "tile_x_separator", "tile_y_separator")}
+
+    def block(th: int, tw: int) -> List[int]:
+        out = [sp["image_start"]]
+        if th * tw > 1:
+            for _ in range(th):
+                for x in range(tw):
+                    out += [patch_id] * per_tile
+                    if x < tw - 1:
+                        out.append(sp["tile_x_separator"])
+                out.append(sp["tile_y_separator"])
+        out += [sp["image"]] + [patch_id] * per_tile + [sp["image_end"]]
+        return [i for i in out if i is not None]
+
+    segs = prompt.split(IMAGE_MARK)
+    if len(segs) != len(images) + 1:
+        raise RequestError("image marker mismatch in the rendered chat prompt")
+    ids = tok.encode(segs[0], add_special_tokens=add_special) if segs[0] or add_special else []
+    text, blobs = segs[0], []
+    for src, seg in zip(images, segs[1:]):
+        if not isinstance(src, str) or not src.startswith(("data:", "http://", "https://")):
+            raise RequestError("image_url must be a data: URL or an http(s) URL")
+        try:
+            img = load_image(src)
+            buf = __import__("io").BytesIO()
+            img.save(buf, format="PNG")
+            data = buf.getvalue()
+            _, (th, tw) = preprocess(data, tile=tile)
+        except Exception as e:   # noqa: BLE001 - unreadable image: client error
+            raise RequestError(f"could not load image: {e}") from e
+        ids += block(th, tw)
+        if seg:
+            ids += tok.encode(seg, add_special_tokens=False)
+        text += expand_image_prompt((th, tw), per_tile) + seg
+        blobs.append(data)
+    return text, ids, {"image": blobs}
+
+
 async def create_chat_completion(req: ChatCompletionRequest, ctx: ServingContext):
     ctx.check_model(req.model)
     tools, parse_tools, forced = _tools_for_request(req, ctx)
@@ -335,16 +404,25 @@ async def create_chat_completion(req: ChatCompletionRequest, ctx: ServingContext
         template = resolve_chat_template(req.chat_template)
     elif ctx.chat_template:
         template = ctx.chat_template
+    from .chat_utils import extract_images
+    messages, images = extract_images(req.messages)
     try:
-        prompt = apply_chat_template(ctx.tokenizer, req.messages, template, tools,
+        prompt = apply_chat_template(ctx.tokenizer, messages, template, tools,
                                      req.add_generation_prompt, req.continue_final_message,
                                      req.documents, **(req.chat_template_kwargs or {}))
     except RequestError:
         raise
     except Exception as e:   # noqa: BLE001 - template errors are client errors
         raise RequestError(f"chat template error: {e}") from e
+    mm = None
     add_special = req.add_special_tokens if req.add_special_tokens is not None else False
-    text, ids = ctx.tokenize_prompt(prompt, add_special, req.truncate_prompt_tokens)
+    if images:
+        if req.truncate_prompt_tokens:
+            raise RequestError("truncate_prompt_tokens cannot be combined with image inputs")
+        text, ids, mm = _expand_images(ctx, prompt, images, add_special)
+        _, ids = ctx.tokenize_prompt(ids)
+    else:
+        text, ids = ctx.tokenize_prompt(prompt, add_special, req.truncate_prompt_tokens)
     top_n = (req.top_logprobs or 0) if req.logprobs else None
     max_tokens = req.max_completion_tokens or req.max_tokens
     if max_tokens is not None:
@@ -356,7 +434,8 @@ async def create_chat_completion(req: ChatCompletionRequest, ctx: ServingContext
         params.guided_json = fn.parameters or {}
     rid = random_id("chatcmpl")
     created = int(time.time())
-    gen = ctx.engine.generate(rid, text, params, prompt_token_ids=ids, priority=req.priority)
+    gen = ctx.engine.generate(rid, text, params, prompt_token_ids=ids, priority=req.priority,
+                              **({"multi_modal_data": mm} if mm else {}))
     n = params.n
 
     if not req.stream:

@@ -148,6 +148,8 @@ class LlamaForCausalLM(nn.Module):
         stage, which passes them back in as ``intermediate``."""
         if self.first:
             h, residual = self.embed_tokens(input_ids), None
+            if getattr(md, "mm_rows", None) is not None:   # image placeholders (Llama-4 vision)
+                h = h.index_copy(0, md.mm_rows, md.mm_embeds.to(h.dtype))
         else:
             h, residual = intermediate
         for i in range(self.start_layer, self.end_layer):

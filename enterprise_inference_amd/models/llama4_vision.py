@@ -1,0 +1,278 @@
+"""Llama-4 vision path: image tiles -> ViT encoder -> pixel-shuffle adapter -> projector into
+the text model's embedding space (Llama-4-Scout-17B-16E-Instruct is multimodal; reference
+core/lib/models/model-selection.sh:33).
+
+Pipeline (checkpoint names ``vision_model.*`` / ``multi_modal_projector.*``):
+  preprocess (here, PIL + numpy): best-fit tile canvas of up to ``max_tiles`` 336x336 tiles
+    without distortion, pad, normalise (mean 0.5 / std 0.5), split into tiles, plus a global
+    thumbnail tile when there is more than one;
+  encoder (per tile): 14x14 patch unfold + linear, class token, learned positions, pre-norm,
+    N x [LayerNorm -> MHA with 2-D rotary (x, y patch coordinates, complex pairs) -> LayerNorm
+    -> GELU MLP], post-norm, drop the class token;
+  adapter: pixel shuffle (ratio 0.5: 576 patches -> 144 tokens of 4x the width) -> GELU MLP;
+  projector: linear to the text hidden size.
+Each image becomes ``tiles x 144`` embeddings that replace the ``<|patch|>`` placeholder
+tokens of its prompt expansion (``expand_image_prompt``), written over the token embeddings
+of those positions in the prefill batch (models/llama.py forward, ``md.mm_rows``).
+
+Linear layers run through ops.gemm (hipBLASLt / skinny HIP kernels), LayerNorm through the HIP
+layer-norm kernel, attention through PyTorch SDPA (577 non-causal tokens per tile, once per
+image -- not a hot path).
+"""
+
+from __future__ import annotations
+
+import base64
+import io
+import math
+from typing import List, Optional, Sequence, Tuple
+
+import numpy as np
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+from ..ops import gemm
+
+TILE = 336
+PATCH = 14
+
+
+# ----------------------------------------------------------------------------- preprocessing
+def _supported_canvases(max_tiles: int, tile: int = TILE) -> List[Tuple[int, int]]:
+    out = []
+    for n in range(max_tiles, 0, -1):
+        for h in range(1, n + 1):
+            if n % h == 0:
+                out.append((h * tile, (n // h) * tile))
+    return sorted(set(out))
+
+
+def best_fit_canvas(h: int, w: int, max_tiles: int, tile: int = TILE) -> Tuple[int, int]:
+    """Smallest upscale >= 1 (else the least downscale), ties -> smallest area."""
+    cands = _supported_canvases(max_tiles, tile)
+    scales = [min(ch / h, cw / w) for ch, cw in cands]
+    ups = [s for s in scales if s >= 1]
+    sel = min(ups) if ups else max(scales)
+    best = [c for c, s in zip(cands, scales) if s == sel]
+    return min(best, key=lambda c: c[0] * c[1])
+
+
+def load_image(src) -> "object":
+    """PIL image from a PIL image, raw bytes, a data: URL or a local path."""
+    from PIL import Image
+
+    if hasattr(src, "convert"):
+        return src.convert("RGB")
+    if isinstance(src, (bytes, bytearray)):
+        return Image.open(io.BytesIO(src)).convert("RGB")
+    s = str(src)
+    if s.startswith("data:"):
+        return Image.open(io.BytesIO(base64.b64decode(s.split(",", 1)[1]))).convert("RGB")
+    if s.startswith(("http://", "https://")):
+        import httpx
+        r = httpx.get(s, timeout=30.0, follow_redirects=True)
+        r.raise_for_status()
+        return Image.open(io.BytesIO(r.content)).convert("RGB")
+    return Image.open(s).convert("RGB")
+
+
+def preprocess(image, max_tiles: int = 16,
+               tile: int = TILE) -> Tuple[torch.Tensor, Tuple[int, int]]:
+    """-> (pixel_values [tiles, 3, tile, tile] fp32, (tiles_h, tiles_w))."""
+    from PIL import Image
+
+    TILE = tile                                                     # noqa: N806
+    img = load_image(image)
+    w, h = img.size
+    ch, cw = best_fit_canvas(h, w, max_tiles, tile)
+    s = min(ch / h, cw / w)
+    nh, nw = min(ch, max(1, math.floor(h * s))), min(cw, max(1, math.floor(w * s)))
+    canvas = np.zeros((ch, cw, 3), np.float32)
+    canvas[:nh, :nw] = np.asarray(img.resize((nw, nh), Image.BILINEAR), np.float32)
+    th, tw = ch // TILE, cw // TILE
+
+    def norm(a):
+        return (a / 255.0 - 0.5) / 0.5
+
+    tiles = [norm(canvas[y * TILE:(y + 1) * TILE, x * TILE:(x + 1) * TILE])
+             for y in range(th) for x in range(tw)]
+    if th * tw > 1:
+        tiles.append(norm(np.asarray(img.resize((TILE, TILE), Image.BILINEAR), np.float32)))
+    pv = torch.from_numpy(np.stack(tiles)).permute(0, 3, 1, 2).contiguous()
+    return pv, (th, tw)
+
+
+def expand_image_prompt(aspect: Tuple[int, int], tokens_per_tile: int) -> str:
+    """The placeholder text one image expands to (Llama-4 prompt format)."""
+    th, tw = aspect
+    s = "<|image_start|>"
+    if th * tw > 1:
+        for _ in range(th):
+            for x in range(tw):
+                s += "<|patch|>" * tokens_per_tile
+                if x < tw - 1:
+                    s += "<|tile_x_separator|>"
+            s += "<|tile_y_separator|>"
+    s += "<|image|>" + "<|patch|>" * tokens_per_tile + "<|image_end|>"
+    return s
+
+
+# ----------------------------------------------------------------------------- encoder
+def _linear(x: torch.Tensor, w: torch.Tensor, b: Optional[torch.Tensor] = None) -> torch.Tensor:
+    shp = x.shape
+    y = gemm.linear(x.reshape(-1, shp[-1]), w, b)
+    return y.reshape(*shp[:-1], w.shape[0])
+
+
+def _ln(x: torch.Tensor, w: torch.Tensor, b: torch.Tensor, eps: float = 1e-5) -> torch.Tensor:
+    from ..ops.norm import layer_norm
+    shp = x.shape
+    return layer_norm(x.reshape(-1, shp[-1]).contiguous(), w, b, eps).reshape(shp)
+
+
+def pixel_shuffle(x: torch.Tensor, ratio: float) -> torch.Tensor:
+    B, N, C = x.shape
+    side = int(math.isqrt(N))
+    x = x.view(B, side, side, C)
+    x = x.view(B, side, int(side * ratio), int(C / ratio)).permute(0, 2, 1, 3).contiguous()
+    x = x.view(B, int(side * ratio), int(side * ratio), int(C / ratio ** 2))
+    return x.permute(0, 2, 1, 3).contiguous().view(B, -1, x.shape[-1])
+
+
+class _P(nn.Module):
+    """Parameter holder with HF-compatible names."""
+
+    def __init__(self, **shapes):
+        super().__init__()
+        for k, (shape, dtype, device) in shapes.items():
+            self.register_parameter(k, nn.Parameter(torch.empty(shape, dtype=dtype, device=device),
+                                                    requires_grad=False))
+
+
+class Llama4VisionTower(nn.Module):
+    def __init__(self, vcfg: dict, text_hidden: int, dtype=torch.bfloat16, device=None):
+        super().__init__()
+        self.cfg = vcfg
+        D = vcfg["hidden_size"]
+        I = vcfg["intermediate_size"]
+        self.heads = vcfg["num_attention_heads"]
+        self.hd = D // self.heads
+        self.image_size = vcfg.get("image_size", TILE)
+        self.patch = vcfg.get("patch_size", PATCH)
+        self.side = self.image_size // self.patch
+        self.ratio = vcfg.get("pixel_shuffle_ratio", 0.5)
+        self.tokens_per_tile = int(self.side * self.side * self.ratio ** 2)
+        pin = vcfg["projector_input_dim"]
+        pout = vcfg["projector_output_dim"]
+        ch = vcfg.get("num_channels", 3)
+        kw = dict(dtype=dtype, device=device)
+        t = lambda *s: (s, dtype, device)                               # noqa: E731
+        self.patch_embedding = nn.Module()
+        self.patch_embedding.linear = _P(weight=t(D, ch * self.patch * self.patch))
+        self.class_embedding = nn.Parameter(torch.empty(D, **kw), requires_grad=False)
+        self.positional_embedding_vlm = nn.Parameter(
+            torch.empty(self.side * self.side + 1, D, **kw), requires_grad=False)
+        self.layernorm_pre = _P(weight=t(D), bias=t(D))
+        self.layernorm_post = _P(weight=t(D), bias=t(D))
+        layers = nn.ModuleList()
+        for _ in range(vcfg["num_hidden_layers"]):
+            L = nn.Module()
+            L.input_layernorm = _P(weight=t(D), bias=t(D))
+            L.post_attention_layernorm = _P(weight=t(D), bias=t(D))
+            L.self_attn = nn.Module()
+            for n in ("q_proj", "k_proj", "v_proj", "o_proj"):
+                setattr(L.self_attn, n, _P(weight=t(D, D), bias=t(D)))
+            L.mlp = nn.Module()
+            L.mlp.fc1 = _P(weight=t(I, D), bias=t(I))
+            L.mlp.fc2 = _P(weight=t(D, I), bias=t(D))
+            layers.append(L)
+        self.model = nn.Module()
+        self.model.layers = layers
+        self.vision_adapter = nn.Module()
+        self.vision_adapter.mlp = nn.Module()
+        self.vision_adapter.mlp.fc1 = _P(weight=t(pin, I))      # in: D / ratio^2 == I
+        self.vision_adapter.mlp.fc2 = _P(weight=t(pout, pout))
+        self.projector = _P(weight=t(text_hidden, vcfg["vision_output_dim"]))
+        theta = vcfg.get("rope_theta") or (vcfg.get("rope_parameters") or {}).get("rope_theta",
+                                                                                  10000.0)
+        self.register_buffer("freqs", self._freqs(float(theta), device), persistent=False)
+
+    def _freqs(self, theta: float, device) -> torch.Tensor:
+        """cos/sin [patches + 1, hd/2] of the 2-D rotary (x then y frequencies, class = 0)."""
+        idx = self.side
+        img_idx = torch.arange(idx * idx).reshape(-1, 1)
+        img_idx = torch.cat([img_idx, img_idx[:1]], 0)
+        img_idx[-1, -1] = -2
+        fx, fy = img_idx % idx, img_idx // idx
+        fd = self.hd // 2
+        rf = 1.0 / (theta ** (torch.arange(0, fd, 2)[: fd // 2].float() / fd))
+        ax = ((fx + 1)[..., None] * rf[None, None, :]).repeat_interleave(2, dim=-1)
+        ay = ((fy + 1)[..., None] * rf[None, None, :]).repeat_interleave(2, dim=-1)
+        ang = torch.cat([ax, ay], -1).float()[..., ::2]
+        ang = ang.masked_fill(img_idx.reshape(-1, 1, 1) < 0, 0).reshape(idx * idx + 1, -1)
+        return torch.stack([torch.cos(ang), torch.sin(ang)], -1).to(device)   # [N, hd/2, 2]
+
+    def _rope(self, x: torch.Tensor) -> torch.Tensor:
+        """x [B, N, H, hd]: interleaved pairs rotated by the per-patch angles."""
+        cs = self.freqs.to(x.device)
+        c, s = cs[..., 0][None, :, None, :], cs[..., 1][None, :, None, :]
+        xf = x.float().reshape(*x.shape[:-1], -1, 2)
+        a, b = xf[..., 0], xf[..., 1]
+        out = torch.stack([a * c - b * s, a * s + b * c], -1).flatten(-2)
+        return out.to(x.dtype)
+
+    @torch.no_grad()
+    def forward(self, pixel_values: torch.Tensor) -> torch.Tensor:
+        """pixel_values [tiles, 3, S, S] -> projected embeddings [tiles * tokens_per_tile, H]."""
+        dt = self.class_embedding.dtype
+        x = pixel_values.to(self.class_embedding.device, dt)
+        T = x.shape[0]
+        p = F.unfold(x, kernel_size=self.patch, stride=self.patch).transpose(1, 2)   # [T, N, C*p*p]
+        h = _linear(p.contiguous(), self.patch_embedding.linear.weight)
+        h = torch.cat([h, self.class_embedding.expand(T, 1, -1)], 1)
+        h = h + self.positional_embedding_vlm
+        h = _ln(h, self.layernorm_pre.weight, self.layernorm_pre.bias)
+        N = h.shape[1]
+        for L in self.model.layers:
+            r = h
+            y = _ln(h, L.input_layernorm.weight, L.input_layernorm.bias)
+            a = L.self_attn
+            q = self._rope(_linear(y, a.q_proj.weight, a.q_proj.bias).view(T, N, self.heads, self.hd))
+            k = self._rope(_linear(y, a.k_proj.weight, a.k_proj.bias).view(T, N, self.heads, self.hd))
+            v = _linear(y, a.v_proj.weight, a.v_proj.bias).view(T, N, self.heads, self.hd)
+            o = F.scaled_dot_product_attention(q.transpose(1, 2), k.transpose(1, 2),
+                                               v.transpose(1, 2), is_causal=False)
+            o = o.transpose(1, 2).reshape(T, N, -1)
+            h = r + _linear(o, a.o_proj.weight, a.o_proj.bias)
+            y = _ln(h, L.post_attention_layernorm.weight, L.post_attention_layernorm.bias)
+            y = F.gelu(_linear(y, L.mlp.fc1.weight, L.mlp.fc1.bias))
+            h = h + _linear(y, L.mlp.fc2.weight, L.mlp.fc2.bias)
+        h = _ln(h, self.layernorm_post.weight, self.layernorm_post.bias)[:, :-1]
+        h = pixel_shuffle(h, self.ratio)
+        m = self.vision_adapter.mlp
+        h = F.gelu(_linear(F.gelu(_linear(h, m.fc1.weight)), m.fc2.weight))
+        out = _linear(h.reshape(-1, h.shape[-1]), self.projector.weight)
+        return out
+
+    def load_weight(self, name: str, tensor: torch.Tensor) -> bool:
+        """HF names 'vision_model.<x>' / 'multi_modal_projector.linear_1.weight'."""
+        if name.startswith("multi_modal_projector.linear_1."):
+            tgt = self.projector.weight
+        else:
+            rest = name[len("vision_model."):]
+            tgt = self
+            try:
+                for part in rest.split("."):
+                    tgt = getattr(tgt, part) if not part.isdigit() else tgt[int(part)]
+            except (AttributeError, IndexError):
+                return False
+        if not isinstance(tgt, torch.Tensor) or tgt.shape != tensor.shape:
+            raise ValueError(f"vision weight {name}: shape {tuple(tensor.shape)} vs "
+                             f"{tuple(getattr(tgt, 'shape', ()))}")
+        tgt.data.copy_(tensor.to(tgt.dtype))
+        return True
+
+
+def image_positions(token_ids: Sequence[int], image_token_id: int) -> List[int]:
+    return [i for i, t in enumerate(token_ids) if t == image_token_id]

@@ -19,6 +19,7 @@ instead gives each rank E/tp whole experts (the reference's EP on Gaudi 3,
 from __future__ import annotations
 
 import math
+import os
 from typing import Iterable, List, Optional, Tuple
 
 import torch
@@ -271,7 +272,8 @@ class Llama4MoE(nn.Module):
 class Llama4ForCausalLM(LlamaForCausalLM):
     def __init__(self, cfg: ModelConfig, dtype=torch.bfloat16, device=None):
         cfg.extra.setdefault("rope_interleaved", True)
-        moe_layers = set(cfg.extra.get("moe_layers") or range(cfg.num_hidden_layers))
+        ml = cfg.extra.get("moe_layers")
+        moe_layers = set(range(cfg.num_hidden_layers) if ml is None else ml)
         inter_mlp = cfg.extra.get("intermediate_size_mlp") or cfg.intermediate_size
 
         def make(i):
@@ -282,6 +284,18 @@ class Llama4ForCausalLM(LlamaForCausalLM):
             return layer
 
         super().__init__(cfg, dtype, device, layer_factory=make)
+        self.vision = None
+        vc = cfg.extra.get("vision_config")
+        if vc and os.environ.get("EIA_DISABLE_VISION", "0") != "1" and self.first:
+            from .llama4_vision import Llama4VisionTower
+            self.vision = Llama4VisionTower(vc, cfg.hidden_size, dtype, device)
+            self.image_token_id = int(cfg.extra.get("image_token_id", 200092))
+
+    def encode_images(self, pixel_values: torch.Tensor) -> torch.Tensor:
+        """[tiles, 3, S, S] -> [tiles * 144, hidden] placeholder embeddings."""
+        if self.vision is None:
+            raise ValueError("this model was loaded without its vision tower")
+        return self.vision(pixel_values)
 
     def map_weight_name(self, name: str):
         n = name
@@ -301,11 +315,24 @@ class Llama4ForCausalLM(LlamaForCausalLM):
                 if f".{part}." in n:
                     return n.replace(part, "gate_up_proj"), sid
             return n, None
-        return super().map_weight_name(name if not name.startswith("language_model.")
-                                       else name[len("language_model."):])
+        # dense (non-MoE) layers: feed_forward.{gate,up,down}_proj -> mlp.gate_up_proj / down_proj
+        return super().map_weight_name(n)
 
     def load_weights(self, weights: Iterable[Tuple[str, torch.Tensor]]) -> List[str]:
         strip = lambda n: n[len("language_model."):] if n.startswith("language_model.") else n
-        return _load_with_stacked_experts(
-            self, weights, lambda rest: super(Llama4ForCausalLM, self).load_weights(
+        vis_loaded: List[str] = []
+
+        def text_only(ws):
+            for n, t in ws:
+                m = n[len("model."):] if n.startswith("model.vision_model") or \
+                    n.startswith("model.multi_modal_projector") else n
+                if m.startswith(("vision_model.", "multi_modal_projector.")):
+                    if self.vision is not None and self.vision.load_weight(m, t):
+                        vis_loaded.append(n)
+                    continue
+                yield n, t
+
+        loaded = _load_with_stacked_experts(
+            self, text_only(weights), lambda rest: super(Llama4ForCausalLM, self).load_weights(
                 (strip(n), t) for n, t in rest))
+        return list(loaded) + vis_loaded

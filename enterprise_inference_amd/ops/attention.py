@@ -142,6 +142,9 @@ class AttentionMetadata:
     prefill_work: Optional[torch.Tensor] = None          # [n_work*2] int32
     prefill_n_work: int = 0
     causal: bool = True
+    # multimodal: batch rows whose token embedding is replaced (image placeholders)
+    mm_rows: Optional[torch.Tensor] = None               # [n] int64
+    mm_embeds: Optional[torch.Tensor] = None             # [n, hidden]
 
     @property
     def num_tokens(self) -> int:

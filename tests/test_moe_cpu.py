@@ -54,13 +54,14 @@ def test_qwen3_moe_matches_transformers():
     _check(eng, hf, [[5, 6, 7, 8] * 12, [9, 10, 11]])
 
 
-def test_llama4_text_matches_transformers():
+@pytest.mark.parametrize("moe_layers", [[0, 1, 2, 3], [1, 3]])   # [1, 3]: Maverick-style dense/MoE
+def test_llama4_text_matches_transformers(moe_layers):
     import transformers
     d = tiny_config("Llama4ForCausalLM", num_local_experts=4, num_experts_per_tok=1,
                     intermediate_size=128, intermediate_size_mlp=256, head_dim=32,
                     num_hidden_layers=4, attention_chunk_size=32, no_rope_layers=[1, 1, 1, 0],
                     use_qk_norm=True, attn_temperature_tuning=True, floor_scale=8, attn_scale=0.1,
-                    interleave_moe_layer_step=1, moe_layers=[0, 1, 2, 3])
+                    interleave_moe_layer_step=1, moe_layers=moe_layers)
     hcfg = {k: v for k, v in d.items() if k not in ("architectures",)}
     hc = transformers.Llama4TextConfig(**hcfg)
     hc._attn_implementation = "eager"
