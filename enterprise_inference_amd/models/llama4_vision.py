@@ -16,8 +16,8 @@ tokens of its prompt expansion (``expand_image_prompt``), written over the token
 of those positions in the prefill batch (models/llama.py forward, ``md.mm_rows``).
 
 Linear layers run through ops.gemm (hipBLASLt / skinny HIP kernels), LayerNorm through the HIP
-layer-norm kernel, attention through PyTorch SDPA (577 non-causal tokens per tile, once per
-image -- not a hot path).
+layer-norm kernel, attention as batched GEMMs (hipBLASLt) around an fp32 softmax (577
+non-causal tokens per tile, once per image -- not a hot path).
 """
 
 from __future__ import annotations
@@ -241,8 +241,9 @@ class Llama4VisionTower(nn.Module):
             q = self._rope(_linear(y, a.q_proj.weight, a.q_proj.bias).view(T, N, self.heads, self.hd))
             k = self._rope(_linear(y, a.k_proj.weight, a.k_proj.bias).view(T, N, self.heads, self.hd))
             v = _linear(y, a.v_proj.weight, a.v_proj.bias).view(T, N, self.heads, self.hd)
-            o = F.scaled_dot_product_attention(q.transpose(1, 2), k.transpose(1, 2),
-                                               v.transpose(1, 2), is_causal=False)
+            # non-causal MHA as two batched library GEMMs around an fp32 softmax
+            s = torch.matmul(q.transpose(1, 2), k.permute(0, 2, 3, 1)).float() * self.hd ** -0.5
+            o = torch.matmul(torch.softmax(s, -1).to(v.dtype), v.transpose(1, 2))
             o = o.transpose(1, 2).reshape(T, N, -1)
             h = r + _linear(o, a.o_proj.weight, a.o_proj.bias)
             y = _ln(h, L.post_attention_layernorm.weight, L.post_attention_layernorm.bias)

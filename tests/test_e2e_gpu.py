@@ -144,3 +144,55 @@ def test_kv_swap_under_pressure_matches_fp32_oracle():
     toks = [o.outputs[0].token_ids for o in outs]
     stats = check_greedy(hf, prompts, toks, tol=0.08)
     assert stats["argmax_agreement"] > 0.8, stats
+
+
+def test_llama4_vision_gpu_matches_fp32_oracle():
+    """Llama-4 on the GPU path (interleaved RoPE + NoPE layer, qk L2-norm, chunked local
+    attention, a top-1 MoE layer with a shared expert) with an image: the vision tower runs
+    bf16 on the GPU, its embeddings replace the placeholder tokens inside a chunked prefill,
+    and every generated token is teacher-forced against HF Llama4ForConditionalGeneration fp32
+    on the CPU with the same weights and pixels."""
+    import transformers
+
+    IMG = 1000
+    text = tiny_config("Llama4ForCausalLM", **SHAPE, num_local_experts=4,
+                       num_experts_per_tok=1, intermediate_size_mlp=2048,
+                       attention_chunk_size=256, no_rope_layers=[1, 0], use_qk_norm=True,
+                       interleave_moe_layer_step=1, moe_layers=[1])
+    text = {k: v for k, v in text.items() if k != "architectures"}
+    vision = {"hidden_size": 256, "intermediate_size": 1024, "num_hidden_layers": 2,
+              "num_attention_heads": 4, "image_size": 112, "patch_size": 14,
+              "pixel_shuffle_ratio": 0.5, "projector_input_dim": 512,
+              "projector_output_dim": 512, "vision_output_dim": 512, "rope_theta": 10000.0,
+              "num_channels": 3}
+    d = {"architectures": ["Llama4ForConditionalGeneration"], "text_config": text,
+         "vision_config": vision, "image_token_index": IMG}
+    vc = transformers.Llama4VisionConfig(**{k: v for k, v in vision.items() if k != "rope_theta"},
+                                         rope_parameters={"rope_theta": 10000.0,
+                                                          "rope_type": "default"})
+    hc = transformers.Llama4Config(text_config=transformers.Llama4TextConfig(**text).to_dict(),
+                                   vision_config=vc.to_dict(), image_token_index=IMG)
+    for c in (hc, hc.text_config, hc.vision_config):
+        c._attn_implementation = "eager"
+    torch.manual_seed(0)
+    hf = transformers.Llama4ForConditionalGeneration(hc).float().eval()
+    eng = _engine(d)
+    model = eng.executor.runner.model
+    assert model.vision is not None and model.vision.tokens_per_tile == 16
+    model.load_weights(hf.state_dict().items())
+    gen = torch.Generator().manual_seed(2)
+    pv = torch.randn(3, 3, 112, 112, generator=gen)                   # 3 tiles -> 48 tokens
+    prompt = (torch.randint(3, 990, (230,), generator=gen).tolist() + [IMG] * 48 +
+              torch.randint(3, 990, (120,), generator=gen).tolist())    # spans prefill chunks
+    n = 16
+    out = eng.generate(prompt_token_ids=[prompt],
+                       params=SamplingParams(max_tokens=n, temperature=0, ignore_eos=True),
+                       multi_modal_data=[{"image": [pv]}])[0]
+    toks = out.outputs[0].token_ids
+    assert len(toks) == n
+    with torch.no_grad():
+        lg = hf(input_ids=torch.tensor([prompt + toks]), pixel_values=pv).logits[0].float()
+    rows = lg[len(prompt) - 1:len(prompt) - 1 + n]
+    margins = rows.max(-1).values - rows.gather(1, torch.tensor(toks)[:, None])[:, 0]
+    assert float(margins.max()) < 0.08, margins
+    assert float((margins == 0).float().mean()) > 0.8, margins
