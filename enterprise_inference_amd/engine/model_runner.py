@@ -13,6 +13,7 @@ from __future__ import annotations
 
 import logging
 import math
+import os
 import time
 from typing import Dict, List, Optional, Tuple
 
@@ -141,6 +142,10 @@ class ModelRunner:
             _native.kernels()         # fail loudly now if the HIP library is unusable
             from ..ops import gemm as _gemm_ops
             _gemm_ops.enable_prefill_tuning()
+        elif "OMP_NUM_THREADS" not in os.environ and hasattr(os, "sched_getaffinity"):
+            # CPU serving pod: one intra-op thread per core of the pod's cpuset (the NRI
+            # balloon), not per core of the host
+            torch.set_num_threads(max(1, len(os.sched_getaffinity(0))))
         torch.manual_seed(cfg.seed)
         t0 = time.time()
         self.model = build_model(cfg, device)

@@ -175,3 +175,19 @@ def test_fast_sse_chunks_match_pydantic(text, finish, stop):
             finish_reason=finish, stop_reason=stop)]))
     got = sv.fast_chat_chunk(sv.chat_chunk_head("chatcmpl-1", 7, "m/x"), 0, text, finish, stop)
     assert body(got) == body(ref)
+
+
+def test_openapi_spec_in_sync():
+    """docs/api-spec.yaml is generated from the apps (scripts/gen_openapi.py) and current."""
+    import os
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    r = subprocess.run([sys.executable, os.path.join(root, "scripts", "gen_openapi.py"), "--check"],
+                       capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr
+    import yaml
+    with open(os.path.join(root, "docs", "api-spec.yaml")) as f:
+        doc = yaml.safe_load(f)
+    for p in ("/v1/chat/completions", "/v1/completions", "/v1/embeddings", "/embed", "/rerank"):
+        assert p in doc["paths"], p
