@@ -154,6 +154,12 @@ def core_main(fd: int) -> int:
     from .llm_engine import LLMEngine
 
     try:
+        if cfg.device == "cuda":
+            import torch
+
+            from ..utils.numa import pin_to_device
+            if torch.cuda.device_count() > 0:   # step loop + staging next to GPU 0's socket
+                pin_to_device(0)
         engine = LLMEngine(cfg)
         engine.delta_outputs = True
     except BaseException as e:   # noqa: BLE001 - reported to the API process, then exit

@@ -133,6 +133,8 @@ def _spawned_worker(cfg: EngineConfig, rank: int, world: int, port: int, ring_na
     os.environ.pop("TORCHELASTIC_USE_AGENT_STORE", None)
     if cfg.device == "cuda" and torch.cuda.device_count() > 0:
         torch.cuda.set_device(rank)
+        from ..utils.numa import pin_to_device
+        pin_to_device(rank)
     pstate.init_distributed(cfg.parallel.tensor_parallel_size,
                             enable_expert_parallel=cfg.parallel.enable_expert_parallel,
                             pp_size=cfg.parallel.pipeline_parallel_size)

@@ -176,3 +176,47 @@ def test_kv_cache_dtype_fp8_warns_and_keeps_model_dtype(tmp_path, caplog):
         cfg = engine_config_from_args(args)
     assert "kv-cache-dtype fp8_e4m3 is not supported" in caplog.text
     assert cfg.cache.cache_dtype == cfg.dtype
+
+
+# ------------------------------------------------------------------ NUMA placement (§5.10)
+def _fake_pci(tmp_path, bdf, cpulist, node):
+    d = tmp_path / bdf
+    d.mkdir(parents=True)
+    (d / "local_cpulist").write_text(cpulist + "\n")
+    (d / "numa_node").write_text(f"{node}\n")
+    return str(tmp_path)
+
+
+def test_numa_cpulist_and_bdf():
+    from enterprise_inference_amd.utils import numa
+    assert numa.parse_cpulist("0-3,8,10-11\n") == {0, 1, 2, 3, 8, 10, 11}
+    assert numa.parse_cpulist("") == set()
+    assert numa.pci_bdf(0, 0x1b, 0) == "0000:1b:00.0"
+
+
+def test_numa_pin_to_device(tmp_path, monkeypatch):
+    """The process is restricted to the GPU-local cores it is allowed to use; a TP worker
+    that inherited another socket's mask still finds its own cores through EIA_ALLOWED_CPUS."""
+    from enterprise_inference_amd.utils import numa
+    allowed = sorted(os.sched_getaffinity(0))
+    if len(allowed) < 2:
+        pytest.skip("needs >= 2 usable cores")
+    half = allowed[: len(allowed) // 2]
+    sysfs = _fake_pci(tmp_path, "0000:1b:00.0", ",".join(map(str, half)), 0)
+    monkeypatch.delenv("EIA_ALLOWED_CPUS", raising=False)
+    monkeypatch.delenv("EIA_NUMA_PIN", raising=False)
+    try:
+        got = numa.pin_to_device(0, sysfs=sysfs, bdf="0000:1b:00.0")
+        assert got == set(half) and os.sched_getaffinity(0) == set(half)
+        assert numa.parse_cpulist(os.environ["EIA_ALLOWED_CPUS"]) == set(allowed)
+        # a second GPU on the other "socket": pinned from the recorded original set
+        other = allowed[len(allowed) // 2:]
+        sysfs2 = _fake_pci(tmp_path / "b", "0000:9c:00.0", ",".join(map(str, other)), 1)
+        assert numa.pin_to_device(1, sysfs=sysfs2, bdf="0000:9c:00.0") == set(other)
+        assert numa.numa_node("0000:9c:00.0", sysfs2) == 1
+        # no NUMA info / disabled: placement unchanged
+        assert numa.pin_to_device(0, sysfs=str(tmp_path / "none"), bdf="0000:00:00.0") == set()
+        monkeypatch.setenv("EIA_NUMA_PIN", "0")
+        assert numa.pin_to_device(0, sysfs=sysfs, bdf="0000:1b:00.0") == set()
+    finally:
+        os.sched_setaffinity(0, set(allowed))
