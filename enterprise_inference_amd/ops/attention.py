@@ -105,7 +105,11 @@ def decode_partitions(batch: int, num_kv_heads: int, num_heads: int, max_len: in
     Fitted to scripts/bench_attn.py on MI355X (graph-timed, Llama-8B heads): short contexts
     never split (the partial write + merge costs more than it hides); grids of >= 4 workgroups
     per CU do not split; small grids split up to one workgroup per CU (B=16: P=2, B=1: P=8);
-    mid-size grids split 2x, or 4x past 2048 tokens (B=65, ctx 4096: 213 us vs 249 us)."""
+    mid-size grids split 2x, or 4x past 2048 tokens (B=65, ctx 4096: 213 us vs 249 us).
+    EIA_DECODE_P forces a partition count (tuning / A-B runs)."""
+    forced = int(os.environ.get("EIA_DECODE_P", "0"))
+    if forced > 0:
+        return max(1, min(forced, max_parts, max(1, max_len // 64)))
     if max_len <= 512:
         return 1
     g = num_heads // num_kv_heads

@@ -14,7 +14,7 @@ if [[ -n "$KEXPR" ]]; then
   tail -2 gpurun_out/ab_tests.log
 fi
 for v in ${VALS:-0 1 0 1}; do
-  env "$VAR=$v" timeout -k 10 600 python bench.py --mode engine --steps "$STEPS" --warmup 1 \
+  env "$VAR=$v" timeout -k 10 600 python bench.py --mode ${MODE:-engine} --steps "$STEPS" --warmup 1 \
     > "gpurun_out/ab_${VAR}_$v.log" 2>&1 || { tail -20 "gpurun_out/ab_${VAR}_$v.log"; exit 1; }
   echo "$VAR=$v $(grep -o '"value": [0-9.]*\|"tpot_p50_ms": [0-9.]*' gpurun_out/ab_${VAR}_$v.log | tr '\n' ' ')"
 done
