@@ -20,6 +20,8 @@ and the caller's all-reduce sums the ranks' partial outputs.
 
 from __future__ import annotations
 
+import os
+
 from typing import Optional, Tuple
 
 import torch
@@ -30,6 +32,11 @@ from ._dispatch import check, lib, ptr, stream, use_hip
 
 SCORING = {"softmax": 0, "sigmoid": 1}
 
+
+# grouped skinny GEMM configurations (csrc/kernels/gemm_skinny.hip cfg bits: NT-1 | (WAVES/2-1)<<1);
+# -1 = the shape rule below.  Overrides for tuning runs.
+UP_CFG = int(os.environ.get("EIA_MOE_UP_CFG", "-1"))
+DOWN_CFG = int(os.environ.get("EIA_MOE_DOWN_CFG", "-1"))
 
 def topk_route(logits: torch.Tensor, k: int, renormalize: bool = True,
                scoring: str = "softmax") -> Tuple[torch.Tensor, torch.Tensor]:
@@ -124,12 +131,14 @@ def _fused_moe_grouped(x, w13, w2, topk_w, topk_ids, e_lo, e_hi, mfma: bool = Fa
               "moe_grouped_gemm_down")
     else:
         mt = max(1, min(8, -(-int(1.5 * n / El + 1) // 16)))
+        up_cfg = UP_CFG if UP_CFG >= 0 else (3 if (I % 64 == 0) else 1)
+        down_cfg = DOWN_CFG if DOWN_CFG >= 0 else (2 if H % 128 == 0 else 0)
         check(lib().eia_moe_gemm(ptr(x), x.stride(0), ptr(w13), w13.stride(1), None, ptr(h1),
                                  h1.stride(0), I2, H, El, ptr(offs), ptr(row_idx), mt, 2,
-                                 3 if (I % 64 == 0) else 1, st), "moe_gemm_gate_up")
+                                 up_cfg, st), "moe_gemm_gate_up")
         check(lib().eia_moe_gemm(ptr(h1), h1.stride(0), ptr(w2), w2.stride(1), None, ptr(h2),
                                  h2.stride(0), H, I, El, ptr(offs), None, mt, 0,
-                                 2 if H % 128 == 0 else 0, st), "moe_gemm_down")
+                                 down_cfg, st), "moe_gemm_down")
     out = torch.empty(T, H, dtype=x.dtype, device=dev)
     check(lib().eia_moe_combine(ptr(h2), h2.stride(0), ptr(topk_w), ptr(inv), T, k, H, ptr(out),
                                 out.stride(0), st), "moe_combine")
