@@ -135,6 +135,34 @@ def _run_op(engine, op: str):
     raise ValueError(f"unknown engine op {op!r}")
 
 
+# Intake coalescing: an idle engine that receives a request keeps reading for as long as more
+# requests keep arriving (gaps <= INTAKE_GAP_S, INTAKE_MAX_S in all) before it schedules, so a
+# burst of concurrent requests (N users starting together) is prefilled in one step instead of
+# a small step for the first few arrivals that everyone else then queues behind.  A lone
+# request pays at most one INTAKE_GAP_S.  EIA_INTAKE_GAP_MS=0 disables it.
+INTAKE_GAP_S = float(os.environ.get("EIA_INTAKE_GAP_MS", "2")) / 1000.0
+INTAKE_MAX_S = float(os.environ.get("EIA_INTAKE_MAX_MS", "20")) / 1000.0
+
+
+def intake(reader, busy: bool, gap: float = None, cap: float = None) -> list:
+    """Frames for this loop iteration: whatever is pending (blocking up to 0.5 s when idle),
+    extended by the coalescing window above when the idle engine just received requests."""
+    gap = INTAKE_GAP_S if gap is None else gap
+    cap = INTAKE_MAX_S if cap is None else cap
+    msgs = reader.poll(0 if busy else 0.5)
+    if busy or gap <= 0 or not any(m[0] == "add" for m in msgs):
+        return msgs
+    t_end = time.time() + cap
+    while True:
+        left = t_end - time.time()
+        if left <= 0:
+            return msgs
+        more = reader.poll(min(gap, left))
+        if not more:
+            return msgs
+        msgs += more
+
+
 def core_main(fd: int) -> int:
     """Entry point of the engine-core process (``python -m ...core_proc --fd N``)."""
     import signal
@@ -176,7 +204,7 @@ def core_main(fd: int) -> int:
     try:
         while True:
             busy = engine.has_unfinished_requests()
-            for msg in reader.poll(0 if busy else 0.5):
+            for msg in intake(reader, busy):
                 k = msg[0]
                 if k == "add":
                     _, rid, prompt, params, ids, arrival, prio = msg[:7]

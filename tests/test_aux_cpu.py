@@ -220,3 +220,47 @@ def test_numa_pin_to_device(tmp_path, monkeypatch):
         assert numa.pin_to_device(0, sysfs=sysfs, bdf="0000:1b:00.0") == set()
     finally:
         os.sched_setaffinity(0, set(allowed))
+
+
+# ------------------------------------------------------------------ engine-core intake window
+class _FakeReader:
+    """poll(timeout) -> the frames due by then (arrival offsets in seconds from creation)."""
+
+    def __init__(self, arrivals):
+        self.t0 = time.time()
+        self.pending = sorted(arrivals, key=lambda a: a[0])
+
+    def poll(self, timeout):
+        deadline = time.time() + (timeout or 0)
+        while True:
+            now = time.time() - self.t0
+            due = [f for t, f in self.pending if t <= now]
+            if due:
+                self.pending = [(t, f) for t, f in self.pending if t > now]
+                return due
+            if time.time() >= deadline:
+                return []
+            time.sleep(0.0002)
+
+
+def test_intake_coalesces_a_burst():
+    from enterprise_inference_amd.engine.core_proc import intake
+    burst = [(0.001 * i, ("add", i)) for i in range(10)]          # 10 requests, 1 ms apart
+    late = [(0.2, ("add", 99))]
+    r = _FakeReader(burst + late)
+    got = intake(r, busy=False, gap=0.004, cap=0.05)
+    assert [m[1] for m in got] == list(range(10))                  # the whole burst, not the late one
+    # busy engine: no waiting, whatever is pending now
+    r2 = _FakeReader([(0.0, ("add", 1)), (0.003, ("add", 2))])
+    time.sleep(0.001)
+    assert [m[1] for m in intake(r2, busy=True, gap=0.004, cap=0.05)] == [1]
+    # disabled / non-add frames: returned as they come
+    r3 = _FakeReader([(0.0, ("add", 1)), (0.002, ("add", 2))])
+    assert [m[1] for m in intake(r3, busy=False, gap=0.0, cap=0.05)] == [1]
+    r4 = _FakeReader([(0.0, ("abort", 7)), (0.002, ("add", 2))])
+    assert [m[1] for m in intake(r4, busy=False, gap=0.004, cap=0.05)] == [7]
+    # the window is capped
+    steady = [(0.001 * i, ("add", i)) for i in range(200)]
+    t0 = time.time()
+    got = intake(_FakeReader(steady), busy=False, gap=0.004, cap=0.02)
+    assert time.time() - t0 < 0.1 and 5 <= len(got) < 200
