@@ -180,8 +180,9 @@ gemm_skinny_kernel(const bf16_t* __restrict__ X, long ldx, const bf16_t* __restr
 
   constexpr int XV = MT * 16 * (KC / 8);                // 16-B vectors per X chunk
   constexpr int XTHREADS = LOADER ? 64 : WAVES * 64;    // threads that stage X
-  constexpr int XPT = XV / XTHREADS;                    // per staging thread
-  static_assert(XV % XTHREADS == 0, "X chunk split");
+  constexpr int XPT = (XV + XTHREADS - 1) / XTHREADS;   // per staging thread
+  // 7-wave workgroups (cfg bit 8) do not divide the chunk evenly: the last vectors are guarded
+  constexpr bool XGUARD = XV % XTHREADS != 0;
   const int xt = LOADER ? lane : (int)threadIdx.x;      // index among the staging threads
   const bool is_loader = LOADER && wave == WAVES;
 
@@ -203,6 +204,7 @@ gemm_skinny_kernel(const bf16_t* __restrict__ X, long ldx, const bf16_t* __restr
       for (int j = 0; j < XPT; ++j) {
         const int v = xt + j * XTHREADS;
         const int col = (v % (KC / 8)) * 8;
+        if (XGUARD && j == XPT - 1 && v >= XV) continue;
         xr[j] = *reinterpret_cast<const bf16x8*>(X + (long)xrows[j] * ldx + k0 + rc(c) * KC + col);
       }
     };
@@ -210,6 +212,7 @@ gemm_skinny_kernel(const bf16_t* __restrict__ X, long ldx, const bf16_t* __restr
 #pragma unroll
       for (int j = 0; j < XPT; ++j) {
         const int v = xt + j * XTHREADS;
+        if (XGUARD && j == XPT - 1 && v >= XV) continue;
         const int row = v / (KC / 8), col = (v % (KC / 8)) * 8;
         *reinterpret_cast<bf16x8*>(xs + (buf * MT * 16 + row) * XLD + col) = xr[j];
       }
@@ -649,6 +652,12 @@ int launch_mt(int cfg, const bf16_t* X, long ldx, const bf16_t* W, long ldw, con
       }
 #undef EIA_GL
     }
+    if (cfg & 256) {   // 7 waves x (gate, up) pairs: 1792 pairs = 256 workgroups (70B gate_up)
+      if constexpr (MT <= 4) {
+        if (cfg == 256 + 17) EIA_CFG(2, 7, 2, 128);
+      }
+      return EIA_BAD_SHAPE;
+    }
     switch (cfg) {
       case 0: EIA_CFG(1, 2, 2, 256);
       case 1: EIA_CFG(2, 2, 2, 256);
@@ -736,9 +745,12 @@ int dispatch_mt(int mt, int cfg, const bf16_t* x, long ldx, const bf16_t* w, lon
 constexpr unsigned long long kSpillCfg[9] = {0x0ull, 0x8000a00ull, 0x8000a20ull, 0x8800ba0ull, 0x80000000e800bb0ull, 0x44400000ec00fb2ull, 0x80000000ee80fb2ull, 0x88000000fe80ff3ull, 0xccc00000ff80ffbull};
 
 int check_shape(int N, int K, int sk, int mode, int cfg) {
-  const int nt = (cfg & 1) ? 2 : 1, waves = (cfg & 2) ? 4 : 2;
+  const int nt = (cfg & 1) ? 2 : 1, waves = (cfg & 256) ? 7 : (cfg & 2) ? 4 : 2;
   const int kc = (cfg & 16) ? 128 : 256;
-  if (sk < 1 || cfg < 0 || (cfg & ~(16 | 32 | 64 | 128)) > 11 || K % (sk * kc) != 0) return EIA_BAD_SHAPE;
+  if (sk < 1 || cfg < 0 || (cfg & ~(16 | 32 | 64 | 128 | 256)) > 11 || K % (sk * kc) != 0) return EIA_BAD_SHAPE;
+  // 7-wave form: SwiGLU pairs only, register-staged, plain layout
+  if ((cfg & 256) && (mode != MODE_SWIGLU || !(cfg & 1) || (cfg & (2 | 8 | 32 | 64 | 128))))
+    return EIA_BAD_SHAPE;
   if ((cfg & 32) && !((cfg & 16) && (cfg & 2))) return EIA_BAD_SHAPE;   // loader: 4 waves, KC 128
   if ((cfg & 128) && ((cfg & 32) || !(cfg & 16) || !(cfg & 2) || ((cfg >> 2) & 3) == 3))
     return EIA_BAD_SHAPE;                                                // LDS-DMA ring
@@ -760,12 +772,17 @@ int check_shape(int N, int K, int sk, int mode, int cfg) {
 // bits 2-3 -> W pipeline stages - 2 (2..4), bit 4 -> 128-deep K chunks (else 256),
 // bit 5 -> extra X-loader wave (with bits 1 and 4), bit 6 -> tile-packed W (ldw must be K),
 // bit 7 -> LDS-DMA ring kernel (with bits 1 and 4; bits 2-3 = ring depth - 2)
+// bit 8 -> 7 waves of (gate, up) pairs per workgroup (SwiGLU only; cfg 273 = + bits 0 and 4):
+//          70B's 1792 pairs are exactly 256 workgroups, where 4-wave workgroups leave 448
 EIA_API int eia_gemm_skinny(const void* X, long ldx, const void* W, long ldw, const void* bias,
                             void* out, long ldo, int M, int N, int K, int sk, int mode, int cfg,
                             hipStream_t st) {
   if (M < 1 || M > 128) return EIA_BAD_SHAPE;
   if (int rc = check_shape(N, K, sk, mode, cfg)) return rc;
-  if (!(cfg & 128) && ((kSpillCfg[(M + 15) / 16] >> (cfg & 63)) & 1ull)) return EIA_BAD_SHAPE;
+  if (!(cfg & 384) && ((kSpillCfg[(M + 15) / 16] >> (cfg & 63)) & 1ull)) return EIA_BAD_SHAPE;
+  // 7-wave form: cfg 273 only (KC 128, 2 stages), spill-free up to 4 row tiles (M <= 64); at
+  // 7 waves two share a SIMD, so the register budget is 256
+  if ((cfg & 256) && (cfg != 256 + 17 || M > 64)) return EIA_BAD_SHAPE;
   if ((cfg & 128) && (long)(((cfg >> 2) & 3) + 2) * ((M + 15) / 16 + 4 * ((cfg & 1) + 1)) * 4096 >
                          160 * 1024)
     return EIA_BAD_SHAPE;

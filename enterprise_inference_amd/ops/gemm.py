@@ -36,8 +36,9 @@ MODE_BF16, MODE_SPLIT, MODE_SWIGLU = 0, 1, 2
 # kernel configs: bit0 -> 2 W tiles (32 rows) per wave, bit1 -> 4 waves per workgroup
 # bit0 NT=2, bit1 WAVES=4, bits2-3 pipeline stages-2, bit4 128-deep K chunks (else 256)
 # bit5: an extra wave stages X into LDS (4 compute waves, KC 128): 50, 51, 54, 55, 58, 59
+# bit8: 7 waves of (gate, up) pairs per workgroup, SwiGLU only: 273 (KC 128, 2 stages, M <= 64)
 CFGS = tuple(range(12)) + tuple(range(16, 28)) + (50, 51, 54, 55, 58, 59) + \
-    (146, 147, 150, 151, 154, 155)
+    (146, 147, 150, 151, 154, 155) + (273,)
 # bit6: tile-packed weights (pack_weight) for the layouts the decode tables use
 PACKED_CFGS = tuple(64 + c for c in (1, 2, 3, 7, 17, 18, 19, 22, 23, 51, 55, 146, 147, 150, 151, 154, 155))
 # bit7: LDS-DMA ring kernel, 4 waves, KC 128: 146 | (NT-1) | (depth-2) << 2 (+64 packed)
@@ -53,8 +54,12 @@ def cfg_kc(cfg: int) -> int:
     return 128 if cfg & 16 else KC
 
 
+def cfg_waves(cfg: int) -> int:
+    return 7 if cfg & 256 else (4 if cfg & 2 else 2)
+
+
 def cfg_rows(cfg: int) -> int:
-    return (2 if cfg & 1 else 1) * (4 if cfg & 2 else 2) * 16
+    return (2 if cfg & 1 else 1) * cfg_waves(cfg) * 16
 
 
 def m_bucket(M: int) -> int:
@@ -85,13 +90,16 @@ SPILL_CFGS = {1: (9, 11, 27), 2: (5, 9, 11, 27), 3: (5, 7, 8, 9, 11, 23, 27), 4:
 def valid(N: int, K: int, swiglu: bool, cfg: int, sk: int, M: Optional[int] = None) -> bool:
     if K % (sk * cfg_kc(cfg)):
         return False
+    if cfg & 256:   # 7-wave SwiGLU form: cfg 273 only, spill-free up to M = 64
+        return (swiglu and cfg == 273 and sk == 1 and (M is None or M <= 64)
+                and (N // 2) % (7 * 16) == 0)
     if cfg & 128:
         if M is not None and glds_lds_bytes(cfg, M) > 160 * 1024:
             return False
     elif M is not None and (cfg & 63) in SPILL_CFGS.get(m_bucket(M), ()):
         return False
     if swiglu:
-        return sk == 1 and (cfg & 1) == 1 and (N // 2) % ((4 if cfg & 2 else 2) * 16) == 0
+        return sk == 1 and (cfg & 1) == 1 and (N // 2) % (cfg_waves(cfg) * 16) == 0
     return N % cfg_rows(cfg) == 0
 
 

@@ -80,9 +80,23 @@ def test_swiglu_gemm(M, I, K):
     w = (torch.randn(2 * I, K, device=DEV) * K ** -0.5).to(BF)
     y = _ref(x, w)
     ref = F.silu(y[:, :I]) * y[:, I:]
-    for cfg in (1, 3, 5, 7, 9, 11):
+    for cfg in (1, 3, 5, 7, 9, 11, 273):
         if gemm.valid(2 * I, K, True, cfg, 1, M=M):
             _check(gemm.swiglu_gemm(x, w, cfg=cfg), ref, f"swiglu M={M} I={I} cfg={cfg}")
+
+
+@pytest.mark.parametrize("M", [1, 35, 64])
+def test_swiglu_7wave_70b(M):
+    """7-wave SwiGLU form (cfg 273) at Llama-70B's single-GPU gate_up shape (1792 pairs = 256
+    workgroups, 448 threads each; the X chunk does not divide evenly over the threads) vs fp32."""
+    from enterprise_inference_amd.ops import gemm
+    torch.manual_seed(M)
+    I, K = 28672, 8192
+    x = torch.randn(M, K, device=DEV, dtype=BF)
+    w = (torch.randn(2 * I, K, device=DEV) * K ** -0.5).to(BF)
+    assert gemm.valid(2 * I, K, True, 273, 1, M=M) and not gemm.valid(2 * I, K, True, 273, 1, M=65)
+    y = _ref(x, w)
+    _check(gemm.swiglu_gemm(x, w, cfg=273), F.silu(y[:, :I]) * y[:, I:], f"7-wave M={M}")
 
 
 @pytest.mark.parametrize("M,H,sk", [(1, 4096, 4), (65, 4096, 4), (128, 8192, 4), (65, 4096, 2),
