@@ -23,3 +23,19 @@ def test_packed_cfgs_share_base_validity():
     for c in gemm.PACKED_CFGS:
         assert c & 64 and (c & 63) in gemm.CFGS
         assert gemm.cfg_rows(c) == gemm.cfg_rows(c & 63) and gemm.cfg_kc(c) == gemm.cfg_kc(c & 63)
+
+
+def test_seven_wave_swiglu_cfg_rules():
+    """cfg 273 (7 pair-waves per workgroup) is a SwiGLU-only, spill-bounded form: valid for
+    70B's 1792 pairs (256 workgroups) up to M = 64, never for plain or split-K GEMMs."""
+    from enterprise_inference_amd.ops import gemm
+    assert gemm.cfg_waves(273) == 7 and gemm.cfg_rows(273) == 7 * 2 * 16
+    assert 273 in gemm.CFGS
+    assert gemm.valid(2 * 28672, 8192, True, 273, 1, M=35)
+    assert gemm.valid(2 * 28672, 8192, True, 273, 1, M=64)
+    assert not gemm.valid(2 * 28672, 8192, True, 273, 1, M=65)        # spills past 4 row tiles
+    assert not gemm.valid(2 * 28672, 8192, False, 273, 1, M=35)       # SwiGLU only
+    assert not gemm.valid(2 * 28672, 8192, True, 273, 2, M=35)        # no split-K
+    assert not gemm.valid(2 * 11008, 4096, True, 273, 1, M=35)        # 688 pairs: not 7 | pairs
+    assert not gemm.valid(2 * 28672, 8192, True, 257, 1, M=35)        # only the KC-128 form
+    assert (28672 // 16) // 7 == 256
