@@ -194,6 +194,8 @@ def core_main(fd: int) -> int:
         logger.exception("engine init failed")
         sock.sendall(encode_frame(("dead", f"engine init failed: {e!r}")))
         return 1
+    from ..utils.gc_tuning import tune_after_startup
+    tune_after_startup()
     sock.sendall(encode_frame(("ready", {"num_blocks": engine.num_blocks, "pid": os.getpid()})))
     log_requests = bool(opts.get("log_requests"))
     fault = opts.get("fault", "")

@@ -252,6 +252,8 @@ def main(argv=None) -> int:
                 pstats.Stats(prof, stream=f).sort_stats("tottime").print_stats(60)
 
         app.router.on_shutdown.append(_dump_profile)
+    from ...utils.gc_tuning import tune_after_startup
+    tune_after_startup()
     try:
         uvicorn.run(app, host=args.host, port=args.port, log_level=args.uvicorn_log_level,
                     timeout_keep_alive=5)

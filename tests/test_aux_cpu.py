@@ -264,3 +264,18 @@ def test_intake_coalesces_a_burst():
     t0 = time.time()
     got = intake(_FakeReader(steady), busy=False, gap=0.004, cap=0.02)
     assert time.time() - t0 < 0.1 and 5 <= len(got) < 200
+
+
+def test_gc_tuning(monkeypatch):
+    import gc
+    from enterprise_inference_amd.utils.gc_tuning import tune_after_startup
+    old = gc.get_threshold()
+    try:
+        monkeypatch.setenv("EIA_GC_FREEZE", "0")
+        assert tune_after_startup() is False
+        monkeypatch.setenv("EIA_GC_FREEZE", "1")
+        assert tune_after_startup(gen0=12345) is True
+        assert gc.get_freeze_count() > 0 and gc.get_threshold()[0] >= 12345
+    finally:
+        gc.unfreeze()
+        gc.set_threshold(*old)
