@@ -139,6 +139,8 @@ def _spawned_worker(cfg: EngineConfig, rank: int, world: int, port: int, ring_na
                             enable_expert_parallel=cfg.parallel.enable_expert_parallel,
                             pp_size=cfg.parallel.pipeline_parallel_size)
     runner = setup_runner(cfg)
+    from ..utils.gc_tuning import tune_after_startup
+    tune_after_startup()
     worker_loop(runner, ring_name, driver_pid)
     pstate.destroy_distributed()
 

@@ -291,7 +291,10 @@ def main(argv=None) -> int:
     if hasattr(emb.model, "pooling"):
         emb.model.pooling = args.pooling
     emb.warmup(int(os.environ.get("MAX_WARMUP_SEQUENCE_LENGTH", 512)))
-    uvicorn.run(build_tei_app(emb), host=args.hostname, port=args.port)
+    app = build_tei_app(emb)
+    from ...utils.gc_tuning import tune_after_startup
+    tune_after_startup()
+    uvicorn.run(app, host=args.hostname, port=args.port)
     return 0
 
 
