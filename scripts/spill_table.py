@@ -41,7 +41,7 @@ def main() -> int:
     for mt, nt, waves, st, grouped, kc, loader, _packed in spill:
         # grouped (MoE) variants are not table-selected; the 7-wave SwiGLU form (cfg bit 8) has
         # its own fixed M bound in check_shape / gemm.valid
-        if grouped or waves == 7:
+        if grouped or waves in (5, 7):
             continue
         cfg = (nt - 1) | ((waves // 2 - 1) << 1) | ((st - 2) << 2) | (16 if kc == 128 else 0) \
             | (32 if loader else 0)
