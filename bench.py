@@ -64,6 +64,9 @@ def parse():
     ap.add_argument("--mode", default="endpoint", choices=["endpoint", "engine"])
     ap.add_argument("--model", default="meta-llama/Llama-3.1-8B-Instruct")
     ap.add_argument("--tp", type=int, default=1)
+    ap.add_argument("--co-deploy", action="store_true",
+                    help="config #5: replicas alternate --model / --co-model on disjoint GPUs")
+    ap.add_argument("--co-model", default="mistralai/Mistral-7B-Instruct-v0.3")
     ap.add_argument("--users", type=int, default=65)
     ap.add_argument("--input-len", type=int, default=128)
     ap.add_argument("--output-len", type=int, default=128)
@@ -190,7 +193,8 @@ def _visible_devices(first: int, n: int) -> str:
     return ",".join(ids[first:first + n])
 
 
-def start_server(args, local_rank: int, port: int, log_path: str) -> subprocess.Popen:
+def start_server(args, first_gpu: int, port: int, log_path: str,
+                 model: str = None) -> subprocess.Popen:
     # the server runs its own process groups: drop every torchrun / elastic-agent variable
     # (TORCHELASTIC_USE_AGENT_STORE would make its rank 0 wait for an agent-hosted store)
     env = {k: v for k, v in os.environ.items()
@@ -198,11 +202,12 @@ def start_server(args, local_rank: int, port: int, log_path: str) -> subprocess.
                         "GROUP_WORLD_SIZE", "ROLE_RANK", "ROLE_NAME", "ROLE_WORLD_SIZE",
                         "MASTER_ADDR", "MASTER_PORT")
            and not k.startswith("TORCHELASTIC_")}
-    env["HIP_VISIBLE_DEVICES"] = _visible_devices(local_rank, args.tp)
+    env["HIP_VISIBLE_DEVICES"] = _visible_devices(first_gpu, args.tp)
     env.pop("CUDA_VISIBLE_DEVICES", None)
     env["PYTHONPATH"] = ROOT + os.pathsep + env.get("PYTHONPATH", "")
+    env["EIA_BENCH_ENDPOINTS"] = "1"          # /eia/sync + /eia/stats (opt-in, bench only)
     cmd = [sys.executable, "-m", "enterprise_inference_amd.entrypoints.openai.api_server",
-           "--model", args.model, "--port", str(port), "--host", "127.0.0.1",
+           "--model", model or args.model, "--port", str(port), "--host", "127.0.0.1",
            "--load-format", "dummy", "--tensor-parallel-size", str(args.tp),
            "--max-model-len", str(args.input_len + args.output_len + 64),
            "--max-num-seqs", str(args.max_num_seqs),
@@ -251,7 +256,153 @@ def stop_server(proc: subprocess.Popen) -> None:
             proc.wait(timeout=30)
 
 
+class Replica:
+    """One serving replica: an OpenAI server on GPUs [first_gpu, first_gpu + tp) plus the
+    client processes holding its --users concurrent streams."""
+
+    def __init__(self, args, idx: int, first_gpu: int, model: str, logdir: str):
+        self.args, self.idx, self.model = args, idx, model
+        self.log_path = os.path.join(logdir, f"bench_server_rank{first_gpu}.log")
+        port = _free_port()
+        self.base = f"http://127.0.0.1:{port}"
+        self.proc = start_server(args, first_gpu, port, self.log_path, model)
+        self.pool = ClientPool(max(1, min(args.client_procs, args.users)),
+                               self.base + "/v1/completions", model, args.output_len,
+                               args.temperature)
+        from enterprise_inference_amd.models.catalog import resolve_name
+        from enterprise_inference_amd.models.loader import resolve_model_config
+        self.vocab = min(resolve_model_config(resolve_name(model)).vocab_size, 128000)
+        self.rng = random.Random(args.seed * 7919 + first_gpu)
+        self.res = []
+        self.init_s = 0.0
+
+    def wait(self) -> None:
+        t0 = time.time()
+        wait_healthy(self.base, self.proc, self.args.startup_timeout, self.log_path)
+        self.init_s = time.time() - t0
+
+    def one_round(self):
+        a = self.args
+        prompts = [[self.rng.randrange(1000, self.vocab) for _ in range(a.input_len)]
+                   for _ in range(a.users)]
+        return self.pool.round(prompts)
+
+    def rounds(self, n: int, timed: bool) -> None:
+        for s in range(n):
+            t0 = time.time()
+            res = self.one_round()
+            if not timed:
+                bad = [r for r in res if not r[0]]
+                if bad:
+                    raise RuntimeError(f"warmup request failed: {bad[0][4]}")
+                continue
+            self.res.append(res)
+            if self.args.verbose:
+                ok_tt = sorted(r[1] for r in res if r[0]) or [0.0]
+                print(f"[replica {self.idx}] round {s}: {sum(r[3] for r in res)} tok in "
+                      f"{time.time() - t0:.3f}s, ttft p50 {1000 * statistics.median(ok_tt):.1f} ms",
+                      file=sys.stderr)
+
+    def sync(self) -> None:
+        _http("POST", self.base + "/eia/sync")
+
+    def stats(self) -> dict:
+        return json.loads(_http("GET", self.base + "/eia/stats")[1])
+
+    def summary(self, elapsed: float, stats0: dict, stats1: dict) -> dict:
+        tot, ttft, tpot, e2e, failed = 0, [], [], [], []
+        for res in self.res:
+            for ok, tt, ee, n, err in res:
+                if not ok or n != self.args.output_len:
+                    failed.append(err or f"got {n} tokens, expected {self.args.output_len}")
+                    continue
+                tot += n
+                ttft.append(tt)
+                e2e.append(ee)
+                if n > 1:
+                    tpot.append((ee - tt) / (n - 1))
+        return {"tokens": tot, "elapsed": elapsed, "ttft": ttft, "tpot": tpot, "e2e": e2e,
+                "failed": failed, "init_s": self.init_s, "model": self.model,
+                "engine_gen_tokens": stats1["num_generation_tokens"]
+                - stats0["num_generation_tokens"],
+                "engine_steps": stats1["num_steps"] - stats0["num_steps"],
+                "engine_busy_s": stats1["step_time_s"] - stats0["step_time_s"],
+                "num_blocks": stats1["num_blocks"]}
+
+    def close(self) -> None:
+        self.pool.close()
+        stop_server(self.proc)
+
+
+def _parallel(fns) -> None:
+    """Run callables on threads, re-raise the first failure."""
+    import threading
+
+    errs = []
+
+    def wrap(f):
+        try:
+            f()
+        except BaseException as e:  # noqa: BLE001 - re-raised below
+            errs.append(e)
+
+    ts = [threading.Thread(target=wrap, args=(f,)) for f in fns]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join()
+    if errs:
+        raise errs[0]
+
+
+def replica_models(args, n: int):
+    """Model of each replica: all --model, or alternating --model / --co-model (config #5,
+    multi-model co-deploy on disjoint GPU sets)."""
+    if not args.co_deploy:
+        return [args.model] * n
+    return [args.model if i % 2 == 0 else args.co_model for i in range(n)]
+
+
 def run_endpoint(args) -> int:
+    """Two launch forms, same measurement:
+    * torchrun (RANK/WORLD_SIZE set, the driver's multi-GPU form): every --tp-th rank leads
+      one replica on its GPU slice, a gloo barrier brackets the timed rounds, max over ranks;
+    * fan-out (no torchrun env): this process starts --gpus / --tp replicas itself, each
+      pinned to its HIP_VISIBLE_DEVICES slice, and runs their rounds concurrently."""
+    if "WORLD_SIZE" in os.environ:
+        return _run_endpoint_torchrun(args)
+    n_rep = max(1, args.gpus // args.tp)
+    if args.gpus % args.tp:
+        raise SystemExit(f"--gpus {args.gpus} is not a multiple of --tp {args.tp}")
+    logdir = os.environ.get("EIA_BENCH_LOGDIR") or os.path.join(ROOT, "gpurun_out")
+    os.makedirs(logdir, exist_ok=True)
+    models = replica_models(args, n_rep)
+    reps = []
+    try:
+        # children first: nothing in this process ever initialises the GPU
+        for i in range(n_rep):
+            reps.append(Replica(args, i, i * args.tp, models[i], logdir))
+        _parallel([r.wait for r in reps])
+        _parallel([(lambda r=r: r.rounds(args.warmup, False)) for r in reps])
+        stats0 = [r.stats() for r in reps]
+        _parallel([r.sync for r in reps])
+        t0 = time.time()
+        _parallel([(lambda r=r: r.rounds(args.steps, True)) for r in reps])
+        _parallel([r.sync for r in reps])
+        elapsed = time.time() - t0
+        stats1 = [r.stats() for r in reps]
+        summ = [r.summary(elapsed, s0, s1) for r, s0, s1 in zip(reps, stats0, stats1)]
+        _report(args, summ, n_gpus=n_rep * args.tp, via="endpoint")
+        failed = [f for g in summ for f in g["failed"]]
+        if failed:
+            print(f"error: {len(failed)} failed requests, e.g. {failed[0]}", file=sys.stderr)
+        return 1 if failed else 0
+    finally:
+        for r in reps:
+            r.close()
+
+
+def _run_endpoint_torchrun(args) -> int:
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -260,91 +411,50 @@ def run_endpoint(args) -> int:
     leader = local % args.tp == 0
     logdir = os.environ.get("EIA_BENCH_LOGDIR") or os.path.join(ROOT, "gpurun_out")
     os.makedirs(logdir, exist_ok=True)
-    log_path = os.path.join(logdir, f"bench_server_rank{rank}.log")
-    proc = pool = None
-    base = None
-    # children first: nothing in this process ever initialises the GPU
+    rep = None
     if leader:
-        port = _free_port()
-        base = f"http://127.0.0.1:{port}"
-        proc = start_server(args, local, port, log_path)
-        pool = ClientPool(max(1, min(args.client_procs, args.users)), base + "/v1/completions",
-                          args.model, args.output_len, args.temperature)
+        model = replica_models(args, world // args.tp)[rank // args.tp]
+        rep = Replica(args, rank // args.tp, local, model, logdir)
     dist = None
     if world > 1:
         import torch.distributed as dist
         dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
-        t_init = time.time()
-        if leader:
-            wait_healthy(base, proc, args.startup_timeout, log_path)
-        init_s = time.time() - t_init
-        from enterprise_inference_amd.models.catalog import resolve_name
-        from enterprise_inference_amd.models.loader import resolve_model_config
-        vocab = min(resolve_model_config(resolve_name(args.model)).vocab_size, 128000)
-        rng = random.Random(args.seed * 7919 + rank)
-
-        def one_round():
-            prompts = [[rng.randrange(1000, vocab) for _ in range(args.input_len)]
-                       for _ in range(args.users)]
-            t0 = time.time()
-            res = pool.round(prompts)
-            return res, time.time() - t0
+        if rep:
+            rep.wait()
+            rep.rounds(args.warmup, False)
+        stats0 = rep.stats() if rep else None
 
         def barrier():
-            if leader:
-                _http("POST", base + "/eia/sync")
+            if rep:
+                rep.sync()
             if dist is not None:
                 dist.barrier()
 
-        for _ in range(args.warmup if leader else 0):
-            res, _dt = one_round()
-            bad = [r for r in res if not r[0]]
-            if bad:
-                raise RuntimeError(f"warmup request failed: {bad[0][4]}")
-        stats0 = json.loads(_http("GET", base + "/eia/stats")[1]) if leader else None
         barrier()
         t0 = time.time()
-        tot_tokens, ttft, tpot, e2e, failed = 0, [], [], [], []
-        for s in range(args.steps if leader else 0):
-            res, dt = one_round()
-            for ok, tt, ee, n, err in res:
-                if not ok or n != args.output_len:
-                    failed.append(err or f"got {n} tokens, expected {args.output_len}")
-                    continue
-                tot_tokens += n
-                ttft.append(tt)
-                e2e.append(ee)
-                if n > 1:
-                    tpot.append((ee - tt) / (n - 1))
-            if args.verbose:
-                ok_tt = sorted(r[1] for r in res if r[0])
-                print(f"[rank {rank}] round {s}: {sum(r[3] for r in res)} tok in {dt:.3f}s, "
-                      f"ttft p50 {1000 * statistics.median(ok_tt):.1f} ms", file=sys.stderr)
-        if leader:
-            _http("POST", base + "/eia/sync")
+        if rep:
+            rep.rounds(args.steps, True)
+            rep.sync()
         elapsed = time.time() - t0
         if dist is not None:
             dist.barrier()
-        local_stats = None
-        if leader:
-            stats1 = json.loads(_http("GET", base + "/eia/stats")[1])
-            busy = stats1["step_time_s"] - stats0["step_time_s"]
-            local_stats = {"tokens": tot_tokens, "elapsed": elapsed, "ttft": ttft, "tpot": tpot,
-                           "e2e": e2e, "failed": failed, "init_s": init_s,
-                           "engine_gen_tokens": stats1["num_generation_tokens"]
-                           - stats0["num_generation_tokens"],
-                           "engine_steps": stats1["num_steps"] - stats0["num_steps"],
-                           "engine_busy_s": busy, "num_blocks": stats1["num_blocks"]}
-        _report(args, dist, local_stats, rank, world, via="endpoint")
+        local_stats = rep.summary(elapsed, stats0, rep.stats()) if rep else None
+        if dist is not None:
+            gathered = [None] * world
+            dist.all_gather_object(gathered, local_stats)
+        else:
+            gathered = [local_stats]
+        summ = [g for g in gathered if g is not None]
+        if rank == 0:
+            _report(args, summ, n_gpus=world, via="endpoint")
+        failed = [f for g in summ for f in g["failed"]]
         if failed and rank == 0:
             print(f"error: {len(failed)} failed requests, e.g. {failed[0]}", file=sys.stderr)
         return 1 if failed else 0
     finally:
-        if pool is not None:
-            pool.close()
-        if proc is not None:
-            stop_server(proc)
+        if rep is not None:
+            rep.close()
         if dist is not None:
             dist.destroy_process_group()
 
@@ -392,7 +502,7 @@ def run_engine(args) -> int:
         ring = [None, None]
         dist.broadcast_object_list(ring, src=pstate.tp_ranks()[0], group=pstate.tp_cpu_group())
         worker_loop(runner, ring[0], ring[1])
-        _report(args, dist, None, rank, world, via="engine")
+        _gather_report(args, dist, None, rank, world, via="engine")
         return 0
     from enterprise_inference_amd.engine.executor import TPExecutor, UniprocExecutor
     from enterprise_inference_amd.engine.llm_engine import LLMEngine
@@ -458,46 +568,51 @@ def run_engine(args) -> int:
     if tp > 1:
         ex.shutdown()
     local_stats = {"tokens": tot_tokens, "elapsed": elapsed, "ttft": all_ttft, "tpot": all_tpot,
-                   "e2e": [], "failed": [], "init_s": init_s, "num_blocks": engine.num_blocks}
-    _report(args, dist, local_stats, rank, world, via="engine")
+                   "e2e": [], "failed": [], "init_s": init_s, "num_blocks": engine.num_blocks,
+                   "model": model_id}
+    _gather_report(args, dist, local_stats, rank, world, via="engine")
     return 0
 
 
 # --------------------------------------------------------------------------- report
 
-def _report(args, dist, local_stats, rank, world, via: str):
-    from enterprise_inference_amd.models.catalog import resolve_name
-
+def _gather_report(args, dist, local_stats, rank, world, via: str):
     if dist is not None and dist.is_initialized():
         gathered = [None] * world
         dist.all_gather_object(gathered, local_stats)
     else:
         gathered = [local_stats]
-    if rank != 0:
-        return
-    reps = [g for g in gathered if g is not None]
+    if rank == 0:
+        _report(args, [g for g in gathered if g is not None], world, via)
+
+
+def _report(args, reps, n_gpus: int, via: str):
+    """ONE JSON line for the whole job: ``reps`` holds one summary per serving replica."""
+    from enterprise_inference_amd.models.catalog import resolve_name
+
     tokens = sum(g["tokens"] for g in reps)
     elapsed = max(g["elapsed"] for g in reps)
     ttft = sorted(x for g in reps for x in g["ttft"])
     tpot = sorted(x for g in reps for x in g["tpot"])
     e2e = sorted(x for g in reps for x in g["e2e"])
     value = tokens / elapsed
-    model_id = resolve_name(args.model)
-    base = BASELINE_TOK_S.get((model_id, args.input_len, args.output_len))
-    n_replicas = max(1, world // args.tp)
-    vs = None
-    if base is not None:
-        # published number is per replica (e.g. 1 Gaudi 3 for 8B); node = replicas x that
-        vs = value / (base[0] * n_replicas)
+    n_replicas = len(reps)
+    models = [resolve_name(g.get("model") or args.model) for g in reps]
+    # published numbers are per replica (e.g. 1 Gaudi 3 for 8B): node = sum over replicas;
+    # null when any replica's model has no published number (Mistral-7B, Mixtral)
+    bases = [BASELINE_TOK_S.get((m, args.input_len, args.output_len)) for m in models]
+    vs = value / sum(b[0] for b in bases) if all(b is not None for b in bases) else None
+    base = bases[0]
 
     def ms(v, nd=2):
         return None if v is None else round(1000 * v, nd)
 
+    uniq = list(dict.fromkeys(models))
     out = {
         "metric": METRIC,
         "value": round(value, 2),
         "unit": "output tokens/s",
-        "n_gpus": world,
+        "n_gpus": n_gpus,
         "steps": args.steps,
         "warmup": args.warmup,
         "ms_per_step": round(1000.0 * elapsed / max(1, args.steps), 2),
@@ -506,7 +621,7 @@ def _report(args, dist, local_stats, rank, world, via: str):
         "vs_baseline": None if vs is None else round(vs, 3),
         "dtype": "bf16",
         "data": "synthetic",
-        "config": {"model": model_id, "global_batch": args.users * n_replicas,
+        "config": {"model": "+".join(uniq), "global_batch": args.users * n_replicas,
                    "seq_len": args.input_len + args.output_len,
                    "input_len": args.input_len, "output_len": args.output_len,
                    "users_per_replica": args.users,
@@ -524,13 +639,16 @@ def _report(args, dist, local_stats, rank, world, via: str):
         "failed_requests": sum(len(g["failed"]) for g in reps),
         "init_s": round(max(g["init_s"] for g in reps), 1),
     }
+    if len(uniq) > 1:
+        out["per_model"] = {m: {"tok_s": round(sum(g["tokens"] for g, mm in zip(reps, models)
+                                                  if mm == m) / elapsed, 2),
+                                "replicas": models.count(m)} for m in uniq}
     if via == "endpoint":
         busy = max(g["engine_busy_s"] for g in reps)
-        gen = sum(g["engine_gen_tokens"] for g in reps)
-        # engine-level throughput over the engine core's busy time (no HTTP / client), and the
-        # fraction of the timed window the engine loop was stepping
-        out["engine_tok_s"] = round(gen / max(busy, 1e-9) * 1.0, 2) if n_replicas == 1 else \
-            round(sum(g["engine_gen_tokens"] / max(g["engine_busy_s"], 1e-9) for g in reps), 2)
+        # engine-level throughput over each engine core's busy time (no HTTP / client), and
+        # the fraction of the timed window the engine loops were stepping
+        out["engine_tok_s"] = round(sum(g["engine_gen_tokens"] / max(g["engine_busy_s"], 1e-9)
+                                        for g in reps), 2)
         out["engine_busy_frac"] = round(busy / elapsed, 3)
         out["engine_steps"] = sum(g["engine_steps"] for g in reps)
     print(json.dumps(out), flush=True)

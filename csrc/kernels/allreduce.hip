@@ -362,3 +362,16 @@ EIA_API int eia_ar_read_err(const void* sig, int* err) {
   return (int)hipMemcpy(err, &static_cast<const ArSignal*>(sig)->err, sizeof(int),
                         hipMemcpyDeviceToHost);
 }
+
+// Stream-ordered read of the error flag into (pinned) host memory: the serving loop polls it
+// every few steps without a device-wide synchronisation (parallel/custom_allreduce.py).
+EIA_API int eia_ar_read_err_async(const void* sig, int* host_dst, hipStream_t st) {
+  return (int)hipMemcpyAsync(host_dst, &static_cast<const ArSignal*>(sig)->err, sizeof(int),
+                             hipMemcpyDeviceToHost, st);
+}
+
+// Fault injection for the failure-detection tests: sets (or clears) this rank's flag.
+EIA_API int eia_ar_set_err(void* sig, int v) {
+  uint32_t u = (uint32_t)v;
+  return (int)hipMemcpy(&static_cast<ArSignal*>(sig)->err, &u, sizeof(u), hipMemcpyHostToDevice);
+}

@@ -65,6 +65,8 @@ _SIGNATURES = {
     "eia_ar_signal_bytes": [],
     "eia_ar_run": [P, P, I, I, P, P, L, L, I, I, S],
     "eia_ar_read_err": [P, P],
+    "eia_ar_read_err_async": [P, P, S],
+    "eia_ar_set_err": [P, I],
     "eia_ar_add_rmsnorm": [P, P, I, I, P, P, P, P, F, I, I, L, I, I, S],
 }
 

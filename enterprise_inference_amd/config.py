@@ -233,6 +233,19 @@ class ParallelConfig:
     # Custom xGMI all-reduce (one-shot/two-shot) below this many bytes; RCCL above.
     custom_allreduce_max_bytes: int = 16 * 1024 * 1024
     disable_custom_all_reduce: bool = False
+    # torch.distributed backend: "auto" = nccl (RCCL over xGMI) on GPUs, gloo on the CPU path
+    dist_backend: str = "auto"
+    # every TP rank on the driver's GPU (EIA_TP_SHARE_DEVICE=1): a rehearsal mode that runs
+    # the TP engine's per-rank shapes on a one-GPU box.  RCCL refuses two ranks on one device,
+    # so it implies gloo with host-staged collectives, eager decode and no custom all-reduce.
+    share_device: bool = False
+
+    def __post_init__(self) -> None:
+        if os.environ.get("EIA_TP_SHARE_DEVICE", "0") not in ("0", "", "false"):
+            self.share_device = True
+        if self.share_device:
+            self.dist_backend = "gloo"
+            self.disable_custom_all_reduce = True
 
     @property
     def world_size(self) -> int:
@@ -261,6 +274,22 @@ class EngineConfig:
     engine_iteration_timeout_s: float = 120.0  # VLLM_ENGINE_ITERATION_TIMEOUT_S
 
     def __post_init__(self) -> None:
+        if self.device == "cuda" and self.dtype != torch.bfloat16:
+            # the HIP kernels (attention, norms, GEMM epilogues, sampling) are bf16-only; any
+            # other dtype would silently run the PyTorch reference ops on the GPU
+            raise ValueError(f"dtype {self.dtype} is not supported on the MI355X path; serve "
+                             "with --dtype bfloat16 (auto)")
+        if self.load_format not in ("auto", "safetensors", "pt", "dummy"):
+            raise ValueError(f"unknown load_format {self.load_format!r}")
+        if self.device == "cuda" and self.parallel.world_size > 1 and (
+                self.parallel.share_device or self.parallel.dist_backend == "gloo"):
+            self.enforce_eager = True        # host-staged gloo collectives cannot be captured
+        if self.device == "cuda" and self.parallel.tensor_parallel_size > 1 and \
+                self.parallel.enable_expert_parallel and \
+                os.environ.get("EIA_EP_DISPATCH", "allreduce") == "all_to_all":
+            # the all-to-all dispatch reads its split sizes back to the host every layer: not
+            # capturable in a HIP graph, so decode runs eagerly (docs/runtime-flags.md)
+            self.enforce_eager = True
         if self.cache.cache_dtype is None:
             self.cache.cache_dtype = self.dtype
         if self.scheduler.max_model_len > self.model.max_position_embeddings and \

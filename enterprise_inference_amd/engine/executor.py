@@ -46,15 +46,28 @@ def _agree_num_blocks(nb: int) -> int:
 
 def setup_runner(cfg: EngineConfig) -> ModelRunner:
     runner = ModelRunner(cfg)
+    ar = None
     if cfg.parallel.tensor_parallel_size > 1 and runner.is_gpu and \
             not cfg.parallel.disable_custom_all_reduce:
         from ..parallel.custom_allreduce import init_custom_allreduce
-        init_custom_allreduce(cfg.parallel.custom_allreduce_max_bytes)
+        ar = init_custom_allreduce(cfg.parallel.custom_allreduce_max_bytes)
     nb = runner.determine_num_blocks()
     nb = _agree_num_blocks(nb)
     runner.allocate_kv_cache(nb)
     runner.capture_graphs()
+    runner.ar_poller = None
+    if ar is not None:
+        from ..parallel.custom_allreduce import ErrorPoller
+        runner.ar_poller = ErrorPoller(ar)
+        runner.ar_poller.check_now()     # profiling run + graph warm-up used the kernel
     return runner
+
+
+def _init_dist(cfg: EngineConfig) -> None:
+    pstate.init_distributed(cfg.parallel.tensor_parallel_size,
+                            backend=cfg.parallel.dist_backend,
+                            enable_expert_parallel=cfg.parallel.enable_expert_parallel,
+                            pp_size=cfg.parallel.pipeline_parallel_size)
 
 
 class UniprocExecutor:
@@ -113,6 +126,7 @@ def worker_loop(runner: ModelRunner, ring_name: str, driver_pid: Optional[int] =
     message arrives (or the driver process is gone -- then the collectives could never
     complete, so the worker exits instead of waiting forever)."""
     ring = _native.runtime().ShmRing(ring_name, False)
+    poller = getattr(runner, "ar_poller", None)
     with torch.no_grad():
         while True:
             msg = ring.get(1.0)
@@ -124,6 +138,14 @@ def worker_loop(runner: ModelRunner, ring_name: str, driver_pid: Optional[int] =
             if not msg:
                 return
             runner.replay(runner.load_message(msg))
+            if poller is not None:
+                try:
+                    poller.step()
+                except RuntimeError:
+                    # the driver's monitor sees this exit and takes the replica down with it
+                    logger.critical("custom all-reduce error on TP rank %d; worker exiting",
+                                    pstate.tp_rank())
+                    os._exit(71)
 
 
 def _spawned_worker(cfg: EngineConfig, rank: int, world: int, port: int, ring_name: str,
@@ -132,12 +154,13 @@ def _spawned_worker(cfg: EngineConfig, rank: int, world: int, port: int, ring_na
                       MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     os.environ.pop("TORCHELASTIC_USE_AGENT_STORE", None)
     if cfg.device == "cuda" and torch.cuda.device_count() > 0:
-        torch.cuda.set_device(rank)
-        from ..utils.numa import pin_to_device
-        pin_to_device(rank)
-    pstate.init_distributed(cfg.parallel.tensor_parallel_size,
-                            enable_expert_parallel=cfg.parallel.enable_expert_parallel,
-                            pp_size=cfg.parallel.pipeline_parallel_size)
+        if cfg.parallel.share_device:
+            torch.cuda.set_device(0)        # one-GPU TP rehearsal: every rank on cuda:0
+        else:
+            torch.cuda.set_device(rank)
+            from ..utils.numa import pin_to_device
+            pin_to_device(rank)
+    _init_dist(cfg)
     runner = setup_runner(cfg)
     from ..utils.gc_tuning import tune_after_startup
     tune_after_startup()
@@ -181,9 +204,7 @@ class TPExecutor:
             if cfg.device == "cuda" and torch.cuda.device_count() > 0:
                 torch.cuda.set_device(0)
             try:
-                pstate.init_distributed(cfg.parallel.tensor_parallel_size,
-                                        enable_expert_parallel=cfg.parallel.enable_expert_parallel,
-                                        pp_size=cfg.parallel.pipeline_parallel_size)
+                _init_dist(cfg)
             finally:
                 # the rendezvous env is only for init: leaving it behind would make a later
                 # engine in this process think it is a torchrun-launched rank
@@ -224,8 +245,11 @@ class TPExecutor:
     def launch(self, bm, sched, overlap: bool):
         r = self.runner
         plan = r.prepare(bm, sched)
-        return r.launch_plan(plan, sched, overlap,
-                             publish=lambda pl: self._publish(r.encode_plan(pl)))
+        h = r.launch_plan(plan, sched, overlap,
+                          publish=lambda pl: self._publish(r.encode_plan(pl)))
+        if r.ar_poller is not None:
+            r.ar_poller.step()          # raises CustomAllReduceError -> engine dead, exit
+        return h
 
     def execute(self, bm, sched) -> StepOutput:
         return self.launch(bm, sched, overlap=False).result()
@@ -246,8 +270,8 @@ class TPExecutor:
 class FakeExecutor:
     """Test double for host-path benchmarking (``EIA_FAKE_STEP_MS=<ms>``): no model; every step
     sleeps the given time (a stand-in for the GPU) and samples uniform random tokens.  With it
-    the API server / engine core / SSE path can be load-tested on a CPU box at the real step
-    cadence (tests/test_serving_hostpath_cpu.py, scripts/hostpath_bench.sh)."""
+    the API server / engine core / SSE path -- and bench.py's multi-replica fan-out -- run on a
+    CPU box at the real step cadence (tests/test_bench_fanout_cpu.py)."""
 
     supports_overlap = False
 

@@ -167,6 +167,7 @@ class ModelRunner:
         self.graphs: Dict[int, torch.cuda.CUDAGraph] = {}
         self.graph_P: Dict[int, int] = {}
         self.graph_pool = None
+        self.ar_poller = None            # custom all-reduce error poller (TP>1 on GPUs)
         self.vocab = m.vocab_size
         self.num_heads = m.num_attention_heads // pstate.tp_size()
         # TP>1: the LM head stays vocab-sharded; unfiltered rows are sampled per shard and only

@@ -91,6 +91,9 @@ def make_parser(description: str = "MI355X OpenAI-compatible LLM server") -> arg
     a("--swap-space", type=float, default=4)
     a("--api-key", default=os.environ.get("VLLM_API_KEY"))
     a("--uvicorn-log-level", default="info")
+    a("--root-path", default=None,
+      help="URL prefix stripped from every request path (a proxy that cannot rewrite paths, "
+           "e.g. an EKS ALB routing /<model>/... to this pod)")
     a("--disable-custom-all-reduce", action="store_true")
     a("--max-log-len", type=int, default=None)
     a("--device", default="auto", choices=["auto", "cuda", "cpu", "rocm"])

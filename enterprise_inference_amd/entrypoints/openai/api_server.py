@@ -55,8 +55,30 @@ class _BearerAuth:
         await self.app(scope, receive, send)
 
 
+class _StripPrefix:
+    """``--root-path /<prefix>``: requests arrive as /<prefix>/v1/... (EKS ALB paths cannot
+    be rewritten) and are served as /v1/...; unprefixed paths (kubelet probes) pass as is."""
+
+    def __init__(self, app, prefix: str):
+        self.app = app
+        self.prefix = "/" + prefix.strip("/")
+
+    async def __call__(self, scope, receive, send):
+        if scope["type"] == "http":
+            path = scope["path"]
+            if path == self.prefix or path.startswith(self.prefix + "/"):
+                scope = dict(scope, path=path[len(self.prefix):] or "/",
+                             raw_path=(path[len(self.prefix):] or "/").encode())
+        await self.app(scope, receive, send)
+
+
+def bench_endpoints_enabled() -> bool:
+    return os.environ.get("EIA_BENCH_ENDPOINTS", "0") not in ("0", "", "false")
+
+
 def build_app(ctx: ServingContext, metrics=None, embedder=None, api_key: Optional[str] = None,
-              served_model_name: Optional[str] = None, wait_ready: bool = False) -> FastAPI:
+              served_model_name: Optional[str] = None, wait_ready: bool = False,
+              root_path: Optional[str] = None) -> FastAPI:
     """FastAPI app over a ServingContext (LLM) and/or an embedding engine (TEI-style)."""
     app = FastAPI(title="enterprise-inference-amd", version=__version__)
     model_name = served_model_name or (ctx.model if ctx else embedder.model_name)
@@ -65,6 +87,9 @@ def build_app(ctx: ServingContext, metrics=None, embedder=None, api_key: Optiona
         # Pure ASGI middleware (Starlette's BaseHTTPMiddleware re-streams every SSE chunk
         # through anyio memory streams: ~25 us/chunk of API-process CPU at 13k chunks/s).
         app.add_middleware(_BearerAuth, api_key=api_key)
+    if root_path and root_path.strip("/"):
+        # added last = outermost: the auth check above sees the stripped /v1/... path
+        app.add_middleware(_StripPrefix, prefix=root_path)
 
     @app.exception_handler(RequestValidationError)
     async def validation_error(_, exc):
@@ -144,16 +169,20 @@ def build_app(ctx: ServingContext, metrics=None, embedder=None, api_key: Optiona
         async def detokenize(body: dict):
             return {"prompt": ctx.tokenizer.decode(body.get("tokens", []))}
 
-        @app.post("/eia/sync")
-        async def engine_sync():
-            """Barrier with the device: returns once the engine drained its GPU queue
-            (bench.py brackets its timed region with it)."""
-            await ctx.engine.run_op("sync")
-            return {"ok": True}
+        if bench_endpoints_enabled():
+            # benchmark control, opt-in (EIA_BENCH_ENDPOINTS=1, set by bench.py for the servers
+            # it starts): a device sync between steps defeats overlapped scheduling, so a
+            # production pod never exposes it
+            @app.post("/eia/sync")
+            async def engine_sync():
+                """Barrier with the device: returns once the engine drained its GPU queue
+                (bench.py brackets its timed region with it)."""
+                await ctx.engine.run_op("sync")
+                return {"ok": True}
 
-        @app.get("/eia/stats")
-        async def engine_stats():
-            return await ctx.engine.run_op("stats")
+            @app.get("/eia/stats")
+            async def engine_stats():
+                return await ctx.engine.run_op("stats")
 
         from ...utils.profiling import profiler_dir
         if profiler_dir():
@@ -203,7 +232,8 @@ def build_from_args(args, engine_mode: Optional[str] = None, wait_ready: bool = 
         emb = EmbeddingEngine(cfg)
         metrics = EngineMetrics(cfg.served_model_name)
         return build_app(None, metrics, embedder=emb, api_key=args.api_key,
-                         served_model_name=cfg.served_model_name), None
+                         served_model_name=cfg.served_model_name,
+                         root_path=getattr(args, "root_path", None)), None
     metrics = EngineMetrics(cfg.served_model_name)
     if os.environ.get("WORLD_SIZE"):
         mode = "thread"          # torchrun-launched TP rank 0: this process is the driver
@@ -218,6 +248,7 @@ def build_from_args(args, engine_mode: Optional[str] = None, wait_ready: bool = 
         if os.environ.get("WORLD_SIZE"):
             from ...parallel import state as pstate
             pstate.init_distributed(cfg.parallel.tensor_parallel_size,
+                                    backend=cfg.parallel.dist_backend,
                                     enable_expert_parallel=cfg.parallel.enable_expert_parallel,
                                     pp_size=cfg.parallel.pipeline_parallel_size)
         engine = LLMEngine(cfg)
@@ -228,7 +259,8 @@ def build_from_args(args, engine_mode: Optional[str] = None, wait_ready: bool = 
                          tool_parser=args.tool_call_parser,
                          enable_auto_tool_choice=args.enable_auto_tool_choice,
                          generation_defaults=gen_defaults)
-    return build_app(ctx, metrics, api_key=args.api_key, wait_ready=wait_ready), aengine
+    return build_app(ctx, metrics, api_key=args.api_key, wait_ready=wait_ready,
+                     root_path=getattr(args, "root_path", None)), aengine
 
 
 def main(argv=None) -> int:
@@ -254,13 +286,36 @@ def main(argv=None) -> int:
         app.router.on_shutdown.append(_dump_profile)
     from ...utils.gc_tuning import tune_after_startup
     tune_after_startup()
+    if aengine is not None:
+        _exit_on_engine_death(aengine)
     try:
         uvicorn.run(app, host=args.host, port=args.port, log_level=args.uvicorn_log_level,
                     timeout_keep_alive=5)
     finally:
         if aengine is not None:
             aengine.shutdown()
-    return 0
+    return 1 if aengine is not None and aengine.dead is not None else 0
+
+
+def _exit_on_engine_death(aengine, grace_s: Optional[float] = None) -> None:
+    """A dead engine (step exception, custom all-reduce error, lost TP worker) keeps answering
+    ``/health`` with 500 for ``EIA_ENGINE_DEATH_GRACE_S`` (default 10 s: probes and clients see
+    the failure), then the server shuts down and ``main`` exits non-zero so the pod restarts."""
+    import signal
+    import threading
+    import time
+
+    grace = float(os.environ.get("EIA_ENGINE_DEATH_GRACE_S", 10)) if grace_s is None else grace_s
+
+    def watch():
+        while aengine.dead is None:
+            time.sleep(0.5)
+        logger.critical("engine is dead (%s); shutting the server down in %.0f s",
+                        aengine.dead, grace)
+        time.sleep(grace)
+        os.kill(os.getpid(), signal.SIGTERM)
+
+    threading.Thread(target=watch, name="eia-death-watch", daemon=True).start()
 
 
 if __name__ == "__main__":

@@ -274,6 +274,8 @@ def main(argv=None) -> int:
                     choices=["auto", "safetensors", "pt", "dummy"],
                     help="dummy: random weights (benchmarks); otherwise download / load")
     ap.add_argument("--huggingface-hub-cache", default=os.environ.get("HF_HUB_CACHE"))
+    ap.add_argument("--root-path", default=os.environ.get("ROOT_PATH"),
+                    help="URL prefix stripped from request paths (EKS ALB without APISIX)")
     args, unknown = ap.parse_known_args(normalise_argv(list(sys.argv[1:] if argv is None else argv)))
     if unknown:
         logger.warning("ignoring unsupported arguments: %s", unknown)
@@ -292,6 +294,9 @@ def main(argv=None) -> int:
         emb.model.pooling = args.pooling
     emb.warmup(int(os.environ.get("MAX_WARMUP_SEQUENCE_LENGTH", 512)))
     app = build_tei_app(emb)
+    if args.root_path and args.root_path.strip("/"):
+        from ..openai.api_server import _StripPrefix
+        app.add_middleware(_StripPrefix, prefix=args.root_path)
     from ...utils.gc_tuning import tune_after_startup
     tune_after_startup()
     uvicorn.run(app, host=args.hostname, port=args.port)

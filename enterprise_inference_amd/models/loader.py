@@ -54,7 +54,11 @@ def build_model(cfg: EngineConfig, device: torch.device) -> nn.Module:
     model = cls(cfg.model, dtype=cfg.dtype, device=device)
     model.eval()
     fmt = cfg.load_format
-    if cfg.model_path is None or fmt == "dummy":
+    if cfg.model_path is None and fmt != "dummy":
+        # never serve random weights by accident: only --load-format dummy asks for them
+        raise ValueError("no model_path given and load_format is not 'dummy' (random weights "
+                         "must be requested explicitly)")
+    if fmt == "dummy":
         logger.info("random-init weights (load_format=%s, no checkpoint)", fmt)
         init_random_(model, seed=cfg.seed)
         post = getattr(model, "post_load", None)

@@ -177,6 +177,17 @@ class CustomAllReduce:
                       "ar_read_err")
         return v.value
 
+    def read_error_async(self, host_dst: torch.Tensor) -> None:
+        """Enqueue a copy of the flag into pinned int32 ``host_dst`` on the current stream."""
+        _native.check(self.lib.eia_ar_read_err_async(
+            ctypes.c_void_p(self.own_sig), ctypes.c_void_p(host_dst.data_ptr()),
+            torch.cuda.current_stream().cuda_stream), "ar_read_err_async")
+
+    def inject_error(self, v: int = 1) -> None:
+        """Test hook: set this rank's flag as a timed-out barrier would."""
+        _native.check(self.lib.eia_ar_set_err(ctypes.c_void_p(self.own_sig), int(v)),
+                      "ar_set_err")
+
     def close(self) -> None:
         hip = _hiprt()
         if hip is None:
@@ -186,6 +197,54 @@ class CustomAllReduce:
         for p in self._own:
             self.lib.eia_ar_free(ctypes.c_void_p(p))
         self._opened, self._own = [], []
+
+
+class CustomAllReduceError(RuntimeError):
+    """A custom all-reduce barrier timed out: this rank's activations are no longer valid."""
+
+
+class ErrorPoller:
+    """Failure detection for the custom all-reduce.
+
+    A barrier spin that exhausts its bound sets the rank's error flag and the kernel returns
+    with stale peer data summed in, so every activation after it is wrong.  The serving loop
+    calls ``step()`` once per launched step; every ``every`` steps it enqueues a stream-ordered
+    copy of the flag into pinned memory behind an event and, at the next poll, reads the copy
+    it enqueued last time (no device-wide synchronisation on the step path).  ``check_now``
+    is the synchronous form (after graph capture / warm-up).  Both raise
+    ``CustomAllReduceError``; the engine core then reports itself dead (``/health`` -> 500)
+    and exits non-zero, so the pod restarts instead of serving garbage."""
+
+    def __init__(self, ar, every: Optional[int] = None):
+        self.ar = ar
+        self.every = max(1, int(every or os.environ.get("EIA_AR_CHECK_STEPS", 64)))
+        self.n = 0
+        self._host = torch.zeros(1, dtype=torch.int32, pin_memory=torch.cuda.is_available())
+        self._event = None
+        self._pending = False
+
+    def _fail(self) -> None:
+        raise CustomAllReduceError("custom all-reduce barrier timed out (a TP peer stalled); "
+                                   "results since then are invalid")
+
+    def check_now(self) -> None:
+        if self.ar.error_flag():
+            self._fail()
+
+    def step(self) -> None:
+        self.n += 1
+        if self.n % self.every:
+            return
+        if self._pending:
+            if self._event is not None:
+                self._event.synchronize()    # enqueued `every` steps ago: long complete
+            if int(self._host[0]) != 0:
+                self._fail()
+        self.ar.read_error_async(self._host)
+        self._pending = True
+        if torch.cuda.is_available():
+            self._event = torch.cuda.Event()
+            self._event.record()
 
 
 def init_custom_allreduce(max_bytes: int) -> Optional[CustomAllReduce]:

@@ -28,10 +28,12 @@ from typing import Optional, Tuple
 import torch
 import torch.distributed as dist
 
+from . import comm
+
 
 def _exchange_counts(send_counts: torch.Tensor, group) -> torch.Tensor:
     recv = torch.empty_like(send_counts)
-    dist.all_to_all_single(recv, send_counts, group=group)
+    comm.all_to_all_single(recv, send_counts, group=group)
     return recv
 
 
@@ -44,6 +46,7 @@ def moe_all_to_all(x: torch.Tensor, topk_w: torch.Tensor, topk_ids: torch.Tensor
     [e_per, H, I]); expert e lives on rank e // e_per.  Returns [T_r, H]."""
     from ..ops import moe as moe_ops
 
+    group = group if group is not None else dist.group.WORLD
     W = world or dist.get_world_size(group)
     T, H = x.shape
     k = topk_ids.shape[1]
@@ -59,8 +62,8 @@ def moe_all_to_all(x: torch.Tensor, topk_w: torch.Tensor, topk_ids: torch.Tensor
     R = sum(rc)
     recv_x = x.new_empty((R, H))
     recv_e = torch.empty(R, dtype=torch.int32, device=x.device)
-    dist.all_to_all_single(recv_x, send_x, rc, sc, group=group)
-    dist.all_to_all_single(recv_e, send_e, rc, sc, group=group)
+    comm.all_to_all_single(recv_x, send_x, rc, sc, group=group)
+    comm.all_to_all_single(recv_e, send_e, rc, sc, group=group)
     if R:
         ones = torch.ones(R, 1, dtype=torch.float32, device=x.device)
         y = moe_ops.fused_moe(recv_x, w13_local, w2_local, ones, recv_e[:, None],
@@ -68,7 +71,7 @@ def moe_all_to_all(x: torch.Tensor, topk_w: torch.Tensor, topk_ids: torch.Tensor
     else:
         y = x.new_empty((0, H))
     back = x.new_empty((len(order), H))
-    dist.all_to_all_single(back, y.contiguous(), sc, rc, group=group)
+    comm.all_to_all_single(back, y.contiguous(), sc, rc, group=group)
     w_sorted = topk_w.reshape(-1).index_select(0, order).float()
     out = torch.zeros(T, H, dtype=torch.float32, device=x.device)
     out.index_add_(0, tok, back.float() * w_sorted[:, None])
@@ -87,6 +90,7 @@ def moe_all_to_all_replicated(x: torch.Tensor, topk_w: torch.Tensor, topk_ids: t
     """All-to-all EP inside a tensor-parallel engine (tokens replicated on every rank): rank
     r dispatches its 1/W slice of the tokens, then an all-gather rebuilds [T, H] -- the MoE
     output is complete on every rank (no trailing all-reduce)."""
+    group = group if group is not None else dist.group.WORLD
     W = dist.get_world_size(group)
     r = dist.get_rank(group)
     T, H = x.shape
@@ -96,11 +100,5 @@ def moe_all_to_all_replicated(x: torch.Tensor, topk_w: torch.Tensor, topk_ids: t
     per = -(-T // W)
     mine = x.new_zeros((per, H))
     mine[:hi - lo] = part
-    if dist.get_backend(group) == "nccl":
-        buf = x.new_empty((per * W, H))
-        dist.all_gather_into_tensor(buf, mine, group=group)
-    else:                                   # gloo (CPU rehearsal)
-        parts = [x.new_empty((per, H)) for _ in range(W)]
-        dist.all_gather(parts, mine, group=group)
-        buf = torch.cat(parts)
+    buf = comm.all_gather(mine, 0, group=group)          # [per * W, H]
     return buf[:T]

@@ -33,6 +33,7 @@ _PP_SIZE = 1
 _PP_RANKS: List[int] = [0]           # global ranks of my PP group, by stage
 _REPLICA_RANKS: List[int] = [0]      # all PP*TP ranks of my model replica
 _REPLICA_CPU_GROUP: Optional[dist.ProcessGroup] = None
+_BACKEND = "none"
 
 
 def env_rank() -> int:
@@ -52,7 +53,7 @@ def init_distributed(tp_size: int = 1, backend: Optional[str] = None,
                      pp_size: int = 1) -> None:
     """Initialise torch.distributed from the torchrun env (no-op for a single process)."""
     global _TP_GROUP, _DP_GROUP, _CPU_GROUP, _TP_RANK, _TP_SIZE, _TP_RANKS, _EP_ENABLED
-    global _PP_RANK, _PP_SIZE, _PP_RANKS, _REPLICA_RANKS, _REPLICA_CPU_GROUP
+    global _PP_RANK, _PP_SIZE, _PP_RANKS, _REPLICA_RANKS, _REPLICA_CPU_GROUP, _BACKEND
     world = env_world()
     _EP_ENABLED = enable_expert_parallel
     if world == 1 and tp_size == 1 and pp_size == 1:
@@ -63,7 +64,7 @@ def init_distributed(tp_size: int = 1, backend: Optional[str] = None,
     if world % rep != 0:
         raise ValueError(f"WORLD_SIZE={world} not divisible by tensor_parallel_size x "
                          f"pipeline_parallel_size = {rep}")
-    if backend is None:
+    if backend in (None, "auto"):
         backend = "nccl" if torch.cuda.is_available() else "gloo"
     if not dist.is_initialized():
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
@@ -73,6 +74,7 @@ def init_distributed(tp_size: int = 1, backend: Optional[str] = None,
             kw["device_id"] = torch.device("cuda", env_local_rank())
         dist.init_process_group(backend=backend, timeout=datetime.timedelta(seconds=timeout_s),
                                 **kw)
+    _BACKEND = dist.get_backend()
     rank = dist.get_rank()
     # every rank must create every group in the same order
     for g in range(world // tp_size):
@@ -103,12 +105,24 @@ def init_distributed(tp_size: int = 1, backend: Optional[str] = None,
 
 def destroy_distributed() -> None:
     global _TP_GROUP, _DP_GROUP, _CPU_GROUP, _TP_RANK, _TP_SIZE, _TP_RANKS
-    global _PP_RANK, _PP_SIZE, _PP_RANKS, _REPLICA_RANKS, _REPLICA_CPU_GROUP
+    global _PP_RANK, _PP_SIZE, _PP_RANKS, _REPLICA_RANKS, _REPLICA_CPU_GROUP, _BACKEND
+    _BACKEND = "none"
     if dist.is_initialized():
         dist.destroy_process_group()
     _TP_GROUP = _DP_GROUP = _CPU_GROUP = _REPLICA_CPU_GROUP = None
     _TP_RANK, _TP_SIZE, _TP_RANKS = 0, 1, [0]
     _PP_RANK, _PP_SIZE, _PP_RANKS, _REPLICA_RANKS = 0, 1, [0], [0]
+
+
+def backend() -> str:
+    """"nccl" (RCCL), "gloo" or "none" (single process)."""
+    return _BACKEND
+
+
+def host_staged() -> bool:
+    """Device tensors cross a gloo group through host memory (one-GPU TP rehearsal,
+    EIA_TP_SHARE_DEVICE): the collectives in parallel/comm.py stage them."""
+    return _BACKEND == "gloo"
 
 
 def tp_rank() -> int:

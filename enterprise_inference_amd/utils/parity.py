@@ -54,3 +54,27 @@ def check_greedy(hf, prompts, outputs, tol: float) -> Dict[str, float]:
         raise AssertionError(f"engine token {worst:.4f} below the fp32 oracle's best logit "
                              f"(tol {tol}); margins {m}")
     return {"worst_margin": worst, "argmax_agreement": exact}
+
+
+@torch.no_grad()
+def check_logprobs(hf, prompts, outputs, engine_logprobs, tol: float) -> Dict[str, float]:
+    """Logits-level bound: for every generated step the engine's reported log-probs (its
+    top-k + the chosen token, i.e. ``SamplingParams(logprobs=k)``) must match the fp32
+    oracle's log-softmax over the same prefix within ``tol`` nats.  Log-probs are the logits
+    minus their logsumexp, so this bounds the whole logit row's shape on the entries that
+    matter for sampling -- a much sharper check than the token margin on near-flat rows."""
+    worst = 0.0
+    n = 0
+    for p, o, lps in zip(prompts, outputs, engine_logprobs):
+        full = torch.tensor([list(p) + list(o)])
+        ref = torch.log_softmax(hf(full).logits[0].float(), -1)[len(p) - 1:len(p) - 1 + len(o)]
+        for r, d in enumerate(lps):
+            ids = torch.tensor(list(d.keys()))
+            got = torch.tensor(list(d.values()), dtype=torch.float32)
+            err = (got - ref[r, ids]).abs().max().item()
+            worst = max(worst, err)
+            n += len(d)
+    if worst > tol:
+        raise AssertionError(f"engine log-probs differ from the fp32 oracle by {worst:.4f} "
+                             f"nats (tol {tol})")
+    return {"logprob_max_abs": worst, "entries": n}

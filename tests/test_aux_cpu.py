@@ -279,3 +279,57 @@ def test_gc_tuning(monkeypatch):
     finally:
         gc.unfreeze()
         gc.set_threshold(*old)
+
+
+def test_custom_allreduce_error_poller_cpu():
+    """Failure detection: the poller reads the flag it enqueued one period earlier and raises
+    once a barrier timeout was recorded (fake all-reduce object, no GPU)."""
+    from enterprise_inference_amd.parallel.custom_allreduce import CustomAllReduceError, ErrorPoller
+
+    class FakeAR:
+        flag = 0
+
+        def error_flag(self):
+            return self.flag
+
+        def read_error_async(self, host):
+            host[0] = self.flag
+
+    ar = FakeAR()
+    p = ErrorPoller(ar, every=3)
+    for _ in range(9):
+        p.step()
+    p.check_now()
+    ar.flag = 1
+    with pytest.raises(CustomAllReduceError):
+        p.check_now()
+    hit = None
+    for i in range(12):
+        try:
+            p.step()
+        except CustomAllReduceError:
+            hit = i
+            break
+    assert hit is not None and hit < 6
+
+
+def test_engine_death_stops_server(monkeypatch):
+    """A dead engine keeps /health at 500 for the grace period, then the server is signalled
+    to shut down (main() then exits non-zero)."""
+    import signal
+    from enterprise_inference_amd.entrypoints.openai import api_server
+
+    class Eng:
+        dead = None
+
+    sent = []
+    monkeypatch.setattr(api_server.os, "kill", lambda pid, sig: sent.append(sig))
+    e = Eng()
+    api_server._exit_on_engine_death(e, grace_s=0.1)
+    time.sleep(0.7)
+    assert not sent
+    e.dead = RuntimeError("custom all-reduce barrier timed out")
+    deadline = time.time() + 5
+    while not sent and time.time() < deadline:
+        time.sleep(0.1)
+    assert sent == [signal.SIGTERM]

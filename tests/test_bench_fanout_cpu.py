@@ -1,0 +1,84 @@
+"""bench.py multi-GPU launch forms, rehearsed on the CPU with the fake executor
+(``EIA_FAKE_STEP_MS``: every engine step sleeps instead of running a model).
+
+* ``python bench.py --gpus N`` without torchrun (how a driver may start it) must fan out by
+  itself: N/tp servers, each on its own HIP_VISIBLE_DEVICES slice, one JSON line with
+  ``n_gpus: N`` and the aggregate tok/s.
+* the same under ``torch.distributed.run --nproc-per-node N``: one replica per rank.
+* ``--co-deploy`` (BASELINE config #5): replicas alternate Llama-3.1-8B / Mistral-7B.
+"""
+
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+SMALL = ["--steps", "2", "--warmup", "1", "--users", "3", "--input-len", "8",
+         "--output-len", "4", "--client-procs", "1", "--max-num-seqs", "8",
+         "--max-num-batched-tokens", "64"]
+
+
+def _run(tmp_path, argv, launcher=()):
+    env = dict(os.environ, EIA_FAKE_STEP_MS="2", EIA_BENCH_LOGDIR=str(tmp_path),
+               PYTHONPATH=ROOT)
+    env.pop("HIP_VISIBLE_DEVICES", None)
+    r = subprocess.run([sys.executable, *launcher, os.path.join(ROOT, "bench.py"), *argv, *SMALL],
+                       cwd=ROOT, env=env, capture_output=True, text=True, timeout=400)
+    assert r.returncode == 0, (r.stdout + r.stderr)[-4000:]
+    lines = [json.loads(x) for x in r.stdout.splitlines() if x.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    return lines[0]
+
+
+def test_visible_device_slices(monkeypatch):
+    sys.path.insert(0, ROOT)
+    import bench
+    monkeypatch.delenv("HIP_VISIBLE_DEVICES", raising=False)
+    monkeypatch.delenv("CUDA_VISIBLE_DEVICES", raising=False)
+    assert bench._visible_devices(0, 1) == "0"
+    assert bench._visible_devices(4, 4) == "4,5,6,7"
+    monkeypatch.setenv("HIP_VISIBLE_DEVICES", "3,5,6,7")
+    assert bench._visible_devices(2, 2) == "6,7"
+
+
+def test_fanout_without_torchrun(tmp_path):
+    out = _run(tmp_path, ["--gpus", "4"])
+    assert out["n_gpus"] == 4
+    assert out["config"]["parallelism"] == "dp4"
+    assert out["config"]["global_batch"] == 12
+    assert out["failed_requests"] == 0
+    assert out["value"] > 0
+    logs = sorted(p.name for p in tmp_path.iterdir() if p.name.startswith("bench_server"))
+    assert logs == [f"bench_server_rank{i}.log" for i in range(4)]
+
+
+def test_fanout_tensor_parallel_replicas(tmp_path):
+    """--gpus 4 --tp 2: two replicas on GPUs {0,1} and {2,3} (the fake executor ignores TP)."""
+    out = _run(tmp_path, ["--gpus", "4", "--tp", "2"])
+    assert out["n_gpus"] == 4
+    assert out["config"]["parallelism"] == "dp2xtp2"
+    logs = sorted(p.name for p in tmp_path.iterdir() if p.name.startswith("bench_server"))
+    assert logs == ["bench_server_rank0.log", "bench_server_rank2.log"]
+
+
+def test_co_deploy(tmp_path):
+    out = _run(tmp_path, ["--gpus", "2", "--co-deploy"])
+    assert out["n_gpus"] == 2
+    assert out["config"]["model"] == \
+        "meta-llama/Llama-3.1-8B-Instruct+mistralai/Mistral-7B-Instruct-v0.3"
+    pm = out["per_model"]
+    assert set(pm) == {"meta-llama/Llama-3.1-8B-Instruct", "mistralai/Mistral-7B-Instruct-v0.3"}
+    assert all(v["replicas"] == 1 and v["tok_s"] > 0 for v in pm.values())
+    assert out["vs_baseline"] is None     # no published Mistral-7B number
+
+
+@pytest.mark.slow
+def test_torchrun_form(tmp_path):
+    out = _run(tmp_path, ["--gpus", "2"],
+               launcher=("-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+                         "--master-addr", "127.0.0.1", "--master-port", "29637"))
+    assert out["n_gpus"] == 2
+    assert out["config"]["parallelism"] == "dp2"

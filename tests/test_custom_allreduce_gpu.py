@@ -240,3 +240,53 @@ def test_allreduce_add_rmsnorm_multistream(tmp_path, world):
     out = r.stdout + r.stderr
     assert r.returncode == 0, out[-3000:]
     assert "NO_SPIN_ERR BAD 0" in out, out[-3000:]
+
+
+ERRFLAG = textwrap.dedent('''
+    import os, sys, torch, torch.distributed as dist
+    sys.path.insert(0, os.environ["EIA_ROOT"])
+    torch.cuda.set_device(0)
+    dist.init_process_group("gloo", rank=0, world_size=1,
+                            init_method="tcp://127.0.0.1:" + os.environ["EIA_PORT"])
+    from enterprise_inference_amd.parallel.custom_allreduce import (CustomAllReduce,
+                                                                    CustomAllReduceError,
+                                                                    ErrorPoller)
+    ar = CustomAllReduce(1 << 20, cpu_group=dist.group.WORLD, rank=0, world=1, nblocks=4)
+    p = ErrorPoller(ar, every=2)
+    assert ar.error_flag() == 0
+    p.check_now()
+    for _ in range(4):
+        p.step()                 # clean flag: polls pass
+    ar.inject_error(1)
+    try:
+        p.check_now()
+        raise SystemExit("check_now missed the flag")
+    except CustomAllReduceError:
+        pass
+    raised_at = None
+    for i in range(8):
+        try:
+            p.step()
+        except CustomAllReduceError:
+            raised_at = i
+            break
+    assert raised_at is not None and raised_at <= 3, raised_at
+    ar.inject_error(0)
+    assert ar.error_flag() == 0
+    ar.close()
+    print("ERRFLAG_OK", raised_at, flush=True)
+''')
+
+
+def test_error_flag_poller_on_device(tmp_path):
+    """The barrier-timeout flag lives in the uncached signal block: fault-inject it and the
+    stream-ordered poller (what the TP driver and workers run every EIA_AR_CHECK_STEPS steps)
+    raises within two poll periods; the synchronous check raises at once."""
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    f = tmp_path / "errflag.py"
+    f.write_text(ERRFLAG)
+    env = dict(os.environ, EIA_ROOT=root, EIA_PORT=str(_port()))
+    r = subprocess.run([sys.executable, str(f)], env=env, capture_output=True, text=True,
+                       timeout=120)
+    out = r.stdout + r.stderr
+    assert r.returncode == 0 and "ERRFLAG_OK" in out, out[-3000:]

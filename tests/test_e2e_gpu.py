@@ -14,7 +14,7 @@ from enterprise_inference_amd.config import CacheConfig, EngineConfig, ModelConf
 from enterprise_inference_amd.engine.llm_engine import LLMEngine
 from enterprise_inference_amd.engine.sampling_params import SamplingParams
 from enterprise_inference_amd.models.catalog import tiny_config
-from enterprise_inference_amd.utils.parity import check_greedy, hf_reference_model
+from enterprise_inference_amd.utils.parity import check_greedy, check_logprobs, hf_reference_model
 
 pytestmark = pytest.mark.gpu
 
@@ -59,6 +59,14 @@ def test_engine_greedy_matches_fp32_oracle(arch):
     stats = check_greedy(hf, prompts, toks, tol=0.08)
     print(arch, stats)
     assert stats["argmax_agreement"] > 0.8
+    # logits-level bound (graph decode + logprobs path): top-5 + chosen log-probs vs fp32
+    lp_prompts = [short, mid]
+    lp_outs = eng.generate(prompt_token_ids=lp_prompts,
+                           params=SamplingParams(max_tokens=8, temperature=0, ignore_eos=True,
+                                                 logprobs=5))
+    lstats = check_logprobs(hf, lp_prompts, [o.outputs[0].token_ids for o in lp_outs],
+                            [o.outputs[0].logprobs for o in lp_outs], tol=0.05)
+    print(arch, lstats)
 
 
 def test_engine_sampled_run_is_reproducible():

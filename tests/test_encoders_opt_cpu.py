@@ -59,7 +59,7 @@ def test_tei_server(tmp_path, cfgd):
     from enterprise_inference_amd.entrypoints.tei.server import EmbeddingEngine, build_tei_app
     (tmp_path / "config.json").write_text(json.dumps(cfgd))
     cfg = EngineConfig(model=ModelConfig.from_hf_dict(cfgd, name="m"), device="cpu",
-                       dtype=torch.float32, served_model_name="m")
+                       dtype=torch.float32, served_model_name="m", load_format="dummy")
     emb = EmbeddingEngine(cfg, max_batch_tokens=64)
     c = TestClient(build_tei_app(emb))
     assert c.get("/health").status_code == 200
@@ -93,7 +93,7 @@ def test_opt_matches_transformers():
                        cache=CacheConfig(block_size=16, num_gpu_blocks=32),
                        scheduler=SchedulerConfig(max_num_seqs=4, max_num_batched_tokens=32,
                                                  max_model_len=256),
-                       device="cpu", dtype=torch.float32)
+                       device="cpu", dtype=torch.float32, load_format="dummy")
     eng = LLMEngine(cfg)
     eng.executor.runner.model.load_weights(hf.state_dict().items())
     prompt = [2, 11, 45, 7, 99, 100, 3, 5, 8, 13, 21, 34, 55, 89, 144, 233, 17, 18, 19, 20]

@@ -15,7 +15,7 @@ def _engine(d, mbt=64, bs=16, nblocks=64, prefix=True, max_seqs=8):
                                                   enable_prefix_caching=prefix),
                        scheduler=SchedulerConfig(max_num_seqs=max_seqs, max_num_batched_tokens=mbt,
                                                  max_model_len=512),
-                       device="cpu", dtype=torch.float32)
+                       device="cpu", dtype=torch.float32, load_format="dummy")
     return LLMEngine(cfg)
 
 

@@ -61,7 +61,7 @@ def test_vision_greedy_matches_transformers(lead):
                        cache=CacheConfig(block_size=16, num_gpu_blocks=64),
                        scheduler=SchedulerConfig(max_num_seqs=4, max_num_batched_tokens=48,
                                                  max_model_len=512),
-                       device="cpu", dtype=torch.float32)
+                       device="cpu", dtype=torch.float32, load_format="dummy")
     eng = LLMEngine(cfg)
     model = eng.executor.runner.model
     assert model.vision is not None and model.vision.tokens_per_tile == 4

@@ -14,7 +14,7 @@ def _engine(d):
                        cache=CacheConfig(block_size=16, num_gpu_blocks=64),
                        scheduler=SchedulerConfig(max_num_seqs=4, max_num_batched_tokens=48,
                                                  max_model_len=512),
-                       device="cpu", dtype=torch.float32)
+                       device="cpu", dtype=torch.float32, load_format="dummy")
     return LLMEngine(cfg)
 
 
