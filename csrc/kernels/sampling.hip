@@ -176,7 +176,8 @@ EIA_API int eia_sample(const float* logits, long stride, int B, int V, const flo
 __global__ void __launch_bounds__(SPLIT_THREADS)
 sample_split_kernel(const float* __restrict__ logits, long stride, int V, int chunk,
                     const float* __restrict__ temperature, const uint64_t* __restrict__ seeds,
-                    float* __restrict__ part_v, int* __restrict__ part_i, int vocab_offset) {
+                    float* __restrict__ part_v, int* __restrict__ part_i, int vocab_offset,
+                    const uint32_t* __restrict__ floor_keys) {
   __shared__ float sv[SPLIT_THREADS / 64];
   __shared__ int si[SPLIT_THREADS / 64];
   const int b = blockIdx.y, c = blockIdx.x, C = gridDim.x;
@@ -185,10 +186,14 @@ sample_split_kernel(const float* __restrict__ logits, long stride, int V, int ch
   const float T = temperature[b];
   const bool greedy = !(T > 0.f);
   const uint64_t seed = seeds[b];
+  // admissible-set floor of a filtered row (tensor-parallel top-k / top-p / min-p; the
+  // threshold key is global, computed over all shards): keys below it do not take part
+  const uint32_t fk = (floor_keys != nullptr && !greedy) ? floor_keys[b] : 0u;
   ArgMax best{-INFINITY, 0x7fffffff};
   for (int i = lo + threadIdx.x; i < hi; i += SPLIT_THREADS) {
     const float l = row[i];
     const int gi = i + vocab_offset;
+    if (fk != 0u && f2key(l) < fk) continue;
     float v = l;
     if (!greedy) {
       const float u = rng_uniform(seed, (uint32_t)gi);
@@ -230,7 +235,7 @@ EIA_API int eia_sample_split(const float* logits, long stride, int B, int V, int
   const int C = (V + chunk - 1) / chunk;
   if (C > 4096) return EIA_BAD_SHAPE;
   hipLaunchKernelGGL(sample_split_kernel, dim3(C, B), dim3(SPLIT_THREADS), 0, st, logits, stride,
-                     V, chunk, temperature, seeds, part_v, part_i, 0);
+                     V, chunk, temperature, seeds, part_v, part_i, 0, nullptr);
   hipLaunchKernelGGL(sample_merge_kernel, dim3(B), dim3(64), 0, st, part_v, part_i, C, out_tokens,
                      nullptr);
   EIA_LAUNCH_CHECK();
@@ -240,18 +245,61 @@ EIA_API int eia_sample_split(const float* logits, long stride, int B, int V, int
 // shard [vocab_offset, vocab_offset + V) of unfiltered rows and writes the shard winner's
 // (perturbed value, global id); the ranks then exchange B (value, id) pairs and keep the max,
 // lowest id on ties -- the same token the full-row sampler picks.
+// floor_keys (nullable): per-row admissible floor of filtered rows (ops/shard_sampling.py).
 EIA_API int eia_sample_shard(const float* logits, long stride, int B, int V, int chunk,
                              int vocab_offset, const float* temperature, const uint64_t* seeds,
                              float* part_v, int* part_i, float* out_v, int* out_i,
-                             hipStream_t st) {
+                             const uint32_t* floor_keys, hipStream_t st) {
   if (B < 0 || V <= 0 || chunk <= 0 || vocab_offset < 0) return EIA_BAD_SHAPE;
   if (B == 0) return EIA_OK;
   const int C = (V + chunk - 1) / chunk;
   if (C > 4096) return EIA_BAD_SHAPE;
   hipLaunchKernelGGL(sample_split_kernel, dim3(C, B), dim3(SPLIT_THREADS), 0, st, logits, stride,
-                     V, chunk, temperature, seeds, part_v, part_i, vocab_offset);
+                     V, chunk, temperature, seeds, part_v, part_i, vocab_offset, floor_keys);
   hipLaunchKernelGGL(sample_merge_kernel, dim3(B), dim3(64), 0, st, part_v, part_i, C, out_i,
                      out_v);
+  EIA_LAUNCH_CHECK();
+}
+
+// Tensor-parallel exact top-p (ops/shard_sampling.py): one round of the radix select of
+// sample_kernel, distributed over vocab shards.  Per row: the probability-mass histogram of
+// the 8-bit digit at `shift` of the keys that match (prefix, pmask) and lie at or above the
+// row's floor (its top-k threshold); weights exp((l - m) / T) with the GLOBAL row max m.  The
+// ranks all-reduce the [B, 256] histograms and pick the digit; 4 rounds give the exact
+// nucleus threshold without gathering any logits.
+__global__ void __launch_bounds__(1024)
+radix_hist_kernel(const float* __restrict__ logits, long stride, int V,
+                  const float* __restrict__ row_max, const float* __restrict__ temperature,
+                  const uint32_t* __restrict__ floor_key, const uint32_t* __restrict__ prefix,
+                  const uint32_t* __restrict__ pmask, int shift, float* __restrict__ hist_out) {
+  __shared__ float hist[256];
+  const int b = blockIdx.x;
+  for (int i = threadIdx.x; i < 256; i += blockDim.x) hist[i] = 0.f;
+  __syncthreads();
+  const float T = temperature[b];
+  if (T > 0.f) {
+    const float* row = logits + (long)b * stride;
+    const float m = row_max[b], invT = 1.f / T;
+    const uint32_t fk = floor_key[b], pf = prefix[b], pm = pmask[b];
+    for (int i = threadIdx.x; i < V; i += blockDim.x) {
+      const float l = row[i];
+      const uint32_t k = f2key(l);
+      if (k < fk || (k & pm) != pf) continue;
+      atomicAdd(&hist[(k >> shift) & 0xFF], __expf((l - m) * invT));
+    }
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < 256; i += blockDim.x) hist_out[(long)b * 256 + i] = hist[i];
+}
+
+EIA_API int eia_radix_hist(const float* logits, long stride, int B, int V, const float* row_max,
+                           const float* temperature, const uint32_t* floor_key,
+                           const uint32_t* prefix, const uint32_t* pmask, int shift,
+                           float* hist_out, hipStream_t st) {
+  if (B < 0 || V <= 0 || shift < 0 || shift > 24 || (shift & 7)) return EIA_BAD_SHAPE;
+  if (B == 0) return EIA_OK;
+  hipLaunchKernelGGL(radix_hist_kernel, dim3(B), dim3(1024), 0, st, logits, stride, V, row_max,
+                     temperature, floor_key, prefix, pmask, shift, hist_out);
   EIA_LAUNCH_CHECK();
 }
 

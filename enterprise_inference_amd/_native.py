@@ -49,7 +49,8 @@ _SIGNATURES = {
     "eia_sample": [P, L, I, I, P, P, P, P, P, P, S],
     "eia_apply_penalties": [P, L, P, P, P, I, P, P, P, S],
     "eia_sample_split": [P, L, I, I, I, P, P, P, P, P, S],
-    "eia_sample_shard": [P, L, I, I, I, I, P, P, P, P, P, P, S],
+    "eia_sample_shard": [P, L, I, I, I, I, P, P, P, P, P, P, P, S],
+    "eia_radix_hist": [P, L, I, I, P, P, P, P, P, I, P, S],
     "eia_fill_ids": [P, P, P, I, S],
     "eia_moe_topk": [P, I, I, I, I, I, I, P, P, S],
     "eia_moe_align": [P, I, I, I, I, P, P, P, I, S],

@@ -54,6 +54,11 @@ def setup_runner(cfg: EngineConfig) -> ModelRunner:
     nb = runner.determine_num_blocks()
     nb = _agree_num_blocks(nb)
     runner.allocate_kv_cache(nb)
+    # K14 swap space on every rank of the replica (each swaps its own KV shard), same count
+    from .swap import swap_blocks_for
+    runner.allocate_swap(_agree_num_blocks(
+        swap_blocks_for(runner.kv_bytes_per_block(), cfg.cache.swap_space_gb)
+        if swap_enabled(runner) else 0))
     runner.capture_graphs()
     runner.ar_poller = None
     if ar is not None:
@@ -61,6 +66,13 @@ def setup_runner(cfg: EngineConfig) -> ModelRunner:
         runner.ar_poller = ErrorPoller(ar)
         runner.ar_poller.check_now()     # profiling run + graph warm-up used the kernel
     return runner
+
+
+def swap_enabled(runner: ModelRunner) -> bool:
+    """Swapping KV into host memory only pays off from a GPU: a CPU engine's KV already lives
+    in host RAM (vLLM's CPU backend has no swap space either), so it keeps recompute
+    preemption -- EIA_CPU_SWAP=1 turns it on for the CPU tests of the swap machinery."""
+    return runner.is_gpu or os.environ.get("EIA_CPU_SWAP", "0") not in ("0", "", "false")
 
 
 def _init_dist(cfg: EngineConfig) -> None:
@@ -84,13 +96,9 @@ class UniprocExecutor:
     def launch(self, bm, sched, overlap: bool):
         return self.runner.launch(bm, sched, overlap)
 
-    # KV swap (K14): single-rank engines only -- TP/PP keep recompute preemption
+    # KV swap (K14): the pool is allocated in setup_runner (swap_enabled)
     def allocate_swap(self, swap_space_gb: float) -> int:
-        from .swap import swap_blocks_for
-        r = self.runner
-        if getattr(r, "kv_buf", None) is None:
-            return 0
-        return r.allocate_swap(swap_blocks_for(r.kv_bytes_per_block(), swap_space_gb))
+        return getattr(self.runner, "num_cpu_blocks", 0)
 
     def swap_out(self, gpu_blocks, cpu_blocks) -> None:
         self.runner.swap_out(gpu_blocks, cpu_blocks)
@@ -104,6 +112,9 @@ class UniprocExecutor:
 
     def swap_in(self, cpu_blocks, gpu_blocks) -> None:
         self.runner.swap_in(cpu_blocks, gpu_blocks)
+
+    def copy_blocks(self, pairs) -> None:
+        self.runner.copy_blocks(pairs)
 
     def shutdown(self) -> None:
         pass
@@ -216,6 +227,7 @@ class TPExecutor:
             self._start_monitor()
         self.runner = setup_runner(cfg)
         self.num_blocks = self.runner.num_blocks
+        self._swaps = []             # (kind, gpu block, cpu block) until the next plan
 
     # ------------------------------------------------------------------ liveness
     def dead_workers(self):
@@ -241,10 +253,33 @@ class TPExecutor:
             if dead:
                 raise RuntimeError(f"TP worker(s) {[p.pid for p in dead]} died")
 
+    # ------------------------------------------------------------------ KV swap (K14)
+    # Every rank holds its own KV shard (and PP stage layers), so swaps travel with the
+    # step plan and each rank applies them before the step's kernels (ModelRunner.run).
+    def allocate_swap(self, swap_space_gb: float) -> int:
+        return getattr(self.runner, "num_cpu_blocks", 0)
+
+    def swap_out(self, gpu_blocks, cpu_blocks) -> None:
+        self._swaps += [(0, g, c) for g, c in zip(gpu_blocks, cpu_blocks)]
+
+    def swap_in(self, cpu_blocks, gpu_blocks) -> None:
+        self._swaps += [(1, g, c) for c, g in zip(cpu_blocks, gpu_blocks)]
+
+    def copy_blocks(self, pairs) -> None:
+        self._swaps += [(2, a, b) for a, b in pairs]
+
+    def _take_swaps(self):
+        import numpy as np
+        if not self._swaps:
+            return None
+        ops, self._swaps = self._swaps, []
+        return np.asarray(ops, dtype=np.int32).reshape(-1)
+
     # ------------------------------------------------------------------ steps
     def launch(self, bm, sched, overlap: bool):
         r = self.runner
         plan = r.prepare(bm, sched)
+        plan.swap = self._take_swaps()
         h = r.launch_plan(plan, sched, overlap,
                           publish=lambda pl: self._publish(r.encode_plan(pl)))
         if r.ar_poller is not None:
@@ -287,6 +322,9 @@ class FakeExecutor:
         n = len(sched.decodes) + sum(1 for p in sched.prefills if p.samples)
         _time.sleep(self.step_s)
         return StepOutput([self._rng.randrange(3, self.vocab) for _ in range(n)], None)
+
+    def copy_blocks(self, pairs) -> None:
+        pass
 
     def shutdown(self) -> None:
         pass

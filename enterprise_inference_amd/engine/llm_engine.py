@@ -68,7 +68,7 @@ class RequestOutput:
 
 class _Request:
     __slots__ = ("request_id", "prompt", "prompt_token_ids", "params", "seqs", "arrival_time",
-                 "n", "finished_emitted")
+                 "n", "finished_emitted", "beam")
 
     def __init__(self, request_id, prompt, prompt_token_ids, params, seqs, arrival_time):
         self.request_id = request_id
@@ -79,6 +79,7 @@ class _Request:
         self.arrival_time = arrival_time
         self.n = params.n
         self.finished_emitted = False
+        self.beam = None
 
 
 @dataclasses.dataclass
@@ -99,7 +100,7 @@ class LLMEngine:
         self.executor = executor
         self.num_blocks = executor.num_blocks
         self.scheduler = Scheduler(cfg.scheduler, cfg.cache, self.num_blocks)
-        # K14 swap space (single-rank executors; TP/PP engines keep recompute preemption)
+        # K14 swap space (GPU engines, every TP/PP rank; executor.swap_enabled)
         alloc = getattr(executor, "allocate_swap", None)
         if alloc is not None and cfg.cache.swap_space_gb > 0:
             from .swap import SwapSpace
@@ -165,6 +166,10 @@ class LLMEngine:
             params = params.clone(logprobs=0)
             params.eos_ids = sorted(self.eos_ids)
         arrival = arrival_time if arrival_time is not None else time.time()
+        if params.use_beam_search:
+            self._add_beam_request(request_id, prompt, list(prompt_token_ids), params, arrival,
+                                   priority)
+            return
         mm = self._encode_images(multi_modal_data, prompt_token_ids) if multi_modal_data else None
         seqs = []
         for i in range(params.best_of):
@@ -181,6 +186,92 @@ class LLMEngine:
             self.scheduler.add(s)
         self.requests[request_id] = _Request(request_id, prompt, list(prompt_token_ids), params,
                                              seqs, arrival)
+
+    def _add_beam_request(self, request_id, prompt, prompt_ids, params, arrival, priority):
+        """Beam search: one sequence to start with (the prompt is prefilled once); it reports
+        the top-2W log-probs of every step to its BeamGroup (engine/beam_search.py)."""
+        from .beam_search import BeamGroup
+        width = max(params.best_of, params.n)
+        group = BeamGroup(request_id, len(prompt_ids), width, params.n, params.length_penalty,
+                          params.early_stopping, params.eos_ids, params.stop_token_ids,
+                          params.ignore_eos, params.max_tokens, self.cfg.scheduler.max_model_len)
+        bparams = params.clone(n=1, best_of=1, temperature=0.0, logprobs=2 * width)
+        bparams.eos_ids = params.eos_ids
+        seq = Sequence(request_id, prompt_ids, bparams, index=0, arrival_time=arrival, seed=0,
+                       priority=priority)
+        seq.beam = group
+        group.beams.append(seq)
+        self.scheduler.add(seq)
+        r = _Request(request_id, prompt, prompt_ids, params, [seq], arrival)
+        r.beam = group
+        self.requests[request_id] = r
+
+    def _beam_steps(self, groups, touched: Dict[str, "_Request"]) -> None:
+        """Advance the beam groups that reported this step (see BeamGroup.advance)."""
+        from .beam_search import fork_sequence
+        bm = self.scheduler.bm
+        copies = []
+        for g in groups:
+            r = self.requests.get(g.request_id)
+            if r is None:            # aborted meanwhile
+                g.take_partial()
+                continue
+            if not g.ready():
+                for s in g.take_partial():
+                    s.num_computed_tokens -= 1   # recompute its logits with its siblings
+                continue
+            appends, forks, dropped = g.advance()
+            now = time.time()
+            for parent, tok, lp in forks:
+                if bm.num_free_blocks() < 2:
+                    continue                   # no room to copy-on-write: drop the candidate
+                child = fork_sequence(parent)
+                bm.native.fork(parent.seq_id, child.seq_id)
+                bm._committed[child.seq_id] = bm._committed.get(parent.seq_id, 0)
+                if parent.num_computed_tokens % bm.block_size:
+                    src, dst = bm.native.cow_last(child.seq_id)
+                    if src >= 0:
+                        copies.append((src, dst))
+                self._beam_append(child, tok, lp, now)
+                self.scheduler.running.append(child)
+                g.beams.append(child)
+                r.seqs.append(child)
+            for seq, tok, lp in appends:
+                self._beam_append(seq, tok, lp, now)
+            for seq in dropped:
+                self.scheduler.finish(seq, SeqStatus.FINISHED_ABORTED)
+                g.beams.remove(seq)
+            if g.done:
+                touched[g.request_id] = r
+        if copies:
+            self.executor.copy_blocks(copies)
+
+    @staticmethod
+    def _beam_append(seq: Sequence, tok: int, lp: float, now: float) -> None:
+        seq.output_token_ids.append(tok)
+        seq.cumulative_logprob += lp
+        if seq.first_token_time is None:
+            seq.first_token_time = now
+        seq.last_token_time = now
+
+    def _emit_beam(self, r: "_Request") -> RequestOutput:
+        g = r.beam
+        comps = []
+        for i, h in enumerate(g.results()):
+            text = self.tokenizer.decode(h.tokens,
+                                         skip_special_tokens=r.params.skip_special_tokens)
+            comps.append(CompletionOutput(index=i, text=text, token_ids=list(h.tokens),
+                                          cumulative_logprob=h.cum_logprob, logprobs=None,
+                                          finish_reason=h.finish_reason,
+                                          stop_reason=h.stop_reason, new_text=text,
+                                          new_token_ids=list(h.tokens)))
+        s0 = r.seqs[0]
+        now = time.time()
+        metrics = RequestMetrics(r.arrival_time, s0.first_scheduled_time,
+                                 min((s.first_token_time for s in r.seqs if s.first_token_time),
+                                     default=None), now, now)
+        return RequestOutput(r.request_id, r.prompt, r.prompt_token_ids, comps, True, metrics,
+                             s0.num_cached_tokens)
 
     def abort_request(self, request_id: Union[str, Iterable[str]]) -> None:
         ids = [request_id] if isinstance(request_id, str) else list(request_id)
@@ -256,6 +347,7 @@ class LLMEngine:
         res = handle.result()
         now = time.time()
         self.phase_times["wait"] = self.phase_times.get("wait", 0.0) + now - tw
+        beams = set()
         for r, it in enumerate(handle.items):
             seq = it.seq
             if seq.num_pending:
@@ -264,6 +356,11 @@ class LLMEngine:
                 continue
             tok = res.tokens[r]
             lp = res.logprobs[r] if res.logprobs is not None else None
+            if seq.beam is not None:
+                seq.beam.report(seq, lp)
+                beams.add(seq.beam)
+                self.stats.num_generation_tokens += 1
+                continue
             self._append_token(seq, tok, lp, now)
             before = len(seq.output_text)
             new_text = self.detok.step(seq)
@@ -277,6 +374,8 @@ class LLMEngine:
                                       (d[2] or []) + [lp] if lp is not None else d[2])
             touched[seq.request_id] = self.requests[seq.request_id]
             self.stats.num_generation_tokens += 1
+        if beams:
+            self._beam_steps(beams, touched)
 
     def _step_sync(self) -> List[RequestOutput]:
         t0 = time.time()
@@ -302,12 +401,18 @@ class LLMEngine:
             it.num_tokens for it in sched.decodes if it.seq.is_prefill)
         deltas: Dict[int, tuple] = {}
         sample_items = sched.decodes + [p for p in sched.prefills if p.samples]
+        beams = set()
         for r, it in enumerate(sample_items):
             seq = it.seq
             if seq.finished:
                 continue
             tok = res.tokens[r]
             lp = res.logprobs[r] if res.logprobs is not None else None
+            if seq.beam is not None:
+                seq.beam.report(seq, lp)
+                beams.add(seq.beam)
+                self.stats.num_generation_tokens += 1
+                continue
             self._append_token(seq, tok, lp, now)
             before = len(seq.output_text)
             new_text = self.detok.step(seq)
@@ -316,6 +421,8 @@ class LLMEngine:
             deltas[seq.seq_id] = (new_text, [tok], [lp] if lp is not None else None)
             touched[seq.request_id] = self.requests[seq.request_id]
             self.stats.num_generation_tokens += 1
+        if beams:
+            self._beam_steps(beams, touched)
         self.stats.step_time_s += time.time() - t0
         return self._emit(touched, deltas)
 
@@ -356,6 +463,13 @@ class LLMEngine:
     def _emit(self, touched: Dict[str, _Request], deltas: Dict[int, tuple]) -> List[RequestOutput]:
         outs = []
         for rid, r in touched.items():
+            if r.beam is not None:
+                if r.beam.done and rid in self.requests:
+                    ro = self._emit_beam(r)
+                    outs.append(ro)
+                    self.requests.pop(rid, None)
+                    self.finished_log.append(ro)
+                continue
             finished = all(s.finished for s in r.seqs)
             seqs = r.seqs
             if finished and r.params.best_of > r.params.n:

@@ -67,12 +67,12 @@ class StepPlan:
     the staging bytes (``ModelRunner.encode_plan``) -- no pickling on the step path."""
 
     __slots__ = ("kind", "Bp", "nd", "T", "npf", "mb_d", "mb_p", "n_work", "n_lidx", "P", "off",
-                 "src", "n_sample", "unfiltered", "sharded", "o", "mm")
+                 "src", "n_sample", "unfiltered", "sharded", "o", "mm", "swap")
 
     def __init__(self, kind: str, **kw):
         self.kind = kind
         for k in self.__slots__[1:]:
-            setattr(self, k, kw.get(k, {} if k == "o" else (None if k == "mm" else 0)))
+            setattr(self, k, kw.get(k, {} if k == "o" else (None if k in ("mm", "swap") else 0)))
 
     def __getitem__(self, k):           # plan["nd"] style access
         return getattr(self, k)
@@ -88,6 +88,7 @@ class StepPlan:
         for i, n in enumerate(_O_NAMES):
             h[16 + i] = self.o.get(n, -1)
         h[27] = int(bool(self.sharded))
+        h[28] = 0 if self.swap is None else len(self.swap)
         return h
 
     @classmethod
@@ -100,6 +101,7 @@ class StepPlan:
                 n_sample=int(h[13]), unfiltered=bool(h[14]), sharded=bool(h[27]))
         if p.kind == "eager":
             p.o = {n: int(h[16 + i]) for i, n in enumerate(_O_NAMES)}
+        p.swap = int(h[28])          # word count; load_message replaces it with the words
         return p, int(h[15])
 
 
@@ -358,13 +360,15 @@ class ModelRunner:
             self.head_dim * self.kv_buf.element_size()
 
     def allocate_swap(self, num_cpu_blocks: int) -> int:
-        """Pinned host mirror of the KV layout, [layers, 2, cpu_blocks, block elems]."""
+        """Pinned host swap space, block-major [cpu_blocks, layers, 2, block elems]: every
+        swapped block is ONE contiguous host range, so a swap is a device gather + one async
+        DMA per block (no host-side scatter, no synchronisation, no re-pinning)."""
         self.num_cpu_blocks = int(num_cpu_blocks)
         if self.num_cpu_blocks <= 0:
             self.swap_buf = None
             return 0
         L, blk = self.num_local_layers, self.kv_buf.shape[2] // self.num_blocks
-        self.swap_buf = torch.empty(L, 2, self.num_cpu_blocks, blk, dtype=self.kv_buf.dtype,
+        self.swap_buf = torch.empty(self.num_cpu_blocks, L, 2, blk, dtype=self.kv_buf.dtype,
                                     pin_memory=self.is_gpu)
         logger.info("KV swap space: %d blocks (%.1f GiB pinned)", self.num_cpu_blocks,
                     self.swap_buf.numel() * self.swap_buf.element_size() / 2**30)
@@ -374,22 +378,61 @@ class ModelRunner:
         return self.kv_buf.view(self.kv_buf.shape[0], 2, self.num_blocks, -1)
 
     def swap_out(self, gpu_blocks: List[int], cpu_blocks: List[int]) -> None:
-        """Device blocks -> pinned host blocks (after the in-flight step on this stream)."""
+        """Device blocks -> pinned host blocks, stream-ordered after the in-flight step that
+        wrote them; the host never waits (nothing on the host reads swapped data)."""
         if not gpu_blocks:
             return
-        g = torch.tensor(gpu_blocks, dtype=torch.long, device=self.device)
-        data = self._kv_blocks().index_select(2, g).cpu()    # waits for the writers
-        self.swap_buf[:, :, torch.tensor(cpu_blocks, dtype=torch.long)] = data
+        g = torch.tensor(gpu_blocks, dtype=torch.long).to(self.device, non_blocking=True)
+        # [L, 2, n, blk] -> block-major [n, L, 2, blk] on the device, then one DMA per block
+        data = self._kv_blocks().index_select(2, g).permute(2, 0, 1, 3).contiguous()
+        # `data` may be freed right after: the caching allocator only hands its memory to
+        # later work on this same stream, i.e. after these copies
+        for i, c in enumerate(cpu_blocks):
+            self.swap_buf[c].copy_(data[i], non_blocking=True)
 
     def swap_in(self, cpu_blocks: List[int], gpu_blocks: List[int]) -> None:
         """Pinned host blocks -> device blocks, ahead of the step that reads them."""
         if not gpu_blocks:
             return
-        data = self.swap_buf[:, :, torch.tensor(cpu_blocks, dtype=torch.long)]
-        if self.is_gpu:
-            data = data.pin_memory().to(self.device, non_blocking=True)
-        g = torch.tensor(gpu_blocks, dtype=torch.long, device=self.device)
-        self._kv_blocks().index_copy_(2, g, data)
+        L, blk = self.swap_buf.shape[1], self.swap_buf.shape[3]
+        data = torch.empty(len(cpu_blocks), L, 2, blk, dtype=self.kv_buf.dtype,
+                           device=self.device)
+        for i, c in enumerate(cpu_blocks):
+            data[i].copy_(self.swap_buf[c], non_blocking=True)
+        g = torch.tensor(gpu_blocks, dtype=torch.long).to(self.device, non_blocking=True)
+        self._kv_blocks().index_copy_(2, g, data.permute(1, 2, 0, 3))
+
+    def apply_swaps(self, swap: Optional[np.ndarray]) -> None:
+        """Swaps carried by a step plan (TP/PP: every rank moves its own KV shard), in the
+        order the scheduler issued them: [kind, gpu_block, cpu_block] * n (kind 0 = out,
+        1 = in, 2 = device copy gpu_block -> block in the third word); runs of one kind are
+        batched into one gather / scatter."""
+        if swap is None or len(swap) == 0:
+            return
+        ops = np.asarray(swap).reshape(-1, 3)
+        i = 0
+        while i < len(ops):
+            j = i
+            while j < len(ops) and ops[j, 0] == ops[i, 0]:
+                j += 1
+            g, c = ops[i:j, 1].tolist(), ops[i:j, 2].tolist()
+            if ops[i, 0] == 0:
+                self.swap_out(g, c)
+            elif ops[i, 0] == 1:
+                self.swap_in(c, g)
+            else:                       # 2: device block copy (beam fork copy-on-write)
+                self.copy_blocks(list(zip(g, c)))
+            i = j
+
+    def copy_blocks(self, pairs) -> None:
+        """KV block src -> dst on every local layer (K and V), stream-ordered before the next
+        step: the copy-on-write of a forked beam's partially filled last block (K14)."""
+        if not pairs or getattr(self, "kv_buf", None) is None:
+            return
+        src = torch.tensor([p[0] for p in pairs], dtype=torch.long).to(self.device)
+        dst = torch.tensor([p[1] for p in pairs], dtype=torch.long).to(self.device)
+        kb = self._kv_blocks()
+        kb.index_copy_(2, dst, kb.index_select(2, src))
 
     # ------------------------------------------------------------------ inputs
     def _decode_partitions(self, B: int, max_len: int) -> int:
@@ -554,7 +597,10 @@ class ModelRunner:
         plan.n_sample = len(items)
         if items:
             plan.unfiltered = self._fill_sampling(items)
-            plan.sharded = self.sharded_lm and plan.unfiltered and not any(
+            # vocab-sharded sampling for every row the host does not post-process: unfiltered
+            # rows race per shard, filtered rows get their global thresholds from a few tiny
+            # exchanges (ops/shard_sampling.py) -- no B x V logit gather either way
+            plan.sharded = self.sharded_lm and not any(
                 needs_host_processing(it.seq) for it in items)
         return plan
 
@@ -591,8 +637,11 @@ class ModelRunner:
         return views
 
     def encode_plan(self, plan: StepPlan) -> bytes:
-        """Wire message for TP workers: 32-word header + staging bytes (one copy)."""
+        """Wire message for TP workers: 32-word header + staging bytes (+ the step's KV swap
+        lists) in one copy."""
         views = self._staging_words(plan)
+        if plan.swap is not None and len(plan.swap):
+            views = views + [plan.swap]
         return b"".join([plan.header(sum(v.size for v in views)).tobytes()] +
                         [v.tobytes() for v in views])
 
@@ -605,12 +654,17 @@ class ModelRunner:
         for v in self._staging_words(plan):
             v[:] = a[pos:pos + v.size]
             pos += v.size
+        nsw = plan.swap
+        plan.swap = a[pos:pos + nsw].copy() if nsw else None
+        pos += nsw
         if pos != _HDR_WORDS + nwords:
             raise RuntimeError("step plan payload size mismatch")
         return plan
 
     def run(self, plan: StepPlan) -> Optional[torch.Tensor]:
         """Device side of a step (every TP rank): returns logits of the sampling rows."""
+        if plan.swap is not None:
+            self.apply_swaps(plan.swap)     # before the step's kernels, on the step stream
         if plan["kind"] == "graph":
             Bp = plan["Bp"]
             self._upload_graph(Bp)
@@ -710,13 +764,23 @@ class ModelRunner:
         temp, top_k, top_p, min_p, seeds = self._sampling_tensors(n)
         if self.sharded_lm and not full:
             if plan.sharded:
-                local = logits[:, :self.lm_valid].float()
-                v, i = sampling_ops.sample_shard(local, temp, seeds, self.lm_offset)
                 from ..parallel import comm
-                pair = torch.cat([v, i.view(torch.float32)])[None, :]
-                g = comm.all_gather(pair, 0)                     # [W, 2n]
-                toks = sampling_ops.merge_shard_winners(g[:, :n],
-                                                        g[:, n:].contiguous().view(torch.int32))
+                local = logits[:, :self.lm_valid].float()
+                if plan.unfiltered:
+                    v, i = sampling_ops.sample_shard(local, temp, seeds, self.lm_offset)
+                    pair = torch.cat([v, i.view(torch.float32)])[None, :]
+                    g = comm.all_gather(pair, 0)                     # [W, 2n]
+                    toks = sampling_ops.merge_shard_winners(
+                        g[:, :n], g[:, n:].contiguous().view(torch.int32))
+                else:
+                    from ..ops import shard_sampling as ss
+                    S = self.max_num_seqs
+                    f = self.s_f32.numpy()
+                    kmax, any_p, any_m = ss.host_filter_facts(
+                        self.s_i32.numpy()[:n], f[S:S + n], f[2 * S:2 * S + n], f[:n], self.vocab)
+                    gen = ss.filtered_shard_sample(local, temp, top_k, top_p, min_p, seeds,
+                                                   self.lm_offset, self.vocab, kmax, any_p, any_m)
+                    toks = ss.run_spmd(gen, lambda t: comm.all_gather(t[None], 0))
                 self.d_tok[:n].copy_(toks)
                 return self.d_tok[:n]
             logits = self.gather_logits(logits)
@@ -734,7 +798,11 @@ class ModelRunner:
                plan: StepPlan) -> StepOutput:
         from .logits_process import apply_logits_processors
 
-        if self.sharded_lm and not plan.sharded:
+        if plan.sharded:
+            # no host processing on these rows: the same vocab-sharded sampler (and the same
+            # collectives) the TP workers run in replay()
+            return StepOutput(self._sample_tokens(logits, items, plan).tolist(), None)
+        if self.sharded_lm:
             logits = self.gather_logits(logits)
         logits = apply_logits_processors(logits, items)
         toks = self._sample_tokens(logits, items, plan, full=True)

@@ -35,6 +35,10 @@ class SamplingParams:
     guided_regex: Optional[str] = None
     guided_json: Optional[object] = None
     guided_grammar: Optional[str] = None
+    # beam search (width = best_of), vLLM semantics (engine/beam_search.py)
+    use_beam_search: bool = False
+    length_penalty: float = 1.0
+    early_stopping: bool = False
 
     def __post_init__(self) -> None:
         if isinstance(self.stop, str):
@@ -71,6 +75,14 @@ class SamplingParams:
             raise ValueError("min_tokens must be >= 0")
         if self.logprobs is not None and self.logprobs < 0:
             raise ValueError("logprobs must be non-negative")
+        if self.use_beam_search:
+            if self.temperature > 1e-5:
+                raise ValueError("beam search requires temperature 0")
+            if self.top_p < 1.0 or self.top_k not in (-1,) or self.min_p > 0.0:
+                raise ValueError("beam search does not combine with top_p / top_k / min_p")
+            if self.needs_penalties or self.guided_choice or self.guided_regex or \
+                    self.guided_json is not None or self.guided_grammar:
+                raise ValueError("beam search does not combine with penalties or guided decoding")
 
     @property
     def greedy(self) -> bool:

@@ -19,7 +19,7 @@ def needs_host_processing(seq: "Sequence") -> bool:
     p = seq.params
     return (p.needs_penalties or p.needs_logit_processing or p.logprobs is not None
             or p.prompt_logprobs is not None or seq.guided_state is not None
-            or p.best_of > p.n)
+            or p.best_of > p.n or seq.beam is not None)
 
 
 class SeqStatus(enum.Enum):
@@ -53,7 +53,7 @@ class Sequence:
                  "detok_offset", "output_text", "prefix_offset", "read_offset", "lora",
                  "num_preemptions", "seed", "guided_state", "swap_blocks", "mm_embeds",
                  "mm_positions", "cache_salt", "token_times", "priority",
-                 "num_pending")
+                 "num_pending", "beam")
 
     def __init__(self, request_id: str, prompt_token_ids: List[int], params: SamplingParams,
                  index: int = 0, arrival_time: Optional[float] = None, seed: int = 0,
@@ -93,6 +93,7 @@ class Sequence:
         # tokens sampled by a launched, not yet read-back step (overlapped scheduling): they
         # count toward num_tokens so the next step can be planned before the values are known
         self.num_pending = 0
+        self.beam = None               # engine.beam_search.BeamGroup of a beam-search request
 
     @property
     def num_tokens(self) -> int:

@@ -120,9 +120,15 @@ class _SamplingFields(OpenAIBase):
         if self.guided_grammar:
             from ...engine.fsm import grammar_to_regex
             grammar_to_regex(self.guided_grammar)      # reject unsupported grammars with a 400
-        if self.use_beam_search:
-            raise ValueError("use_beam_search is not supported; use best_of/n sampling")
         max_tokens = self.max_tokens if self.max_tokens is not None else default_max_tokens
+        if self.use_beam_search:
+            # beam search ranks candidates by log-prob: deterministic, unfiltered rows (an
+            # explicit non-zero temperature / top_p / top_k is a client error)
+            if self.temperature not in (None, 0.0):
+                raise ValueError("use_beam_search requires temperature 0")
+            temperature = 0.0
+            top_p = 1.0 if self.top_p is None else top_p
+            top_k = -1 if self.top_k is None else top_k
         return SamplingParams(
             n=self.n or 1, best_of=self.best_of, temperature=temperature, top_p=top_p,
             top_k=top_k, min_p=self.min_p if self.min_p is not None else gd.get("min_p", 0.0),
@@ -140,7 +146,8 @@ class _SamplingFields(OpenAIBase):
             allowed_token_ids=self.allowed_token_ids,
             guided_choice=self.guided_choice, guided_regex=self.guided_regex,
             guided_grammar=self.guided_grammar,
-            guided_json=guided_json)
+            guided_json=guided_json, use_beam_search=self.use_beam_search,
+            length_penalty=self.length_penalty, early_stopping=self.early_stopping)
 
 
 class ChatCompletionRequest(_SamplingFields):

@@ -419,7 +419,10 @@ async def create_chat_completion(req: ChatCompletionRequest, ctx: ServingContext
     if images:
         if req.truncate_prompt_tokens:
             raise RequestError("truncate_prompt_tokens cannot be combined with image inputs")
-        text, ids, mm = _expand_images(ctx, prompt, images, add_special)
+        # download / decode / tile on a worker thread: a slow image URL must not stall the
+        # event loop that feeds every other SSE stream and /health
+        import asyncio
+        text, ids, mm = await asyncio.to_thread(_expand_images, ctx, prompt, images, add_special)
         _, ids = ctx.tokenize_prompt(ids)
     else:
         text, ids = ctx.tokenize_prompt(prompt, add_special, req.truncate_prompt_tokens)

@@ -24,6 +24,7 @@ from __future__ import annotations
 
 import base64
 import io
+import os
 import math
 from typing import List, Optional, Sequence, Tuple
 
@@ -58,22 +59,87 @@ def best_fit_canvas(h: int, w: int, max_tiles: int, tile: int = TILE) -> Tuple[i
     return min(best, key=lambda c: c[0] * c[1])
 
 
+MAX_IMAGE_BYTES = int(os.environ.get("EIA_MAX_IMAGE_BYTES", 20 << 20))
+MAX_IMAGE_PIXELS = int(os.environ.get("EIA_MAX_IMAGE_PIXELS", 64 << 20))
+
+
+def _remote_media_policy():
+    """(enabled, allowed domains or None, private addresses allowed) from the environment:
+    EIA_DISABLE_REMOTE_MEDIA=1 turns http(s) image URLs off, EIA_ALLOWED_MEDIA_DOMAINS
+    (comma list) restricts the hosts (vLLM's --allowed-media-domains), and loopback /
+    private / link-local targets are refused unless EIA_ALLOW_PRIVATE_MEDIA=1 (the server
+    must not become a proxy into the cluster network)."""
+    off = os.environ.get("EIA_DISABLE_REMOTE_MEDIA", "0") not in ("0", "", "false")
+    doms = [d.strip().lower() for d in os.environ.get("EIA_ALLOWED_MEDIA_DOMAINS", "").split(",")
+            if d.strip()]
+    priv = os.environ.get("EIA_ALLOW_PRIVATE_MEDIA", "0") not in ("0", "", "false")
+    return not off, (doms or None), priv
+
+
+def _check_url(url: str) -> None:
+    import ipaddress
+    import socket
+    from urllib.parse import urlparse
+
+    enabled, domains, allow_private = _remote_media_policy()
+    if not enabled:
+        raise ValueError("remote image URLs are disabled on this server")
+    host = (urlparse(url).hostname or "").lower()
+    if not host:
+        raise ValueError("image URL has no host")
+    if domains is not None and not any(host == d or host.endswith("." + d) for d in domains):
+        raise ValueError(f"image host {host!r} is not in the allowed media domains")
+    if not allow_private:
+        for info in socket.getaddrinfo(host, None):
+            ip = ipaddress.ip_address(info[4][0])
+            if ip.is_private or ip.is_loopback or ip.is_link_local or ip.is_reserved:
+                raise ValueError(f"image host {host!r} resolves to a non-public address")
+
+
+def fetch_image_bytes(url: str, max_bytes: Optional[int] = None, timeout: float = 30.0) -> bytes:
+    """Download an image URL with the media policy above and a byte cap (streamed: a huge or
+    endless body is cut off at ``max_bytes`` instead of being buffered).  Redirects are
+    followed by hand so every hop passes the same checks."""
+    import httpx
+
+    cap = MAX_IMAGE_BYTES if max_bytes is None else max_bytes
+    for _ in range(5):
+        _check_url(url)
+        with httpx.stream("GET", url, timeout=timeout, follow_redirects=False) as r:
+            if r.is_redirect:
+                url = str(r.next_request.url) if r.next_request else r.headers["location"]
+                continue
+            r.raise_for_status()
+            n = int(r.headers.get("content-length") or 0)
+            if n > cap:
+                raise ValueError(f"image is {n} bytes (limit {cap})")
+            buf = bytearray()
+            for chunk in r.iter_bytes():
+                buf += chunk
+                if len(buf) > cap:
+                    raise ValueError(f"image exceeds {cap} bytes")
+            return bytes(buf)
+    raise ValueError("too many redirects")
+
+
 def load_image(src) -> "object":
-    """PIL image from a PIL image, raw bytes, a data: URL or a local path."""
+    """PIL image from a PIL image, raw bytes, a data: URL, an http(s) URL or a local path.
+    Decompression bombs are refused (``EIA_MAX_IMAGE_PIXELS``)."""
     from PIL import Image
 
+    Image.MAX_IMAGE_PIXELS = MAX_IMAGE_PIXELS
     if hasattr(src, "convert"):
         return src.convert("RGB")
     if isinstance(src, (bytes, bytearray)):
         return Image.open(io.BytesIO(src)).convert("RGB")
     s = str(src)
     if s.startswith("data:"):
-        return Image.open(io.BytesIO(base64.b64decode(s.split(",", 1)[1]))).convert("RGB")
+        data = base64.b64decode(s.split(",", 1)[1])
+        if len(data) > MAX_IMAGE_BYTES:
+            raise ValueError(f"image exceeds {MAX_IMAGE_BYTES} bytes")
+        return Image.open(io.BytesIO(data)).convert("RGB")
     if s.startswith(("http://", "https://")):
-        import httpx
-        r = httpx.get(s, timeout=30.0, follow_redirects=True)
-        r.raise_for_status()
-        return Image.open(io.BytesIO(r.content)).convert("RGB")
+        return Image.open(io.BytesIO(fetch_image_bytes(s))).convert("RGB")
     return Image.open(s).convert("RGB")
 
 

@@ -148,7 +148,8 @@ def _fused_moe_grouped(x, w13, w2, topk_w, topk_ids, e_lo, e_hi, mfma: bool = Fa
 def _align(topk_ids, El, e_lo, e_hi, n, dev, st):
     E_total = max(e_hi, int(El + e_lo))
     offs = torch.empty(El + 1, dtype=torch.int32, device=dev)
-    row_idx = torch.empty(max(1, n), dtype=torch.int32, device=dev)
+    # zero-filled: with expert parallelism the align kernel writes only the local rows
+    row_idx = torch.zeros(max(1, n), dtype=torch.int32, device=dev)
     inv = torch.empty(max(1, n), dtype=torch.int32, device=dev)
     check(lib().eia_moe_align(ptr(topk_ids), n, E_total, e_lo, e_hi, ptr(offs), ptr(row_idx),
                               ptr(inv), topk_ids.shape[1], st), "moe_align")
@@ -167,8 +168,10 @@ def _fused_moe_sorted_blas(x, w13, w2, topk_w, topk_ids, e_lo, e_hi, act):
     dev = x.device
     st = stream(x)
     offs, row_idx, inv = _align(topk_ids, El, e_lo, e_hi, n, dev, st)
-    xs = x.index_select(0, row_idx[:n].long())
     bounds = offs.tolist()                     # the one host synchronisation of this layer
+    # expert parallelism: only the first bounds[El] sorted rows belong to local experts (the
+    # rest of row_idx is never written by the align kernel)
+    xs = x.index_select(0, row_idx[:bounds[El]].long())
     h2 = torch.empty(max(1, n), H, dtype=x.dtype, device=dev)
     for e in range(El):
         a, b = bounds[e], bounds[e + 1]

@@ -76,19 +76,29 @@ def sample_reference(logits: torch.Tensor, temperature: torch.Tensor, top_k: tor
 SPLIT_CHUNK = 4096     # tokens per workgroup of the split-row sampler
 
 
+def f2key_t(x: torch.Tensor) -> torch.Tensor:
+    """Order-preserving uint32 key of fp32 values (as int64), bit-identical to f2key()."""
+    u = x.float().contiguous().view(torch.int32).to(torch.int64) & 0xFFFFFFFF
+    return torch.where(u >= 0x80000000, (~u) & 0xFFFFFFFF, u | 0x80000000)
+
+
 def sample_shard(logits: torch.Tensor, temperature: torch.Tensor, seeds: torch.Tensor,
-                 vocab_offset: int):
-    """Unfiltered sampling restricted to one tensor-parallel vocab shard.
+                 vocab_offset: int, floor_keys: Optional[torch.Tensor] = None):
+    """Sampling restricted to one tensor-parallel vocab shard.
 
     logits fp32 [B, V_shard] hold global ids vocab_offset..; returns (value fp32 [B], global
     id int32 [B]) of the shard's Gumbel-max winner (greedy rows: the plain max).  The max over
-    shards (lowest id on ties) equals ``sample(full_logits, ..., unfiltered=True)``."""
+    shards (lowest id on ties) equals ``sample(full_logits, ...)``: unfiltered rows directly,
+    filtered rows with ``floor_keys`` [B] (int64 holding uint32 keys: the admissible-set
+    threshold computed over ALL shards by ops/shard_sampling.py)."""
     B, V = logits.shape
     if not use_hip(logits):
         l = logits.float()
         t = temperature.float()
         tt = torch.where(t > 0, t, torch.ones_like(t))
         g = l / tt[:, None] - torch.log(-torch.log(uniform_t(seeds, V, vocab_offset)))
+        if floor_keys is not None:
+            g = g.masked_fill(f2key_t(l) < floor_keys.to(torch.int64)[:, None], float("-inf"))
         v = torch.where((t > 0)[:, None], g, l)
         best_v, best_i = v.max(-1)          # first max = lowest id on ties
         return best_v, (best_i + vocab_offset).to(torch.int32)
@@ -97,10 +107,40 @@ def sample_shard(logits: torch.Tensor, temperature: torch.Tensor, seeds: torch.T
     ws = torch.empty(2 * B * C, dtype=torch.int32, device=logits.device)
     out_v = torch.empty(B, dtype=torch.float32, device=logits.device)
     out_i = torch.empty(B, dtype=torch.int32, device=logits.device)
+    fk = None
+    if floor_keys is not None:
+        require(floor_keys.numel() >= B and floor_keys.is_cuda, "sample_shard: floor keys")
+        fk = floor_keys.to(torch.int64).to(torch.int32).contiguous()     # uint32 bit pattern
     check(lib().eia_sample_shard(ptr(logits), logits.stride(0), B, V, SPLIT_CHUNK, vocab_offset,
                                  ptr(temperature), ptr(seeds), ptr(ws), ws.data_ptr() + 4 * B * C,
-                                 ptr(out_v), ptr(out_i), stream(logits)), "sample_shard")
+                                 ptr(out_v), ptr(out_i), None if fk is None else ptr(fk),
+                                 stream(logits)), "sample_shard")
     return out_v, out_i
+
+
+def radix_hist(logits: torch.Tensor, row_max: torch.Tensor, temperature: torch.Tensor,
+               floor_key: torch.Tensor, prefix: torch.Tensor, pmask: torch.Tensor,
+               shift: int) -> torch.Tensor:
+    """[B, 256] fp32 mass histogram of one radix round over this shard (see
+    radix_hist_kernel); key tensors are int64 holding uint32 values."""
+    B, V = logits.shape
+    if not use_hip(logits):
+        l = logits.float()
+        k = f2key_t(l)
+        t = temperature.float()
+        ok = (k >= floor_key[:, None]) & ((k & pmask[:, None]) == prefix[:, None]) & \
+            (t > 0)[:, None]
+        tt = torch.where(t > 0, t, torch.ones_like(t))
+        w = torch.exp((l - row_max[:, None]) / tt[:, None]).masked_fill(~ok, 0.0)
+        h = torch.zeros(B, 256, dtype=torch.float32, device=logits.device)
+        return h.scatter_add_(1, (k >> shift) & 0xFF, w)
+    require(logits.dtype == torch.float32 and logits.stride(-1) == 1, "radix_hist: fp32")
+    out = torch.empty(B, 256, dtype=torch.float32, device=logits.device)
+    i32 = [x.to(torch.int32).contiguous() for x in (floor_key, prefix, pmask)]
+    check(lib().eia_radix_hist(ptr(logits), logits.stride(0), B, V, ptr(row_max.float().contiguous()),
+                               ptr(temperature), ptr(i32[0]), ptr(i32[1]), ptr(i32[2]), shift,
+                               ptr(out), stream(logits)), "radix_hist")
+    return out
 
 
 def merge_shard_winners(vals: torch.Tensor, ids: torch.Tensor) -> torch.Tensor:

@@ -65,7 +65,7 @@ def test_engine_greedy_matches_fp32_oracle(arch):
                            params=SamplingParams(max_tokens=8, temperature=0, ignore_eos=True,
                                                  logprobs=5))
     lstats = check_logprobs(hf, lp_prompts, [o.outputs[0].token_ids for o in lp_outs],
-                            [o.outputs[0].logprobs for o in lp_outs], tol=0.05)
+                            [o.outputs[0].logprobs for o in lp_outs], tol=0.1)
     print(arch, lstats)
 
 

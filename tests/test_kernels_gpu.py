@@ -378,6 +378,45 @@ def test_sample_shard_merge_equals_full_row(B, V, W):
     assert got.cpu().tolist() == full.cpu().tolist()
 
 
+@pytest.mark.parametrize("B,V,W", [(65, 128256, 8), (33, 32000, 4), (17, 4097, 2)])
+def test_filtered_shard_sampling_equals_full_kernel(B, V, W):
+    """C4 with top-k / top-p / min-p: W vocab shards run ops/shard_sampling.py in lockstep
+    (radix_hist kernel + floor-keyed shard race on the GPU, exchanges simulated by stacking)
+    and pick the token of the full-row sample_kernel with the same seeds.  Rows whose only
+    filters are top-k / min-p are exact; the top-p threshold sums fp32 mass in a different
+    order than the kernel's LDS atomics, so a row may differ only at the nucleus boundary."""
+    from enterprise_inference_amd.ops import sampling, shard_sampling as ss
+    torch.manual_seed(B + V)
+    logits = torch.randn(B, V, device=DEV) * 3
+    temp = torch.rand(B, device=DEV) * 1.5 + 0.1
+    temp[::9] = 0.0
+    top_k = torch.randint(0, 100, (B,), dtype=torch.int32, device=DEV)
+    top_k[1::3] = 0
+    top_p = torch.where(torch.rand(B, device=DEV) < 0.6, torch.rand(B, device=DEV) * 0.9 + 0.05,
+                        torch.ones(B, device=DEV))
+    min_p = torch.where(torch.rand(B, device=DEV) < 0.3, torch.rand(B, device=DEV) * 0.2,
+                        torch.zeros(B, device=DEV))
+    seeds = torch.tensor([sampling.row_seed(11 + i, i) for i in range(B)], dtype=torch.int64,
+                         device=DEV)
+    full = sampling.sample(logits, temp, top_k, top_p, min_p, seeds).cpu()
+    cpu_ref = sampling.sample_reference(logits.cpu(), temp.cpu(), top_k.cpu(), top_p.cpu(),
+                                        min_p.cpu(), seeds.cpu())
+    per = (V + W - 1) // W
+    kmax, any_p, any_m = ss.host_filter_facts(top_k.cpu().numpy(), top_p.cpu().numpy(),
+                                              min_p.cpu().numpy(), temp.cpu().numpy(), V)
+    gens = [ss.filtered_shard_sample(logits[:, r * per:min(V, (r + 1) * per)].contiguous(), temp,
+                                     top_k, top_p, min_p, seeds, r * per, V, kmax, any_p, any_m)
+            for r in range(W)]
+    outs = ss.run_simulated(gens)
+    for o in outs[1:]:
+        assert torch.equal(o, outs[0])
+    got = outs[0].cpu()
+    no_p = (top_p.cpu() >= 1.0) | (temp.cpu() <= 0)
+    assert torch.equal(got[no_p], full[no_p])
+    assert torch.equal(got[no_p], cpu_ref[no_p])
+    assert (got == full).float().mean().item() >= 0.95, (got.tolist(), full.tolist())
+
+
 def test_fill_ids():
     from enterprise_inference_amd.ops import sampling
     ids = torch.tensor([5, 6, 7, 8, 9], dtype=torch.int32, device=DEV)

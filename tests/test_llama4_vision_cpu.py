@@ -174,3 +174,98 @@ def test_openai_chat_image_parts(tmp_path):
             assert junk.status_code == 400
     finally:
         aeng.shutdown()
+
+
+def _serve_bytes(payload: bytes, delay: float = 0.0):
+    """Local HTTP server returning `payload` for every GET; returns (url, stop)."""
+    import http.server
+    import threading
+    import time as _t
+
+    class H(http.server.BaseHTTPRequestHandler):
+        def do_GET(self):
+            _t.sleep(delay)
+            self.send_response(200)
+            self.send_header("Content-Type", "image/png")
+            self.end_headers()
+            self.wfile.write(payload)
+
+        def log_message(self, *a):
+            pass
+
+    srv = http.server.ThreadingHTTPServer(("127.0.0.1", 0), H)
+    threading.Thread(target=srv.serve_forever, daemon=True).start()
+    return f"http://127.0.0.1:{srv.server_address[1]}/img.png", srv.shutdown
+
+
+def test_remote_image_policy(monkeypatch):
+    """http(s) image URLs: private/loopback targets refused by default (no SSRF into the
+    cluster), domain allowlist, a streamed byte cap, and an off switch."""
+    import base64
+
+    from enterprise_inference_amd.models import llama4_vision as lv
+    png = base64.b64decode(_png_data_url().split(",", 1)[1])
+    url, stop = _serve_bytes(png)
+    try:
+        with pytest.raises(ValueError, match="non-public"):
+            lv.fetch_image_bytes(url)
+        monkeypatch.setenv("EIA_ALLOW_PRIVATE_MEDIA", "1")
+        assert lv.fetch_image_bytes(url) == png
+        assert lv.load_image(url).size[0] > 0
+        with pytest.raises(ValueError, match="exceeds"):
+            lv.fetch_image_bytes(url, max_bytes=len(png) // 2)
+        monkeypatch.setenv("EIA_ALLOWED_MEDIA_DOMAINS", "images.example.com")
+        with pytest.raises(ValueError, match="allowed media domains"):
+            lv.fetch_image_bytes(url)
+        monkeypatch.setenv("EIA_DISABLE_REMOTE_MEDIA", "1")
+        with pytest.raises(ValueError, match="disabled"):
+            lv.fetch_image_bytes(url)
+    finally:
+        stop()
+
+
+def test_slow_image_url_does_not_block_event_loop(monkeypatch):
+    """The image download runs on a worker thread: while one request waits 1.5 s on a slow
+    image URL, the event loop keeps serving other coroutines."""
+    import asyncio
+    import time as _t
+
+    from enterprise_inference_amd.entrypoints.openai import serving
+
+    calls = []
+
+    def slow_expand(ctx, prompt, images, add_special):
+        _t.sleep(1.5)
+        calls.append(1)
+        raise serving.RequestError("done")
+
+    monkeypatch.setattr(serving, "_expand_images", slow_expand)
+
+    class Ctx:
+        model = "m"
+        chat_template = None
+        tokenizer = None
+
+        def check_model(self, m):
+            pass
+
+    monkeypatch.setattr(serving, "apply_chat_template", lambda *a, **k: "prompt")
+    req = serving.ChatCompletionRequest(model="m", messages=[{"role": "user", "content": [
+        {"type": "image_url", "image_url": {"url": "http://slow.example.com/x.png"}}]}])
+
+    async def main():
+        ticks = 0
+
+        async def ticker():
+            nonlocal ticks
+            while not calls:
+                await asyncio.sleep(0.05)
+                ticks += 1
+
+        t = asyncio.create_task(ticker())
+        with pytest.raises(serving.RequestError):
+            await serving.create_chat_completion(req, Ctx())
+        await t
+        return ticks
+
+    assert asyncio.run(main()) >= 10

@@ -134,3 +134,24 @@ def test_fused_route_matches_linear_plus_topk(T, E, k, H, scoring):
     same = (s1 == s2).all(-1)
     assert same.float().mean() > 0.97            # bf16 logit ties may flip a rare token
     assert torch.allclose(w1.gather(1, o1)[same], w2.gather(1, o2)[same], atol=2e-2)
+
+
+def test_sorted_blas_expert_parallel_after_poisoned_allocator():
+    """EP ranks own [e_lo, e_hi): the align kernel writes only the local rows of its sorted
+    list.  With the caching allocator handing back memory full of garbage, the long-prompt
+    regime must still read only those rows (this faulted the GPU in the TP=2 Mixtral test)."""
+    from enterprise_inference_amd.ops import moe
+    torch.manual_seed(4)
+    T, E, k, H, I = 600, 4, 2, 512, 256
+    x = torch.randn(T, H, device=DEV, dtype=BF)
+    w13 = (torch.randn(E, 2 * I, H, device=DEV) * H ** -0.5).to(BF)
+    w2 = (torch.randn(E, H, I, device=DEV) * I ** -0.5).to(BF)
+    w, ids = moe.topk_route(torch.randn(T, E, device=DEV), k, True)
+    full = moe._fused_moe_sorted_blas(x, w13, w2, w, ids, 0, E, "silu").float()
+    part = 0
+    for r in range(2):
+        junk = torch.full((1 << 20,), 0x7FFFFFF0, dtype=torch.int32, device=DEV)
+        del junk                                 # next int32 allocations reuse this block
+        part = part + moe._fused_moe_sorted_blas(x, w13[2 * r:2 * r + 2], w2[2 * r:2 * r + 2],
+                                                 w, ids, 2 * r, 2 * r + 2, "silu").float()
+    assert (full - part).abs().max() < 5e-2

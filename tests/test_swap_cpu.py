@@ -2,22 +2,33 @@
 space and resume from them; greedy tokens equal an unpressured run (and the recompute
 path), the swap metrics move, and aborting a swapped request frees its host blocks."""
 
+import pytest
 import torch
 
-from enterprise_inference_amd.config import CacheConfig, EngineConfig, ModelConfig, SchedulerConfig
+from enterprise_inference_amd.config import (CacheConfig, EngineConfig, ModelConfig,
+                                             ParallelConfig, SchedulerConfig)
 from enterprise_inference_amd.engine.llm_engine import LLMEngine
 from enterprise_inference_amd.engine.sampling_params import SamplingParams
 from enterprise_inference_amd.models.catalog import tiny_config
 
 
-def _engine(blocks, swap_gb):
+@pytest.fixture(autouse=True)
+def _cpu_swap(monkeypatch):
+    # CPU engines keep recompute preemption in production (their KV already lives in host
+    # memory); the swap machinery itself is exercised here with EIA_CPU_SWAP=1
+    monkeypatch.setenv("EIA_CPU_SWAP", "1")
+
+
+def _engine(blocks, swap_gb, tp=1, path=None):
     d = tiny_config("LlamaForCausalLM", vocab_size=320)
-    cfg = EngineConfig(model=ModelConfig.from_hf_dict(d),
+    cfg = EngineConfig(model=ModelConfig.from_hf_dict(d), model_path=path,
                        cache=CacheConfig(block_size=16, num_gpu_blocks=blocks,
                                          swap_space_gb=swap_gb, enable_prefix_caching=False),
                        scheduler=SchedulerConfig(max_num_seqs=8, max_num_batched_tokens=64,
                                                  max_model_len=256),
-                       device="cpu", dtype=torch.float32, load_format="dummy")
+                       parallel=ParallelConfig(tensor_parallel_size=tp),
+                       device="cpu", dtype=torch.float32,
+                       load_format="dummy" if path is None else "auto")
     return LLMEngine(cfg)
 
 
@@ -61,3 +72,43 @@ def test_abort_swapped_request_frees_host_blocks():
     while eng.has_unfinished_requests():
         eng.step()
     assert eng.scheduler.swap.usage() == 0.0
+
+
+def test_cpu_engine_has_no_swap_pool_by_default(monkeypatch):
+    monkeypatch.delenv("EIA_CPU_SWAP")
+    eng = _engine(24, 4)
+    assert eng.scheduler.swap is None
+    assert getattr(eng.executor.runner, "swap_buf", None) is None
+
+
+def test_tp2_swap_matches_tp1(tmp_path):
+    """TP=2 under block pressure: the swap lists travel in the step plan and every rank
+    swaps its own KV shard; tokens equal the unpressured TP=1 run and the swap gauges move."""
+    import json
+
+    import transformers
+    from safetensors.torch import save_file
+
+    from enterprise_inference_amd.parallel import state
+    d = tiny_config("LlamaForCausalLM", vocab_size=320)
+    hc = transformers.LlamaConfig(**{k: v for k, v in d.items() if k != "architectures"})
+    torch.manual_seed(0)
+    hf = transformers.LlamaForCausalLM(hc).eval()
+    save_file({k: v.contiguous() for k, v in hf.state_dict().items()},
+              str(tmp_path / "model.safetensors"))
+    (tmp_path / "config.json").write_text(json.dumps(d))
+    ref = [o.outputs[0].token_ids for o in _engine(256, 0, path=str(tmp_path)).generate(
+        prompt_token_ids=PROMPTS, params=PARAMS)]
+    eng = _engine(24, 0.01, tp=2, path=str(tmp_path))
+    try:
+        assert eng.scheduler.swap is not None and eng.scheduler.swap.num_blocks > 0
+        got = [o.outputs[0].token_ids for o in eng.generate(prompt_token_ids=PROMPTS,
+                                                             params=PARAMS)]
+        assert eng.scheduler.num_swapouts > 0, "the pressured run must swap"
+        assert got == ref
+        from enterprise_inference_amd.metrics import EngineMetrics
+        snap = EngineMetrics.engine_snapshot(eng, 0.0)
+        assert len(snap) > 0
+    finally:
+        eng.shutdown()
+        state.destroy_distributed()

@@ -30,18 +30,19 @@ def _ckpt(tmp_path, d):
     return str(tmp_path)
 
 
-def _run(path, d, tp, ep=False, pp=1, temperature=0.0):
+def _run(path, d, tp, ep=False, pp=1, temperature=0.0, delayed=True, **sp):
     cfg = EngineConfig(model=ModelConfig.from_hf_dict(d), model_path=path,
                        cache=CacheConfig(block_size=16, num_gpu_blocks=64),
                        scheduler=SchedulerConfig(max_num_seqs=4, max_num_batched_tokens=40,
-                                                 max_model_len=256),
+                                                 max_model_len=256, delayed_sampling=delayed),
                        parallel=ParallelConfig(tensor_parallel_size=tp, enable_expert_parallel=ep,
                                                pipeline_parallel_size=pp),
                        device="cpu", dtype=torch.float32)
     eng = LLMEngine(cfg)
     try:
         prompts = [[5, 6, 7, 8, 9, 10] * 8, [11, 12, 13], list(range(40, 90))]
-        params = SamplingParams(max_tokens=6, temperature=temperature, ignore_eos=True, seed=11)
+        params = SamplingParams(max_tokens=6, temperature=temperature, ignore_eos=True, seed=11,
+                                **sp)
         outs = eng.generate(prompt_token_ids=prompts, params=params)
         return [o.outputs[0].token_ids for o in outs]
     finally:
@@ -104,3 +105,28 @@ def test_tp2_gemm_allreduce_overlap_matches_tp1(tmp_path, monkeypatch):
     monkeypatch.setenv("EIA_TP_OVERLAP_MIN_TOKENS", "8")
     got = _run(path, d, 2)
     assert got == ref
+
+
+FILTERS = dict(top_p=0.9, top_k=50, min_p=0.05)
+
+
+@pytest.mark.parametrize("tp,filters", [(2, FILTERS), (4, FILTERS), (2, {"top_p": 0.7}),
+                                        (2, {"top_k": 7}), (4, {"min_p": 0.2})])
+def test_tp_filtered_sampling_matches_tp1(tmp_path, tp, filters):
+    """top-k / top-p / min-p rows on the vocab-sharded LM head: global thresholds from the
+    shard exchanges (ops/shard_sampling.py), no full-logit gather; tokens equal the TP=1
+    full-row sampler with the same seeds."""
+    d = tiny_config("LlamaForCausalLM")
+    path = _ckpt(tmp_path, d)
+    ref = _run(path, d, 1, temperature=0.8, **filters)
+    assert _run(path, d, tp, temperature=0.8, **filters) == ref
+
+
+def test_tp2_sync_mode_sharded_sampling(tmp_path):
+    """Without overlapped scheduling the driver samples through ModelRunner.sample(): it must
+    take the same sharded path (and collectives) as the workers."""
+    d = tiny_config("LlamaForCausalLM")
+    path = _ckpt(tmp_path, d)
+    ref = _run(path, d, 1, temperature=0.8, delayed=False, **FILTERS)
+    assert _run(path, d, 2, temperature=0.8, delayed=False, **FILTERS) == ref
+    assert _run(path, d, 2, temperature=0.8, delayed=False) == _run(path, d, 1, temperature=0.8)

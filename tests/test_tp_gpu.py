@@ -46,7 +46,9 @@ def _ckpt(tmp_path, d):
     return hf, str(tmp_path)
 
 
-TOL = 0.12      # init std 0.05 (2.5x the e2e tests'): logits and bf16 rounding scale with it
+# init std 0.05 (2.5x the e2e tests'): logits, and their bf16 rounding, scale with the init
+# and sqrt(hidden); a token may trail the oracle's best by 10 % of the row's logit std
+TOL, REL = 0.08, 0.1
 
 
 def _generate(path, d, tp, ep=False, temperature=0.0, logprobs=None):
@@ -85,11 +87,11 @@ def test_tp_llama_70b_rank_layout_matches_oracle(tmp_path, tp):
     d = tiny_config("LlamaForCausalLM", **SHAPES[tp])
     hf, path = _ckpt(tmp_path, d)
     prompts, got = _generate(path, d, tp)
-    stats = check_greedy(hf, prompts, got, tol=TOL)
+    stats = check_greedy(hf, prompts, got, tol=TOL, rel=REL)
     assert stats["argmax_agreement"] > 0.8, stats
     # logits-level bound on the gathered (vocab-sharded) rows through the logprobs path
     p2, got2, lps = _generate(path, d, tp, logprobs=5)
-    check_logprobs(hf, p2, got2, lps, tol=0.08)
+    check_logprobs(hf, p2, got2, lps, tol=0.25)   # O(1) nats for a real sharding bug
     _, ref = _generate(path, d, 1)
     same = sum(a == b for x, y in zip(got, ref) for a, b in zip(x, y)) / sum(map(len, ref))
     assert same > 0.8, (got, ref)
@@ -103,7 +105,9 @@ def test_tp2_mixtral_expert_parallel_matches_oracle(tmp_path, monkeypatch, dispa
                                              "num_experts_per_tok": 2})
     hf, path = _ckpt(tmp_path, d)
     prompts, got = _generate(path, d, 2, ep=True)
-    stats = check_greedy(hf, prompts, got, tol=TOL)
+    # top-2 routing is discrete: a bf16-level near-tie between two experts' router logits
+    # flips the expert set of a token, so MoE rows get a wider logit bound
+    stats = check_greedy(hf, prompts, got, tol=TOL, rel=2.5 * REL)
     assert stats["argmax_agreement"] > 0.8, stats
 
 
