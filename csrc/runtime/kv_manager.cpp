@@ -290,7 +290,8 @@ class KVCacheManager {
 
 }  // namespace
 
-void register_shm(py::module_& m);   // shm_ring.cpp
+void register_shm(py::module_& m);       // shm_ring.cpp
+void register_grammar(py::module_& m);   // grammar.cpp
 
 PYBIND11_MODULE(_eia_runtime, m) {
   m.doc() = "MI355X inference runtime: native KV block manager, batch builder, shm broadcast";
@@ -318,4 +319,5 @@ PYBIND11_MODULE(_eia_runtime, m) {
       .def("check_invariants", &KVCacheManager::check_invariants)
       .def("stats", &KVCacheManager::stats);
   register_shm(m);
+  register_grammar(m);
 }

@@ -12,7 +12,8 @@ pattern; its mask lives on the device as a bool row, so masking a guided row is 
 
 ``grammar_to_regex`` accepts the regular (non-recursive) subset of GBNF / Lark-style EBNF
 grammars (``guided_grammar``): rules of literals, character classes, /regex/ terminals, rule
-references, grouping, alternation and ``* + ?``; a recursive rule is rejected.
+references, grouping, alternation and ``* + ?``; recursive grammars (nested JSON, expression
+languages) are context-free and run on the pushdown matcher of engine/grammar.py instead.
 """
 
 from __future__ import annotations
@@ -484,43 +485,18 @@ def _lit_regex(body: str) -> str:
 
 
 def grammar_to_regex(grammar: str) -> str:
-    """Regular subset of GBNF (``name ::= ...``) / Lark EBNF (``name: ...``) -> one regex."""
-    toks = _lex(grammar)
-    rules: Dict[str, list] = {}
-    order: List[str] = []
-    i = 0
-    while i < len(toks):
-        if toks[i][1] == "?" and i + 1 < len(toks) and toks[i + 1][0] == "name":
-            i += 1                                 # Lark's inline-rule marker (?start:)
-        kind, val = toks[i]
-        if kind != "name" or i + 1 >= len(toks) or toks[i + 1][1] not in ("::=", ":"):
-            raise ValueError(f"grammar: expected 'name ::=' or 'name:' at {val!r}")
-        name = val.lstrip("?")
-        j = i + 2
-        body = []
-        depth = 0
-        while j < len(toks):
-            k2, v2 = toks[j]
-            if depth == 0 and k2 == "name" and j + 1 < len(toks) and toks[j + 1][1] in ("::=", ":"):
-                break
-            if (depth == 0 and v2 == "?" and j + 2 < len(toks) and toks[j + 1][0] == "name"
-                    and toks[j + 2][1] in ("::=", ":")):
-                break
-            depth += v2 == "("
-            depth -= v2 == ")"
-            body.append(toks[j])
-            j += 1
-        rules[name] = body
-        order.append(name)
-        i = j
+    """Regular subset of GBNF (``name ::= ...``) / Lark EBNF (``name: ...``) -> one regex.
+    Recursive grammars raise here; engine/guided.py routes them to engine/grammar.py."""
+    from .grammar import split_rules
+    rules, order = split_rules(grammar)
     entry = next((n for n in ("root", "start") if n in rules), order[0] if order else None)
     if entry is None:
         raise ValueError("grammar: no rules")
 
     def expand(name: str, stack: Tuple[str, ...]) -> str:
         if name in stack:
-            raise ValueError(f"grammar: rule {name!r} is recursive; only regular grammars are "
-                             "supported (use guided_json / guided_regex)")
+            raise ValueError(f"grammar: rule {name!r} is recursive; such grammars run on the "
+                             "pushdown matcher (engine/grammar.py)")
         parts = []
         for kind, val in rules[name]:
             if kind in ("str", "sq"):

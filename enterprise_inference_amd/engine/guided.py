@@ -12,8 +12,9 @@ engine/logits_process.py):
   process by walking the vocabulary trie -- shared by every request with the same pattern;
 * json    -> a JSON-schema subset compiled to a regex (objects with typed properties,
   enums, arrays, nested objects; ``{}`` = any flat JSON object), then as regex;
-* grammar -> the regular subset of GBNF / Lark EBNF (``guided_grammar``) compiled to a
-  regex (engine/fsm.py grammar_to_regex); recursive grammars are rejected.
+* grammar -> GBNF / Lark EBNF (``guided_grammar``): a regular grammar compiles to a regex
+  (engine/fsm.py grammar_to_regex) and runs as regex; a recursive one runs on the native
+  pushdown matcher (engine/grammar.py, csrc/runtime/grammar.cpp).
 """
 
 from __future__ import annotations
@@ -176,5 +177,8 @@ def make_guided_state(params, tokenizer, vocab_size: int) -> GuidedState:
         return RegexState(params.guided_regex, tokenizer, vocab_size, eos)
     if getattr(params, "guided_grammar", None):
         from .fsm import grammar_to_regex
+        from .grammar import GrammarState, is_recursive
+        if is_recursive(params.guided_grammar):
+            return GrammarState(params.guided_grammar, tokenizer, vocab_size, eos)
         return RegexState(grammar_to_regex(params.guided_grammar), tokenizer, vocab_size, eos)
     return RegexState(schema_to_regex(params.guided_json), tokenizer, vocab_size, eos)

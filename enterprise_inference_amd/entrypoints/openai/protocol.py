@@ -118,8 +118,8 @@ class _SamplingFields(OpenAIBase):
             elif guided_json is None:
                 guided_json = {}
         if self.guided_grammar:
-            from ...engine.fsm import grammar_to_regex
-            grammar_to_regex(self.guided_grammar)      # reject unsupported grammars with a 400
+            from ...engine.grammar import validate_grammar
+            validate_grammar(self.guided_grammar)      # reject unsupported grammars with a 400
         max_tokens = self.max_tokens if self.max_tokens is not None else default_max_tokens
         if self.use_beam_search:
             # beam search ranks candidates by log-prob: deterministic, unfiltered rows (an
