@@ -8,9 +8,12 @@ native pushdown matcher (csrc/runtime/grammar.cpp) tracks the set of parser stac
   * a stack is a list of (rule, alternative, position) frames; its top always points at a
     character-class terminal (rule references are expanded, finished alternatives popped),
   * a character advances every stack whose top class matches it,
+  * stack sets are interned and (set, character) transitions cached, so the matcher is a
+    lazily built automaton whose states are stack sets, shared by every request using the
+    grammar (a JSON string body loops on one state),
   * a token is allowed when walking its characters keeps at least one stack alive -- found
-    for the whole vocabulary by one walk of the shared vocabulary trie with the stack set
-    (shared prefixes stepped once, dead branches pruned), memoised per stack set,
+    for the whole vocabulary by one walk of the vocabulary trie from the state (shared
+    prefixes stepped once, dead branches pruned), cached per state, with its device mask,
   * EOS is allowed when some stack is empty (the start rule is complete).
 
 Repetition (``* + ? {m,n}``) and groups become helper rules; string literals become class
@@ -323,8 +326,13 @@ def native_grammar(text: str):
     return g
 
 
+_DEV_MASKS: "OrderedDict[tuple, object]" = OrderedDict()
+
+
 class GrammarState:
-    """Per-sequence pushdown state (engine/guided.py GuidedState interface)."""
+    """Per-sequence pushdown state (engine/guided.py GuidedState interface).  The automaton
+    behind it is shared by every request with the same grammar text, and so are the device
+    masks of its states (no host->device copy for a state seen before)."""
 
     def __init__(self, text: str, tokenizer, vocab_size: int, eos_ids: List[int]):
         from .. import _native
@@ -333,22 +341,36 @@ class GrammarState:
         self.m = _native.runtime().GrammarMatcher(self.grammar, self.vocab)
         self.eos = sorted(set(e for e in eos_ids if e is not None and 0 <= e < vocab_size))
         self.done = False
-        self._masks: "OrderedDict[tuple, object]" = OrderedDict()
+
+    def _host_mask(self, vocab: int):
+        import numpy as np
+        m = self.m.mask()
+        out = np.zeros(vocab, dtype=np.bool_)
+        n = min(vocab, m.shape[0])
+        out[:n] = m[:n].astype(np.bool_)
+        if self.m.accepting() or not out.any():
+            e = [t for t in self.eos if t < vocab]
+            out[e] = True
+        return out
 
     def allowed_tokens(self) -> List[int]:
-        ids = list(self.m.allowed())
-        if self.m.accepting():
-            ids += self.eos
-        return sorted(set(ids)) if ids else list(self.eos)
+        import numpy as np
+        return np.nonzero(self._host_mask(max(self.vocab.size, 1 + max(self.eos, default=0))))[0].tolist()
 
     def allowed_mask(self, device, vocab: int):
         import torch
-        ids = self.allowed_tokens()
-        m = torch.zeros(vocab, dtype=torch.bool)
-        if ids:
-            t = torch.tensor(ids, dtype=torch.long)
-            m[t[t < vocab]] = True
-        return m.to(device)
+        key = (id(self.grammar), id(self.vocab), self.m.state(), str(device), vocab)
+        with _lock:
+            hit = _DEV_MASKS.get(key)
+            if hit is not None and hit[0] is self.grammar:
+                _DEV_MASKS.move_to_end(key)
+                return hit[1]
+        t = torch.from_numpy(self._host_mask(vocab)).to(device)
+        with _lock:
+            _DEV_MASKS[key] = (self.grammar, t)
+            while len(_DEV_MASKS) > 256:
+                _DEV_MASKS.popitem(last=False)
+        return t
 
     def advance(self, token: int) -> None:
         if token in self.eos:
