@@ -199,8 +199,10 @@ def split_rules(text: str) -> Tuple[Dict[str, list], List[str]]:
             k2, v2 = toks[j]
             if depth == 0 and k2 == "name" and j + 1 < len(toks) and toks[j + 1][1] in ("::=", ":"):
                 break
+            # Lark's inline-rule marker (``?name:``); before ``name ::=`` a ``?`` is the
+            # optional operator of the previous GBNF rule's last item
             if (depth == 0 and v2 == "?" and j + 2 < len(toks) and toks[j + 1][0] == "name"
-                    and toks[j + 2][1] in ("::=", ":")):
+                    and toks[j + 2][1] == ":"):
                 break
             depth += v2 == "("
             depth -= v2 == ")"

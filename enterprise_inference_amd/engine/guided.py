@@ -11,7 +11,9 @@ engine/logits_process.py):
   determinised lazily, and each DFA state's allowed-token set / mask is computed once per
   process by walking the vocabulary trie -- shared by every request with the same pattern;
 * json    -> a JSON-schema subset compiled to a regex (objects with typed properties,
-  enums, arrays, nested objects; ``{}`` = any flat JSON object), then as regex;
+  enums, arrays, nested objects), then as regex; free-form objects (``{}``, json_object mode)
+  and ``$ref`` schemas (recursive definitions) compile to a grammar instead
+  (``schema_to_grammar``) and run on the pushdown matcher at any nesting depth;
 * grammar -> GBNF / Lark EBNF (``guided_grammar``): a regular grammar compiles to a regex
   (engine/fsm.py grammar_to_regex) and runs as regex; a recursive one runs on the native
   pushdown matcher (engine/grammar.py, csrc/runtime/grammar.cpp).
@@ -86,6 +88,114 @@ def schema_to_regex(schema, depth: int = 0) -> str:
             parts.append(f"{sep}{kv}" if name in required else f"(?:{sep}{kv})?")
         return r"\{" + _WS + "".join(parts) + _WS + r"\}"
     return _SCALAR
+
+
+_G_COMMON = r"""
+ws ::= [ \t\n]? [ \t\n]?
+string ::= /"(?:[^"\\\x00-\x1f]|\\["\\bfnrt\x2f]|\\u[0-9a-fA-F]{4})*"/
+number ::= /-?(?:0|[1-9][0-9]*)(?:\.[0-9]+)?(?:[eE][+-]?[0-9]+)?/
+integer ::= /-?(?:0|[1-9][0-9]*)/
+boolean ::= "true" | "false"
+null ::= "null"
+value ::= object | array | string | number | boolean | null
+object ::= "{" ws (string ws ":" ws value (ws "," ws string ws ":" ws value)*)? ws "}"
+array ::= "[" ws (value (ws "," ws value)*)? ws "]"
+"""
+
+
+def _walk_schema(schema):
+    if isinstance(schema, dict):
+        yield schema
+        for v in schema.values():
+            yield from _walk_schema(v)
+    elif isinstance(schema, list):
+        for v in schema:
+            yield from _walk_schema(v)
+
+
+def schema_needs_grammar(schema) -> bool:
+    """A schema the bounded regex cannot express: ``$ref`` (possibly recursive definitions)
+    or a free-form object / value (any nesting depth)."""
+    if isinstance(schema, str):
+        schema = json.loads(schema)
+    if schema is None or schema is True or schema == {}:
+        return True
+    for d in _walk_schema(schema):
+        if "$ref" in d:
+            return True
+        if d.get("type") == "object" and not d.get("properties"):
+            return True
+    return False
+
+
+def schema_to_grammar(schema) -> str:
+    """JSON schema -> GBNF over the JSON token rules above; ``$ref`` to ``#/$defs/X`` /
+    ``#/definitions/X`` becomes a rule reference, so recursive schemas stay exact.  Property
+    order / required / enum / const / anyOf / type-list semantics match ``schema_to_regex``."""
+    if isinstance(schema, str):
+        schema = json.loads(schema)
+    root = schema if isinstance(schema, dict) else {}
+    defs = {**root.get("definitions", {}), **root.get("$defs", {})}
+    rules: List[str] = []
+    named: Dict[str, str] = {}
+
+    def lit(v) -> str:
+        return json.dumps(json.dumps(v, ensure_ascii=False), ensure_ascii=False)
+
+    def ref(path: str) -> str:
+        name = path.rsplit("/", 1)[-1]
+        if path in ("#", "#/"):
+            key, sub = "root_schema", root
+        elif name in defs:
+            key, sub = "def_" + "".join(c if c.isalnum() else "_" for c in name), defs[name]
+        else:
+            raise ValueError(f"guided_json: unresolvable $ref {path!r}")
+        if key not in named:
+            named[key] = ""                        # reserve before recursing
+            named[key] = emit(sub)
+            rules.append(f"{key} ::= {named[key]}")
+        return key
+
+    def emit(sc) -> str:
+        if sc is None or sc is True or sc == {}:
+            return "value"
+        if "$ref" in sc:
+            return ref(sc["$ref"])
+        if "enum" in sc:
+            return "(" + " | ".join(lit(v) for v in sc["enum"]) + ")"
+        if "const" in sc:
+            return lit(sc["const"])
+        for key in ("anyOf", "oneOf"):
+            if key in sc:
+                return "(" + " | ".join(emit(x) for x in sc[key]) + ")"
+        t = sc.get("type")
+        if isinstance(t, list):
+            return "(" + " | ".join(emit({**sc, "type": x}) for x in t) + ")"
+        if t == "string":
+            if "pattern" in sc:
+                pat = sc["pattern"].lstrip("^").rstrip("$").replace("/", "\\x2f")
+                return '"\\"" /' + pat + '/ "\\""'
+            return "string"
+        if t in ("number", "integer", "boolean", "null"):
+            return t
+        if t == "array":
+            item = emit(sc.get("items", {}))
+            return f'"[" ws ({item} (ws "," ws {item})*)? ws "]"'
+        if t == "object" or "properties" in sc:
+            props = sc.get("properties", {})
+            if not props:
+                return "object"
+            required = set(sc.get("required", list(props)))
+            parts = []
+            for i, (name, sub) in enumerate(props.items()):
+                kv = f'{lit(name)} ws ":" ws {emit(sub)}'
+                sep = "" if i == 0 else 'ws "," ws '
+                parts.append(f"{sep}{kv}" if name in required else f"({sep}{kv})?")
+            return '"{" ws ' + " ".join(parts) + ' ws "}"'
+        return "value"
+
+    body = emit(schema)
+    return "\n".join([f"root ::= {body}"] + rules) + _G_COMMON
 
 
 class GuidedState:
@@ -181,4 +291,7 @@ def make_guided_state(params, tokenizer, vocab_size: int) -> GuidedState:
         if is_recursive(params.guided_grammar):
             return GrammarState(params.guided_grammar, tokenizer, vocab_size, eos)
         return RegexState(grammar_to_regex(params.guided_grammar), tokenizer, vocab_size, eos)
+    if schema_needs_grammar(params.guided_json):
+        from .grammar import GrammarState
+        return GrammarState(schema_to_grammar(params.guided_json), tokenizer, vocab_size, eos)
     return RegexState(schema_to_regex(params.guided_json), tokenizer, vocab_size, eos)

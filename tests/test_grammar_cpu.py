@@ -188,3 +188,63 @@ def test_engine_recursive_grammar_outputs_parse():
             assert oracle.accepts(c.text), c.text
         else:
             assert oracle.viable(c.text), c.text
+
+
+TREE = {"$defs": {"node": {"type": "object", "properties": {
+    "v": {"type": "integer"}, "kids": {"type": "array", "items": {"$ref": "#/$defs/node"}}},
+    "required": ["v", "kids"]}}, "$ref": "#/$defs/node"}
+
+
+def _accepts_text(grammar, text):
+    m = _matcher(grammar, [])
+    return m.advance_text([ord(c) for c in text]) and m.accepting()
+
+
+def test_schema_to_grammar_recursive_and_free_form():
+    import json
+    from enterprise_inference_amd.engine.guided import schema_needs_grammar, schema_to_grammar
+    assert schema_needs_grammar(TREE) and schema_needs_grammar({})
+    assert not schema_needs_grammar({"type": "object", "properties": {"a": {"type": "integer"}}})
+    g = schema_to_grammar(TREE)
+    deep = {"v": 1, "kids": [{"v": 2, "kids": []}]}
+    for _ in range(8):                                   # nesting far past the regex bound
+        deep = {"v": 0, "kids": [deep, {"v": -3, "kids": []}]}
+    assert _accepts_text(g, json.dumps(deep))
+    assert _accepts_text(g, json.dumps(deep, separators=(",", ":")))
+    assert not _accepts_text(g, json.dumps({"v": "x", "kids": []}))
+    assert not _accepts_text(g, json.dumps({"kids": [], "v": 1}))     # property order kept
+    free = schema_to_grammar({})
+    doc = {"a": [1, 2.5e3, {"b": {"c": [True, None, {"d": "e\\né"}]}}], "f": "g"}
+    assert _accepts_text(free, json.dumps(doc))
+    assert _accepts_text(free, json.dumps(doc, ensure_ascii=False))
+    assert not _accepts_text(free, '{"a": [1,]}')
+    enum = schema_to_grammar({"type": "object", "properties": {
+        "k": {"enum": ["x\"y", 3]}, "r": {"$ref": "#"}}, "required": ["k"]})
+    assert _accepts_text(enum, '{"k": "x\\"y", "r": {"k": 3}}')
+
+
+def test_engine_recursive_json_schema_outputs_parse():
+    import json
+    from enterprise_inference_amd.config import (CacheConfig, EngineConfig, ModelConfig,
+                                                 SchedulerConfig)
+    from enterprise_inference_amd.engine.guided import schema_to_grammar
+    from enterprise_inference_amd.engine.llm_engine import LLMEngine
+    from enterprise_inference_amd.engine.sampling_params import SamplingParams
+    from enterprise_inference_amd.models.catalog import tiny_config
+
+    d = tiny_config("LlamaForCausalLM", vocab_size=300)
+    cfg = EngineConfig(model=ModelConfig.from_hf_dict(d), cache=CacheConfig(block_size=16,
+                       num_gpu_blocks=64), scheduler=SchedulerConfig(max_num_seqs=8,
+                       max_num_batched_tokens=256, max_model_len=256), device="cpu",
+                       dtype=torch.float32, load_format="dummy")
+    eng = LLMEngine(cfg)
+    g = schema_to_grammar(TREE)
+    outs = eng.generate(prompts=["tree:", "t"], params=SamplingParams(
+        max_tokens=60, temperature=0.7, seed=3, guided_json=TREE))
+    for o in outs:
+        c = o.outputs[0]
+        m = _matcher(g, [])
+        assert m.advance_text([ord(ch) for ch in c.text]), c.text
+        if c.finish_reason == "stop":
+            assert m.accepting()
+            assert "v" in json.loads(c.text)
