@@ -624,6 +624,283 @@ paged_decode_reduce_kernel(const float* __restrict__ part_o, const float* __rest
   }
 }
 
+// Unit loop of one wave that owns a whole (partition of a) context: NS register sets of K/V
+// rotate so NS-1 units stay in flight while one is multiplied (the wave has no siblings to hide
+// its load latency), and the partition's block-table entries are read once up front into a
+// lane-indexed register (readlane per unit) instead of one dependent scalar load per unit.
+template <int D, int NS, typename Pre>
+EIA_DEV void attn_units_deep(WaveAcc<D>& acc, const bf16x8 (&qs)[D / 32][64],
+                             const bf16_t* __restrict__ kc, const bf16_t* __restrict__ vc,
+                             const int* __restrict__ bt, int ub, int ue, int L, int kvh, int Hkv,
+                             int bs, float scale_log2, int kv_lo, Pre&& pre, int tnew,
+                             const bf16_t* knew, const bf16_t* vnew) {
+  if (ub >= ue) {
+    pre();
+    return;
+  }
+  const int lane = threadIdx.x & 63;
+  const int c = lane & 15, g = lane >> 4;
+  const long hk = (long)bs * D;
+  const unsigned koff = (unsigned)(((8 * (c >> 2) + (c & 3)) * D + 8 * g) * 2);
+  const unsigned voff = (unsigned)((8 * g + c * bs) * 2);
+  const int upb = bs / 32;                           // units per block
+  int wbase = __builtin_amdgcn_readfirstlane(ub / upb);   // first block of the lane window
+  const int blast = (ue - 1) / upb;
+  int wblk = (wbase + lane <= blast) ? bt[wbase + lane] : 0;
+  auto block_of = [&](int uu) -> int {
+    const int bi = uu / upb;
+    if (bi - wbase >= 64) {                          // wave-uniform: slide the window
+      wbase = bi;
+      wblk = (wbase + lane <= blast) ? bt[wbase + lane] : 0;
+    }
+    return __builtin_amdgcn_readlane(wblk, bi - wbase);
+  };
+  // named register sets (an indexed array of them is demoted to scratch by hipcc)
+  bf16x8 ak0[D / 32], ak1[D / 32], av[D / 16], bk0[D / 32], bk1[D / 32], bv[D / 16];
+  bf16x8 ck0[D / 32], ck1[D / 32], cv[D / 16], dk0[D / 32], dk1[D / 32], dv[D / 16];
+  auto load = [&](bf16x8 (&k0)[D / 32], bf16x8 (&k1)[D / 32], bf16x8 (&v)[D / 16], int uu) {
+    const int blk = block_of(uu);
+    const long base = ((long)blk * Hkv + kvh) * hk;
+    const int o = (32 * uu) % bs;
+    const char* kb = reinterpret_cast<const char*>(kc + base + (long)o * D);
+    const char* vb = reinterpret_cast<const char*>(vc + base + o);
+#pragma unroll
+    for (int s = 0; s < D / 32; ++s) {
+      k0[s] = *reinterpret_cast<const bf16x8*>(kb + koff + 64 * s);
+      k1[s] = *reinterpret_cast<const bf16x8*>(kb + koff + 8 * D + 64 * s);
+    }
+#pragma unroll
+    for (int dt = 0; dt < D / 16; ++dt)
+      v[dt] = *reinterpret_cast<const bf16x8*>(vb + (long)dt * 32 * bs + voff);
+  };
+  auto patch = [&](bf16x8 (&k0)[D / 32], bf16x8 (&k1)[D / 32], bf16x8 (&v)[D / 16], int uc) {
+    const int o = tnew - 32 * uc;
+    if (o < 0 || o >= 32) return;
+    const int tr0 = 8 * (c >> 2) + (c & 3);
+    if (tr0 == o || tr0 + 4 == o) {
+#pragma unroll
+      for (int s2 = 0; s2 < D / 32; ++s2) {
+        const bf16x8 kn = *reinterpret_cast<const bf16x8*>(knew + 8 * g + 32 * s2);
+        if (tr0 == o) k0[s2] = kn; else k1[s2] = kn;
+      }
+    }
+    if (g == (o >> 3)) {
+#pragma unroll
+      for (int dt = 0; dt < D / 16; ++dt) {
+        const bf16_t xv = vnew[16 * dt + c];
+#pragma unroll
+        for (int j = 0; j < 8; ++j)
+          if (j == (o & 7)) v[dt][j] = xv;
+      }
+    }
+  };
+  auto step = [&](bf16x8 (&k0)[D / 32], bf16x8 (&k1)[D / 32], bf16x8 (&v)[D / 16],
+                  bf16x8 (&nk0)[D / 32], bf16x8 (&nk1)[D / 32], bf16x8 (&nv)[D / 16], int uc) {
+    load(nk0, nk1, nv, min(uc + NS - 1, ue - 1));    // clamped: static vmcnt accounting
+    __builtin_amdgcn_sched_barrier(0);
+    patch(k0, k1, v, uc);
+    f32x4 s0, s1;
+    {
+      bf16x8 qf[D / 32];
+#pragma unroll
+      for (int s = 0; s < D / 32; ++s) qf[s] = qs[s][lane];
+      qk_unit<D>(s0, s1, qf, k0, k1);
+    }
+    softmax_pv<D>(acc, s0, s1, v, 32 * uc, L, scale_log2, 0x7fffffff, kv_lo);
+    __builtin_amdgcn_sched_barrier(0);
+  };
+  static_assert(NS == 3 || NS == 4, "wave decode pipeline: 3 or 4 register sets");
+  load(ak0, ak1, av, ub);
+  load(bk0, bk1, bv, min(ub + 1, ue - 1));
+  if constexpr (NS == 4) load(ck0, ck1, cv, min(ub + 2, ue - 1));
+  pre();
+  int u = ub;
+  if constexpr (NS == 4) {
+    for (;;) {
+      step(ak0, ak1, av, dk0, dk1, dv, u);
+      if (++u >= ue) return;
+      step(bk0, bk1, bv, ak0, ak1, av, u);
+      if (++u >= ue) return;
+      step(ck0, ck1, cv, bk0, bk1, bv, u);
+      if (++u >= ue) return;
+      step(dk0, dk1, dv, ck0, ck1, cv, u);
+      if (++u >= ue) return;
+    }
+  } else {
+    for (;;) {
+      step(ak0, ak1, av, ck0, ck1, cv, u);
+      if (++u >= ue) return;
+      step(bk0, bk1, bv, ak0, ak1, av, u);
+      if (++u >= ue) return;
+      step(ck0, ck1, cv, bk0, bk1, bv, u);
+      if (++u >= ue) return;
+    }
+  }
+}
+
+// ------------------------------------------------------------------- decode, one wave per item
+// Wave form: every (sequence, KV head, partition) is ONE 64-thread workgroup that walks all of
+// its 32-token units itself (next unit in flight while the current one is multiplied) and
+// normalises its own output -- no cross-wave LDS merge, no workgroup barrier after the
+// prologue.  The 4-wave form splits a short context (ctx 192 = 6 units) over four waves that
+// each see 1-2 units: every wave then pays the full load latency once or twice and the
+// workgroup a 34 KB LDS merge, and co-resident workgroups contend for issue slots
+// (profiles/pmc_decode_attn_r2.md: SQ_WAIT_INST_ANY 43 % of wave cycles at B = 65).  Here the
+// per-unit latency is pipelined along the wave's own unit stream and B * Hkv * P independent
+// waves spread over the CUs.  FUSED: the K4 prologue (split-K reduce / bias / qk-norm / RoPE /
+// KV write, q into LDS) runs on the wave's 64 lanes, D/16 lanes per head row.
+#ifndef EIA_WAVE_NS
+#define EIA_WAVE_NS 3      // K/V register sets of the wave form (NS-1 units in flight)
+#endif
+
+template <int D, bool FUSED, bool SPLIT, bool QK_NORM, bool HAS_BIAS>
+__global__ void __launch_bounds__(64, 2)
+paged_decode_wave_kernel(const bf16_t* __restrict__ q, long q_stride, const bf16_t* kc,
+                         const bf16_t* vc, const int* __restrict__ block_tables, int bt_stride,
+                         const int* __restrict__ seq_lens, bf16_t* __restrict__ out,
+                         long out_stride, float* __restrict__ part_o, float* __restrict__ part_ml,
+                         int* __restrict__ part_cnt, float scale_log2, int Hq, int Hkv, int bs,
+                         int Pmax, int sliding_window, int chunk_size,
+                         const int* __restrict__ p_dyn, DecodeRope rope) {
+  __shared__ bf16x8 qs[D / 32][64];
+  __shared__ __align__(16) bf16_t knew[D], vnew[D];
+  __shared__ int s_last;
+  const int b = blockIdx.x, kvh = blockIdx.y, p = blockIdx.z;
+  const int P = p_dyn != nullptr ? max(1, min(*p_dyn, Pmax)) : Pmax;
+  if (p >= P) return;
+  const int nq = Hq / Hkv;             // <= 16 (host-checked)
+  const int hq0 = kvh * nq;
+  const int L = seq_lens[b];
+  const int lane = threadIdx.x;
+  const int c = lane & 15, g = lane >> 4;
+  WaveAcc<D> acc;
+  wave_acc_init(acc);
+  int kv_lo = 0;
+  if (L > 0 && sliding_window > 0) kv_lo = max(kv_lo, L - sliding_window);
+  if (L > 0 && chunk_size > 0) kv_lo = max(kv_lo, ((L - 1) / chunk_size) * chunk_size);
+  const int U0 = kv_lo / 32;
+  const int U = (L + 31) / 32 - U0;
+  const int A0 = U0 & ~1;
+  const int npair = (U0 + U - A0 + 1) / 2;
+  const int ub = max(U0, A0 + 2 * (int)(((long)p * npair) / P));
+  const int ue = min(U0 + U, A0 + 2 * (int)(((long)(p + 1) * npair) / P));
+  const int* bt = block_tables + (long)b * bt_stride;
+  if constexpr (FUSED) {
+    constexpr int TPH = D / 16;                 // lanes per head row
+    constexpr int RPP = 64 / TPH;               // head rows per pass
+    const int sub = lane % TPH;
+    const bool writer = p == P - 1;
+    auto prologue = [&]() {
+      for (int i = lane; i < (D / 32) * 64; i += 64)
+        if ((i & 15) >= nq) qs[i >> 6][i & 63] = bf16x8{};
+      for (int r0 = 0; r0 < nq + 2; r0 += RPP) {        // wave-uniform trip count
+        const int hs = r0 + lane / TPH;
+        const bool act = hs < nq + 2;
+        const int h = hs < nq ? hq0 + hs : (hs == nq ? Hq + kvh : Hq + Hkv + kvh);
+        float a[8], bv[8];
+        rope_lane_values<D, true, QK_NORM, HAS_BIAS, SPLIT>(rope.src, b, act ? h : 0, act, sub,
+                                                           Hq, Hkv, rope.cos_sin,
+                                                           rope.positions[b], a, bv);
+        if (act) {
+          bf16x8 oa, ob;
+#pragma unroll
+          for (int j = 0; j < 8; ++j) { oa[j] = f2bf(a[j]); ob[j] = f2bf(bv[j]); }
+          int e0, e1;
+          rope_lane_offsets<D, true>(sub, e0, e1);
+          if (hs < nq) {
+            qs[e0 / 32][16 * ((e0 % 32) / 8) + hs] = oa;
+            qs[e1 / 32][16 * ((e1 % 32) / 8) + hs] = ob;
+          } else if (writer) {
+            bf16_t* nw = hs == nq ? knew : vnew;
+            *reinterpret_cast<bf16x8*>(nw + e0) = oa;
+            *reinterpret_cast<bf16x8*>(nw + e1) = ob;
+            const int slot = rope.slot_mapping[b];
+            if (slot >= 0)   // for later steps; this one reads the token from LDS
+              rope_lane_store_kv<D, true>(const_cast<bf16_t*>(kc), const_cast<bf16_t*>(vc), slot,
+                                          bs, Hkv, kvh, hs == nq + 1, sub, oa, ob);
+          }
+        }
+      }
+      __syncthreads();
+    };
+    attn_units_deep<D, EIA_WAVE_NS>(acc, qs, kc, vc, bt, ub, ue, L, kvh, Hkv, bs, scale_log2,
+                                    kv_lo, prologue, writer && L > 0 ? L - 1 : -1, knew, vnew);
+  } else {
+    const bool cval = c < nq;
+    const bf16_t* qp = q + (long)b * q_stride + (long)(hq0 + (cval ? c : 0)) * D + 8 * g;
+#pragma unroll
+    for (int s = 0; s < D / 32; ++s) {
+      bf16x8 t = *reinterpret_cast<const bf16x8*>(qp + 32 * s);
+      if (!cval) t = bf16x8{};
+      qs[s][lane] = t;
+    }
+    __syncthreads();
+    attn_units_deep<D, EIA_WAVE_NS>(acc, qs, kc, vc, bt, ub, ue, L, kvh, Hkv, bs, scale_log2,
+                                    kv_lo, [] {}, -1, nullptr, nullptr);
+  }
+  // lane (c, g) holds O^T rows d = 16 dt + 4 g + i of query column c; l is lane-partial
+  float lt = acc.l;
+  lt += __shfl_xor(lt, 16, 64);
+  lt += __shfl_xor(lt, 32, 64);
+  const bool valid = c < nq;
+  const int hq = hq0 + c;
+  if (P == 1) {
+    if (valid) {
+      const float inv = lt > 0.f ? 1.f / lt : 0.f;
+      bf16_t* op = out + (long)b * out_stride + (long)hq * D + 4 * g;
+#pragma unroll
+      for (int dt = 0; dt < D / 16; ++dt) {
+        bf16x4 v;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) v[i] = f2bf(acc.o[dt][i] * inv);
+        *reinterpret_cast<bf16x4*>(op + 16 * dt) = v;
+      }
+    }
+    return;
+  }
+  if (valid) {
+    const long pi = ((long)b * Hq + hq) * Pmax + p;
+    // agent-scope (sc1) stores: coherent for the merging wave on another XCD
+#pragma unroll
+    for (int dt = 0; dt < D / 16; ++dt)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+        __hip_atomic_store(part_o + pi * D + 16 * dt + 4 * g + i, acc.o[dt][i], __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+    if (g == 0) {
+      __hip_atomic_store(part_ml + 2 * pi, acc.m, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(part_ml + 2 * pi + 1, lt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+  if (part_cnt == nullptr) return;                 // separate reduce kernel
+  __builtin_amdgcn_s_waitcnt(0);
+  __syncthreads();
+  int* cnt = part_cnt + (long)b * Hkv + kvh;
+  if (lane == 0)
+    s_last = __hip_atomic_fetch_add(cnt, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == P - 1;
+  __syncthreads();
+  if (!s_last) return;
+  auto ld = [](const float* ptr_) {
+    return __hip_atomic_load(ptr_, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  };
+  for (int idx = lane; idx < nq * D; idx += 64) {
+    const int cq = idx / D, d = idx % D;
+    const long base = ((long)b * Hq + hq0 + cq) * Pmax;
+    float M = NEG_INF;
+    for (int pp = 0; pp < P; ++pp) M = fmaxf(M, ld(part_ml + 2 * (base + pp)));
+    float Ls = 0.f, O = 0.f;
+    if (M != NEG_INF) {
+      for (int pp = 0; pp < P; ++pp) {
+        const float f = exp2f(ld(part_ml + 2 * (base + pp)) - M);
+        Ls += ld(part_ml + 2 * (base + pp) + 1) * f;
+        O += ld(part_o + (base + pp) * D + d) * f;
+      }
+    }
+    out[(long)b * out_stride + (long)(hq0 + cq) * D + d] = f2bf(Ls > 0.f ? O / Ls : 0.f);
+  }
+  if (lane == 0) __hip_atomic_store(cnt, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 // ---------------------------------------------------------------------------------- prefill
 
 // work[2*i] = sequence index, work[2*i+1] = first query (multiple of 16*QT*(4/HPW)).
@@ -951,6 +1228,14 @@ paged_prefill_lds_kernel(const bf16_t* __restrict__ q, long q_stride,
 
 // ---------------------------------------------------------------------------------- launchers
 
+static int decode_wave_env() {
+  static const int v = [] {
+    const char* e = getenv("EIA_DECODE_WAVE");
+    return e != nullptr ? atoi(e) : 0;
+  }();
+  return v;
+}
+
 static int decode_lean_env() {
   static const int v = [] {
     const char* e = getenv("EIA_DECODE_LEAN");
@@ -974,6 +1259,21 @@ EIA_API int eia_paged_decode(const void* q, long q_stride, const void* k_cache, 
   const int lean_env = decode_lean_env();
   // lean form: whole 32-token units inside a block (bs % 32 == 0), uniform per-unit bases
   const bool lean = (lean_env >= 0 ? lean_env != 0 : true) && bs % 32 == 0 && D <= 128;
+  if (decode_wave_env() != 0 && lean && G <= 16 && (D == 64 || D == 128)) {
+    const DecodeRope none{};
+#define DEC_W(DD)                                                                              \
+    hipLaunchKernelGGL((paged_decode_wave_kernel<DD, false, false, false, false>),             \
+                       dim3(B, Hkv, P), dim3(64), 0, st, (const bf16_t*)q, q_stride,           \
+                       (const bf16_t*)k_cache, (const bf16_t*)v_cache, block_tables, bt_stride, \
+                       seq_lens, (bf16_t*)out, out_stride, part_o, part_ml, part_cnt, sl2, Hq,  \
+                       Hkv, bs, P, sliding_window, chunk_size, p_dyn, none);                   \
+    if (P > 1 && part_cnt == nullptr)                                                          \
+      hipLaunchKernelGGL((paged_decode_reduce_kernel<DD>), dim3(B, Hq), dim3(DD), 0, st,       \
+                         part_o, part_ml, (bf16_t*)out, out_stride, Hq, P, p_dyn);
+    if (D == 128) { DEC_W(128) } else { DEC_W(64) }
+#undef DEC_W
+    EIA_LAUNCH_CHECK();
+  }
   dim3 grid(B, Hkv * NQG, P);
   const DecodeRope none{};
 #define DEC_V(DD, LEAN_)                                                                     \
@@ -1028,11 +1328,19 @@ EIA_API int eia_paged_decode_rope(const void* qkv, long qkv_stride, const float*
                                (const bf16_t*)q_norm_w, (const bf16_t*)k_norm_w, eps},
                         positions, cos_sin, slot_mapping};
   dim3 grid(B, Hkv, P);
+  const bool wave = decode_wave_env() != 0;
 #define DEC_F(DD, SP, QN, HB)                                                                    \
-  hipLaunchKernelGGL((paged_decode_kernel<DD, true, true, SP, QN, HB>), grid, dim3(256), 0, st,  \
-                     nullptr, 0L, (const bf16_t*)k_cache, (const bf16_t*)v_cache, block_tables,  \
-                     bt_stride, seq_lens, (bf16_t*)out, out_stride, part_o, part_ml, part_cnt,    \
-                     sl2, Hq, Hkv, bs, P, 1, sliding_window, chunk_size, p_dyn, rope);
+  if (wave)                                                                                      \
+    hipLaunchKernelGGL((paged_decode_wave_kernel<DD, true, SP, QN, HB>), grid, dim3(64), 0, st,   \
+                       nullptr, 0L, (const bf16_t*)k_cache, (const bf16_t*)v_cache,              \
+                       block_tables, bt_stride, seq_lens, (bf16_t*)out, out_stride, part_o,       \
+                       part_ml, part_cnt, sl2, Hq, Hkv, bs, P, sliding_window, chunk_size, p_dyn, \
+                       rope);                                                                    \
+  else                                                                                           \
+    hipLaunchKernelGGL((paged_decode_kernel<DD, true, true, SP, QN, HB>), grid, dim3(256), 0, st,  \
+                       nullptr, 0L, (const bf16_t*)k_cache, (const bf16_t*)v_cache, block_tables,  \
+                       bt_stride, seq_lens, (bf16_t*)out, out_stride, part_o, part_ml, part_cnt,    \
+                       sl2, Hq, Hkv, bs, P, 1, sliding_window, chunk_size, p_dyn, rope);
 #define DEC_FQ(DD, SP)                                                                           \
   if (q_norm_w) { if (bias) { DEC_F(DD, SP, true, true) } else { DEC_F(DD, SP, true, false) } }  \
   else { if (bias) { DEC_F(DD, SP, false, true) } else { DEC_F(DD, SP, false, false) } }

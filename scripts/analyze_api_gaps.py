@@ -30,18 +30,27 @@ def main():
     ap.add_argument("path")
     ap.add_argument("--n", type=int, default=3)
     ap.add_argument("--min-gap-us", type=float, default=200)
+    ap.add_argument("--lookback-ms", type=float, default=1.5)
     a = ap.parse_args()
     ks = sorted((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r["Kernel_Name"])
                 for r in load(a.path, "*kernel_trace.csv"))
-    api = sorted((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r["Function"])
+    api = sorted((int(r["Start_Timestamp"]), int(r["End_Timestamp"]),
+                  r["Function"] + " [tid %s]" % r.get("Thread_Id", "?"))
                  for r in load(a.path, "*hip_api_trace.csv"))
+    try:
+        for r in load(a.path, "*memory_copy_trace.csv"):
+            ks.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]),
+                       "memcpy " + r.get("Direction", "?")))
+        ks.sort()
+    except SystemExit:
+        pass
     gaps = [(ks[i][0] - ks[i - 1][1], ks[i - 1][1], ks[i][0], ks[i - 1][2], ks[i][2])
             for i in range(1, len(ks)) if ks[i][0] - ks[i - 1][1] > a.min_gap_us * 1e3]
     print(f"{len(gaps)} gaps > {a.min_gap_us} us; showing the last {a.n}")
     for g, s, e, kb, ka in gaps[-a.n:]:
         print(f"\n=== gap {g / 1e3:.1f} us: {short(kb)} -> {short(ka)}")
         for t0, t1, f in api:
-            if s - 1.5e6 <= t0 <= e:
+            if s - a.lookback_ms * 1e6 <= t0 <= e:
                 print(f"  {(t0 - s) / 1e3:9.1f} .. {(t1 - s) / 1e3:9.1f} us  {f}")
 
 

@@ -93,6 +93,7 @@ def main():
     ap.add_argument("--out", default=None, help="also write the tuning table here")
     ap.add_argument("--persist", action="store_true",
                     help="also copy the table into the PVC tuning cache ($EIA_CACHE_DIR)")
+    ap.add_argument("--all", action="store_true", help="print every timed (cfg, sk) variant")
     ap.add_argument("--packed", action="store_true",
                     help="sweep the tile-packed-weight configurations (cfg bit 6)")
     a = ap.parse_args()
@@ -140,6 +141,8 @@ def main():
                  "ours_TBps": round(wbytes / to / 1e6, 2), "hipblaslt_TBps": round(wbytes / tb / 1e6, 2),
                  "speedup": round(tb / to, 2),
                  "runner_up": [(round(t, 1), c, s) for t, c, s in results[1:4]]}
+            if a.all:
+                r["all"] = [(round(t, 1), c, s) for t, c, s in results]
             print(json.dumps(r), flush=True)
             if a.tune:
                 key = f"{gemm.m_bucket(M)},{N},{K},{int(swiglu)}"
