@@ -18,6 +18,26 @@
 #include "eia_common.h"
 #include "eia_rope.h"
 
+// Phase timestamps (diagnostic build only, -DEIA_ATTN_TRACE; scripts/attn_trace.py): lane 0 of
+// every wave stores the 100 MHz wall clock at named points of the decode kernel into
+// g_attn_trace[workgroup][wave][slot] (8 slots per wave, 4 waves per workgroup).
+#ifdef EIA_ATTN_TRACE
+__device__ long long* g_attn_trace;
+#define ATRACE(slot)                                                                            \
+  do {                                                                                          \
+    if ((threadIdx.x & 63) == 0 && g_attn_trace != nullptr)                                     \
+      g_attn_trace[(((long)blockIdx.z * gridDim.y + blockIdx.y) * gridDim.x + blockIdx.x) * 32 + \
+                   (threadIdx.x >> 6) * 8 + (slot)] = wall_clock64();                           \
+  } while (0)
+EIA_API int eia_attn_set_trace(void* p) {
+  return (int)hipMemcpyToSymbol(HIP_SYMBOL(g_attn_trace), &p, sizeof(p));
+}
+#else
+#define ATRACE(slot) \
+  do {               \
+  } while (0)
+#endif
+
 #define NEG_INF (-INFINITY)
 #ifndef EIA_LEAN_OCC
 #define EIA_LEAN_OCC 3
@@ -247,20 +267,25 @@ EIA_DEV void compute_unit(WaveAcc<D>& acc, const bf16x8 (&qf)[D / 32], const KVF
 // bases are wave-uniform (one scalar block-table read) and each lane adds a CONSTANT 32-bit
 // byte offset, so the loads take the SGPR-base + VGPR-offset form -- no per-unit 64-bit
 // per-lane pointers held in VGPRs.
-// `pre` runs once per wave between the first unit's loads and the loop (every wave calls it,
-// also those without units): the fused decode prologue (RoPE, KV write, q -> LDS, barrier)
-// then overlaps the first K/V fetch.  Token `tnew` (this step's, -1: none) is taken from
+// `pre_issue` puts the prologue's loads in flight right behind the first unit's, and `pre` runs
+// once per wave after them (every wave calls both, also those without units): the fused decode
+// prologue (RoPE, KV write, q -> LDS, barrier) then overlaps the first K/V fetch.  The order
+// matters: the unit's bases wait (vmcnt, in-order) for the block-table window load, which must
+// not sit behind the prologue's slab loads (profiles/attn_trace_r3.md: 6 us of entry latency).  Token `tnew` (this step's, -1: none) is taken from
 // knew / vnew in LDS instead of the cache: its K/V stores may still be in flight when the unit
 // holding it is read, so those lanes' fragments are patched after the loads land.
-template <int D, typename Pre>
+template <int D, typename PreIssue, typename Pre>
 EIA_DEV void attn_units_lean(WaveAcc<D>& acc, const bf16x8 (&qs)[D / 32][64],
                              const bf16_t* __restrict__ kc, const bf16_t* __restrict__ vc,
-                             const int* __restrict__ bt, int ub, int ue, int w, int L, int kvh,
-                             int Hkv, int bs, float scale_log2, int kv_lo, int NW, Pre&& pre,
-                             int tnew, const bf16_t* knew, const bf16_t* vnew) {
+                             const int* __restrict__ bt, int bt_win, int ub, int ue, int w, int L,
+                             int kvh,
+                             int Hkv, int bs, float scale_log2, int kv_lo, int NW,
+                             PreIssue&& pre_issue, Pre&& pre, int tnew, const bf16_t* knew,
+                             const bf16_t* vnew) {
   // the unit index is wave-uniform; say so, or the per-unit bases become 64-bit VGPR pointers
   int u = __builtin_amdgcn_readfirstlane(ub + w);
   if (u >= ue) {
+    pre_issue();
     pre();
     return;
   }
@@ -273,7 +298,8 @@ EIA_DEV void attn_units_lean(WaveAcc<D>& acc, const bf16x8 (&qs)[D / 32][64],
   const unsigned voff = (unsigned)((8 * g + c * bs) * 2);
   auto bases = [&](int uu, const char*& kb, const char*& vb) {
     const int tb = 32 * uu;
-    const int blk = bt[__builtin_amdgcn_readfirstlane(tb / bs)];
+    const int bi = __builtin_amdgcn_readfirstlane(tb / bs);
+    const int blk = bi < 64 ? __builtin_amdgcn_readlane(bt_win, bi) : bt[bi];
     const long base = ((long)blk * Hkv + kvh) * hk;
     const int o = __builtin_amdgcn_readfirstlane(tb % bs);
     kb = reinterpret_cast<const char*>(kc + base + (long)o * D);
@@ -298,6 +324,8 @@ EIA_DEV void attn_units_lean(WaveAcc<D>& acc, const bf16x8 (&qs)[D / 32][64],
     ldk(ka0, ka1, kbp);
     ldv(va, vbp);
   }
+  ATRACE(7);
+  pre_issue();
   pre();
   // lanes holding token tnew of unit uc take it from LDS (wave-uniform test)
   auto patch = [&](bf16x8 (&k0)[D / 32], bf16x8 (&k1)[D / 32], bf16x8 (&v)[D / 16], int uc) {
@@ -389,6 +417,7 @@ EIA_DEV void attn_units_pipelined(WaveAcc<D>& acc, const bf16x8 (&qf)[D / 32],
 
 // ---------------------------------------------------------------------------------- decode
 
+
 // 4 waves per workgroup.  LEAN: the attn_units_lean pipeline at 3 workgroups per CU (D <= 128);
 // otherwise two full K/V fragment sets at 2 per CU.  (A 2-wave form with 4 per CU measured
 // 1.9-2.2x slower at B = 16..65: each wave walks twice the units.)
@@ -423,23 +452,39 @@ paged_decode_kernel(const bf16_t* __restrict__ q, long q_stride,
   __shared__ int s_last;
   __shared__ float sm[NW][16];
   __shared__ float sl[NW][16];
-  __shared__ float so[NW][D][17];
+  __shared__ __align__(16) float so[NW][D][17];
 
   const int b = blockIdx.x;
   const int kvh = blockIdx.y / NQG, qg = blockIdx.y % NQG;
   const int p = blockIdx.z;
+  ATRACE(0);
   // partitions actually used this call: a HIP graph is captured with grid.z = Pmax and the
   // host writes the step's P (from the batch's longest context) into device memory, so one
   // graph serves short and long contexts; surplus workgroups exit at once (grid.z is the
   // slowest dispatch dimension, so they trail the real work)
-  const int P = p_dyn != nullptr ? max(1, min(*p_dyn, Pmax)) : Pmax;
-  if (p >= P) return;
+  // The step's P, L and the fused prologue's scalars are independent loads: issued together
+  // (one round trip), the surplus-workgroup exit test after them.
+  const int pd = *(p_dyn != nullptr ? p_dyn : seq_lens);   // unconditional: no wait in a branch
+  const int L = seq_lens[b];
+  const int pos_b = FUSED ? rope.positions[b] : 0;
+  const int slot_b = FUSED ? rope.slot_mapping[b] : -1;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int c = lane & 15, g = lane >> 4;
+  const int* bt = block_tables + (long)b * bt_stride;
+  // Block-table window: entries [0, 64) of this sequence's row, one per lane, loaded beside L so
+  // the first units' K/V bases need no scalar load that waits for L (the entry chain was
+  // kernel args -> L -> block table -> K/V, three cold round trips before the first K/V byte;
+  // profiles/attn_trace_r3.md).  Entries past the row's live blocks are read, never used.
+  int bt_win = 0;
+  if constexpr (LEAN) bt_win = lane < bt_stride ? bt[lane] : 0;
+  const int P = p_dyn != nullptr ? max(1, min(pd, Pmax)) : Pmax;
+  // (L | pos | slot + 1) < 0 never holds; testing it keeps the compiler from sinking those loads past the
+  // exit branch, which would serialise them behind the p_dyn round trip
+  if ((p >= P) | ((L | pos_b | (slot_b + 1)) < 0)) return;   // no short-circuit
+  ATRACE(6);
   const int G = Hq / Hkv;
   const int hq0 = kvh * G + qg * 16;
   const int nq = min(16, G - qg * 16);
-  const int L = seq_lens[b];
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  const int c = lane & 15, g = lane >> 4;
 
   bf16x8 qf[D / 32];
   if constexpr (!FUSED) {
@@ -455,6 +500,120 @@ paged_decode_kernel(const bf16_t* __restrict__ q, long q_stride,
       qf[s] = t;
     }
   }
+  // Q fragments through LDS (one copy, re-read per unit): 16 fewer live VGPRs outside QK.
+  // qs[s][16 g + c] = q head c, dims [32 s + 8 g, +8)
+  __shared__ bf16x8 qs[D / 32][64];
+  // ---- fused K4 prologue state (FUSED); pro_issue runs right behind the first unit's loads
+  constexpr int TPH = D / 16;
+  const int hs = threadIdx.x / TPH, sub = threadIdx.x % TPH;
+  const bool act = hs < nq + 2;
+  const int h = hs < nq ? hq0 + hs : (hs == nq ? Hq + kvh : Hq + Hkv + kvh);
+  const bool writer = p == P - 1 && qg == 0;
+  __shared__ __align__(16) bf16_t knew[D], vnew[D];
+  // Split-K slabs: the whole workgroup loads the nh head rows' fp32 slabs (JS float4 per
+  // thread, all in flight ahead of the K/V units) and parks them in LDS -- in `so`, dead
+  // until the unit loop ends -- where the RoPE lanes sum them in slab order.  One lane per
+  // 16-element row slice loading all sk slabs itself held 64 VGPRs of slab data and spilled
+  // at the 3-workgroups-per-CU budget.  Shapes whose slabs exceed the staging capacity sum
+  // them per lane, one round trip per slab.
+  constexpr int JS = 4;
+  const int nh = nq + 2;
+  const int n4 = SPLIT ? rope.src.sk * nh * (D / 4) : 0;
+  const bool staged = SPLIT && n4 <= JS * 256 && n4 * 4 <= NW * D * 17;
+  f32x4 sv[JS];
+  float* stage = &so[0][0][0];
+  RopeLane<D, true, QK_NORM, HAS_BIAS, SPLIT ? ROPE_SRC_CALLER : ROPE_SRC_BF16> rl;
+  int slot = -1;
+  const int ntot = Hq + 2 * Hkv;
+  auto head_of = [&](int r) { return r < nq ? hq0 + r : (r == nq ? Hq + kvh : Hq + Hkv + kvh); };
+  auto pro_issue = [&]() {
+    if (staged) {
+      // float4 f = row (f / (D/4)) of the [sk][nh] row list, column f % (D/4); the row's
+      // (slab, head) split uses a float reciprocal (exact for these small integers) instead
+      // of a ~40-instruction integer division per float4
+      const float inv_nh = 1.f / (float)nh;
+#pragma unroll
+      for (int j = 0; j < JS; ++j) {
+        const int f = threadIdx.x + 256 * j;
+        if (f < n4) {
+          const int rr = f / (D / 4);
+          const int k = (int)(((float)rr + 0.5f) * inv_nh);
+          const float* src = rope.src.part + (long)k * rope.src.slab + (long)b * ntot * D +
+                             (long)head_of(rr - k * nh) * D + 4 * (f % (D / 4));
+          sv[j] = *reinterpret_cast<const f32x4*>(src);
+        }
+      }
+    }
+    rl.issue(rope.src, b, act ? h : 0, act, sub, Hq, Hkv, rope.cos_sin, pos_b);
+    if (act && hs >= nq && writer) slot = slot_b;
+  };
+  auto prologue = [&]() {
+    ATRACE(1);
+    // zero the unused query columns (c >= nq); the RoPE lanes write the others
+    for (int i = threadIdx.x; i < (D / 32) * 64; i += 256)
+      if ((i & 15) >= nq) qs[i >> 6][i & 63] = bf16x8{};
+    float a[8], bv[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) { a[j] = 0.f; bv[j] = 0.f; }
+    if constexpr (SPLIT) {
+      int e0, e1;
+      rope_lane_offsets<D, true>(sub, e0, e1);
+      if (staged) {
+#pragma unroll
+        for (int j = 0; j < JS; ++j) {
+          const int f = threadIdx.x + 256 * j;
+          if (f < n4) *reinterpret_cast<f32x4*>(stage + 4 * f) = sv[j];
+        }
+        __syncthreads();
+        if (act) {
+          for (int k = 0; k < rope.src.sk; ++k) {
+            const float* row = stage + (k * nh + hs) * D;
+#pragma unroll
+            for (int q4 = 0; q4 < 2; ++q4) {
+              const f32x4 xa = *reinterpret_cast<const f32x4*>(row + e0 + 4 * q4);
+              const f32x4 xb = *reinterpret_cast<const f32x4*>(row + e1 + 4 * q4);
+#pragma unroll
+              for (int j = 0; j < 4; ++j) { a[4 * q4 + j] += xa[j]; bv[4 * q4 + j] += xb[j]; }
+            }
+          }
+        }
+      } else if (act) {
+        const float* pp = rope.src.part + (long)b * ntot * D + (long)h * D;
+        for (int k = 0; k < rope.src.sk; ++k, pp += rope.src.slab) {
+#pragma unroll
+          for (int q4 = 0; q4 < 2; ++q4) {
+            const f32x4 xa = *reinterpret_cast<const f32x4*>(pp + e0 + 4 * q4);
+            const f32x4 xb = *reinterpret_cast<const f32x4*>(pp + e1 + 4 * q4);
+#pragma unroll
+            for (int j = 0; j < 4; ++j) { a[4 * q4 + j] += xa[j]; bv[4 * q4 + j] += xb[j]; }
+          }
+        }
+      }
+#pragma unroll
+      for (int j = 0; j < 8; ++j) { a[j] = bf2f(f2bf(a[j])); bv[j] = bf2f(f2bf(bv[j])); }
+    }
+    rl.finish(rope.src, b, act ? h : 0, act, sub, Hq, Hkv, rope.cos_sin, a, bv);
+    if (act) {
+      bf16x8 oa, ob;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) { oa[j] = f2bf(a[j]); ob[j] = f2bf(bv[j]); }
+      int e0, e1;
+      rope_lane_offsets<D, true>(sub, e0, e1);
+      if (hs < nq) {
+        qs[e0 / 32][16 * ((e0 % 32) / 8) + hs] = oa;
+        qs[e1 / 32][16 * ((e1 % 32) / 8) + hs] = ob;
+      } else if (writer) {
+        bf16_t* nw = hs == nq ? knew : vnew;
+        *reinterpret_cast<bf16x8*>(nw + e0) = oa;
+        *reinterpret_cast<bf16x8*>(nw + e1) = ob;
+        if (slot >= 0)   // for later steps; this one reads the token from LDS
+          rope_lane_store_kv<D, true>(const_cast<bf16_t*>(kc), const_cast<bf16_t*>(vc), slot,
+                                      bs, Hkv, kvh, hs == nq + 1, sub, oa, ob);
+      }
+    }
+    __syncthreads();
+    ATRACE(2);
+  };
   WaveAcc<D> acc;
   wave_acc_init(acc);
   // sliding window (Mistral) / chunked local attention (Llama-4) bound the visible keys
@@ -468,57 +627,19 @@ paged_decode_kernel(const bf16_t* __restrict__ q, long q_stride,
   const int npair = (U0 + U - A0 + 1) / 2;
   const int ub = max(U0, A0 + 2 * (int)(((long)p * npair) / P));
   const int ue = min(U0 + U, A0 + 2 * (int)(((long)(p + 1) * npair) / P));
-  const int* bt = block_tables + (long)b * bt_stride;
   if constexpr (LEAN) {
-    // Q fragments through LDS (one copy, re-read per unit): 16 fewer live VGPRs outside QK.
-    // qs[s][16 g + c] = q head c, dims [32 s + 8 g, +8)
-    __shared__ bf16x8 qs[D / 32][64];
     if constexpr (FUSED) {
-      constexpr int TPH = D / 16;
-      const int hs = threadIdx.x / TPH, sub = threadIdx.x % TPH;
-      const bool act = hs < nq + 2;
-      const int h = hs < nq ? hq0 + hs : (hs == nq ? Hq + kvh : Hq + Hkv + kvh);
-      const bool writer = p == P - 1 && qg == 0;
-      __shared__ __align__(16) bf16_t knew[D], vnew[D];
-      auto prologue = [&]() {
-        // zero the unused query columns (c >= nq); the RoPE lanes write the others
-        for (int i = threadIdx.x; i < (D / 32) * 64; i += 256)
-          if ((i & 15) >= nq) qs[i >> 6][i & 63] = bf16x8{};
-        float a[8], bv[8];
-        rope_lane_values<D, true, QK_NORM, HAS_BIAS, SPLIT>(rope.src, b, act ? h : 0, act, sub,
-                                                           Hq, Hkv, rope.cos_sin,
-                                                           rope.positions[b], a, bv);
-        if (act) {
-          bf16x8 oa, ob;
-#pragma unroll
-          for (int j = 0; j < 8; ++j) { oa[j] = f2bf(a[j]); ob[j] = f2bf(bv[j]); }
-          int e0, e1;
-          rope_lane_offsets<D, true>(sub, e0, e1);
-          if (hs < nq) {
-            qs[e0 / 32][16 * ((e0 % 32) / 8) + hs] = oa;
-            qs[e1 / 32][16 * ((e1 % 32) / 8) + hs] = ob;
-          } else if (writer) {
-            bf16_t* nw = hs == nq ? knew : vnew;
-            *reinterpret_cast<bf16x8*>(nw + e0) = oa;
-            *reinterpret_cast<bf16x8*>(nw + e1) = ob;
-            const int slot = rope.slot_mapping[b];
-            if (slot >= 0)   // for later steps; this one reads the token from LDS
-              rope_lane_store_kv<D, true>(const_cast<bf16_t*>(kc), const_cast<bf16_t*>(vc), slot,
-                                          bs, Hkv, kvh, hs == nq + 1, sub, oa, ob);
-          }
-        }
-        __syncthreads();
-      };
-      attn_units_lean<D>(acc, qs, kc, vc, bt, ub, ue, w, L, kvh, Hkv, bs, scale_log2, kv_lo, NW,
-                         prologue, writer && L > 0 ? L - 1 : -1, knew, vnew);
+      attn_units_lean<D>(acc, qs, kc, vc, bt, bt_win, ub, ue, w, L, kvh, Hkv, bs, scale_log2,
+                         kv_lo, NW, pro_issue, prologue, writer && L > 0 ? L - 1 : -1, knew, vnew);
+      ATRACE(3);
     } else {
       if (w == 0) {
 #pragma unroll
         for (int s = 0; s < D / 32; ++s) qs[s][lane] = qf[s];
       }
       __syncthreads();
-      attn_units_lean<D>(acc, qs, kc, vc, bt, ub, ue, w, L, kvh, Hkv, bs, scale_log2, kv_lo, NW,
-                         [] {}, -1, nullptr, nullptr);
+      attn_units_lean<D>(acc, qs, kc, vc, bt, bt_win, ub, ue, w, L, kvh, Hkv, bs, scale_log2,
+                         kv_lo, NW, [] {}, [] {}, -1, nullptr, nullptr);
     }
   } else
     attn_units_pipelined<D>(acc, qf, kc, vc, bt, ub, ue, w, L, kvh, Hkv, bs, scale_log2, kv_lo, NW);
@@ -532,10 +653,10 @@ paged_decode_kernel(const bf16_t* __restrict__ q, long q_stride,
 #pragma unroll
     for (int i = 0; i < 4; ++i) so[w][16 * dt + 4 * g + i][c] = acc.o[dt][i];
   __syncthreads();
+  ATRACE(4);
 
-  for (int idx = threadIdx.x; idx < 16 * D; idx += blockDim.x) {
+  for (int idx = threadIdx.x; idx < nq * D; idx += blockDim.x) {   // live query columns only
     const int cq = idx / D, d = idx % D;
-    if (cq >= nq) continue;
     float M = NEG_INF;
 #pragma unroll
     for (int ww = 0; ww < NW; ++ww) M = fmaxf(M, sm[ww][cq]);
@@ -563,6 +684,7 @@ paged_decode_kernel(const bf16_t* __restrict__ q, long q_stride,
       }
     }
   }
+  ATRACE(5);
   if (P == 1 || part_cnt == nullptr) return;
   // Fused partition merge: the last of the P workgroups of this (b, kv head, q group) merges
   // the partials (no separate reduce launch).  No __threadfence(): an agent-scope fence
@@ -581,9 +703,8 @@ paged_decode_kernel(const bf16_t* __restrict__ q, long q_stride,
   auto ld = [](const float* p) {
     return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   };
-  for (int idx = threadIdx.x; idx < 16 * D; idx += blockDim.x) {
+  for (int idx = threadIdx.x; idx < nq * D; idx += blockDim.x) {   // live query columns only
     const int cq = idx / D, d = idx % D;
-    if (cq >= nq) continue;
     const long base = ((long)b * Hq + hq0 + cq) * Pmax;
     float M = NEG_INF;
     for (int pp = 0; pp < P; ++pp) M = fmaxf(M, ld(part_ml + 2 * (base + pp)));
@@ -628,13 +749,15 @@ paged_decode_reduce_kernel(const float* __restrict__ part_o, const float* __rest
 // rotate so NS-1 units stay in flight while one is multiplied (the wave has no siblings to hide
 // its load latency), and the partition's block-table entries are read once up front into a
 // lane-indexed register (readlane per unit) instead of one dependent scalar load per unit.
-template <int D, int NS, typename Pre>
+template <int D, int NS, typename PreIssue, typename Pre>
 EIA_DEV void attn_units_deep(WaveAcc<D>& acc, const bf16x8 (&qs)[D / 32][64],
                              const bf16_t* __restrict__ kc, const bf16_t* __restrict__ vc,
-                             const int* __restrict__ bt, int ub, int ue, int L, int kvh, int Hkv,
-                             int bs, float scale_log2, int kv_lo, Pre&& pre, int tnew,
-                             const bf16_t* knew, const bf16_t* vnew) {
+                             const int* __restrict__ bt, int bt_win, int ub, int ue, int L,
+                             int kvh, int Hkv, int bs, float scale_log2, int kv_lo,
+                             PreIssue&& pre_issue, Pre&& pre, int tnew, const bf16_t* knew,
+                             const bf16_t* vnew) {
   if (ub >= ue) {
+    pre_issue();
     pre();
     return;
   }
@@ -644,20 +767,22 @@ EIA_DEV void attn_units_deep(WaveAcc<D>& acc, const bf16x8 (&qs)[D / 32][64],
   const unsigned koff = (unsigned)(((8 * (c >> 2) + (c & 3)) * D + 8 * g) * 2);
   const unsigned voff = (unsigned)((8 * g + c * bs) * 2);
   const int upb = bs / 32;                           // units per block
-  int wbase = __builtin_amdgcn_readfirstlane(ub / upb);   // first block of the lane window
-  const int blast = (ue - 1) / upb;
-  int wblk = (wbase + lane <= blast) ? bt[wbase + lane] : 0;
+  // lane window of block-table entries [wbase, wbase + 64): the caller's window (entries
+  // [0, 64), loaded beside L at kernel entry) until a unit lies past it
+  int wbase = 0;
+  int wblk = bt_win;
   auto block_of = [&](int uu) -> int {
     const int bi = uu / upb;
     if (bi - wbase >= 64) {                          // wave-uniform: slide the window
       wbase = bi;
-      wblk = (wbase + lane <= blast) ? bt[wbase + lane] : 0;
+      wblk = bt[wbase + lane];                       // entries past the row end: never used
     }
     return __builtin_amdgcn_readlane(wblk, bi - wbase);
   };
   // named register sets (an indexed array of them is demoted to scratch by hipcc)
   bf16x8 ak0[D / 32], ak1[D / 32], av[D / 16], bk0[D / 32], bk1[D / 32], bv[D / 16];
   bf16x8 ck0[D / 32], ck1[D / 32], cv[D / 16], dk0[D / 32], dk1[D / 32], dv[D / 16];
+  bf16x8 ek0[D / 32], ek1[D / 32], ev[D / 16], fk0[D / 32], fk1[D / 32], fv[D / 16];
   auto load = [&](bf16x8 (&k0)[D / 32], bf16x8 (&k1)[D / 32], bf16x8 (&v)[D / 16], int uu) {
     const int blk = block_of(uu);
     const long base = ((long)blk * Hkv + kvh) * hk;
@@ -709,13 +834,46 @@ EIA_DEV void attn_units_deep(WaveAcc<D>& acc, const bf16x8 (&qs)[D / 32][64],
     softmax_pv<D>(acc, s0, s1, v, 32 * uc, L, scale_log2, 0x7fffffff, kv_lo);
     __builtin_amdgcn_sched_barrier(0);
   };
-  static_assert(NS == 3 || NS == 4, "wave decode pipeline: 3 or 4 register sets");
+  static_assert(NS >= 3 && NS <= 6, "wave decode pipeline: 3 to 6 register sets");
+  // the first NS-1 units' loads, then the prologue's (behind them: the window readlane above
+  // waits, in-order, only for the window load)
   load(ak0, ak1, av, ub);
   load(bk0, bk1, bv, min(ub + 1, ue - 1));
-  if constexpr (NS == 4) load(ck0, ck1, cv, min(ub + 2, ue - 1));
+  if constexpr (NS >= 4) load(ck0, ck1, cv, min(ub + 2, ue - 1));
+  if constexpr (NS >= 5) load(dk0, dk1, dv, min(ub + 3, ue - 1));
+  if constexpr (NS == 6) load(ek0, ek1, ev, min(ub + 4, ue - 1));
+  pre_issue();
   pre();
   int u = ub;
-  if constexpr (NS == 4) {
+  if constexpr (NS == 6) {
+    for (;;) {
+      step(ak0, ak1, av, fk0, fk1, fv, u);
+      if (++u >= ue) return;
+      step(bk0, bk1, bv, ak0, ak1, av, u);
+      if (++u >= ue) return;
+      step(ck0, ck1, cv, bk0, bk1, bv, u);
+      if (++u >= ue) return;
+      step(dk0, dk1, dv, ck0, ck1, cv, u);
+      if (++u >= ue) return;
+      step(ek0, ek1, ev, dk0, dk1, dv, u);
+      if (++u >= ue) return;
+      step(fk0, fk1, fv, ek0, ek1, ev, u);
+      if (++u >= ue) return;
+    }
+  } else if constexpr (NS == 5) {
+    for (;;) {
+      step(ak0, ak1, av, ek0, ek1, ev, u);
+      if (++u >= ue) return;
+      step(bk0, bk1, bv, ak0, ak1, av, u);
+      if (++u >= ue) return;
+      step(ck0, ck1, cv, bk0, bk1, bv, u);
+      if (++u >= ue) return;
+      step(dk0, dk1, dv, ck0, ck1, cv, u);
+      if (++u >= ue) return;
+      step(ek0, ek1, ev, dk0, dk1, dv, u);
+      if (++u >= ue) return;
+    }
+  } else if constexpr (NS == 4) {
     for (;;) {
       step(ak0, ak1, av, dk0, dk1, dv, u);
       if (++u >= ue) return;
@@ -749,12 +907,20 @@ EIA_DEV void attn_units_deep(WaveAcc<D>& acc, const bf16x8 (&qs)[D / 32][64],
 // per-unit latency is pipelined along the wave's own unit stream and B * Hkv * P independent
 // waves spread over the CUs.  FUSED: the K4 prologue (split-K reduce / bias / qk-norm / RoPE /
 // KV write, q into LDS) runs on the wave's 64 lanes, D/16 lanes per head row.
+// One wave per SIMD (512 registers): NS = 6 register sets keep five 32-token units in flight
+// from the first instruction on -- a short context (ctx <= 160) is fetched in ONE round trip
+// and a long one streams five units deep -- and the fused prologue holds a whole split-K group
+// of slabs beside them.  B * Hkv * P <= 1024 waves still run in one round.
+// The fused form keeps one set fewer: its prologue's slab registers would otherwise spill.
 #ifndef EIA_WAVE_NS
-#define EIA_WAVE_NS 3      // K/V register sets of the wave form (NS-1 units in flight)
+#define EIA_WAVE_NS 6      // K/V register sets of the wave form (NS-1 units in flight)
+#endif
+#ifndef EIA_WAVE_NS_FUSED
+#define EIA_WAVE_NS_FUSED 5
 #endif
 
 template <int D, bool FUSED, bool SPLIT, bool QK_NORM, bool HAS_BIAS>
-__global__ void __launch_bounds__(64, 2)
+__global__ void __launch_bounds__(64, 1)
 paged_decode_wave_kernel(const bf16_t* __restrict__ q, long q_stride, const bf16_t* kc,
                          const bf16_t* vc, const int* __restrict__ block_tables, int bt_stride,
                          const int* __restrict__ seq_lens, bf16_t* __restrict__ out,
@@ -766,13 +932,22 @@ paged_decode_wave_kernel(const bf16_t* __restrict__ q, long q_stride, const bf16
   __shared__ __align__(16) bf16_t knew[D], vnew[D];
   __shared__ int s_last;
   const int b = blockIdx.x, kvh = blockIdx.y, p = blockIdx.z;
-  const int P = p_dyn != nullptr ? max(1, min(*p_dyn, Pmax)) : Pmax;
-  if (p >= P) return;
-  const int nq = Hq / Hkv;             // <= 16 (host-checked)
-  const int hq0 = kvh * nq;
-  const int L = seq_lens[b];
+  ATRACE(0);
   const int lane = threadIdx.x;
   const int c = lane & 15, g = lane >> 4;
+  // entry loads in one round trip (see paged_decode_kernel): P, L, the prologue scalars and the
+  // block-table window [0, 64)
+  const int pd = *(p_dyn != nullptr ? p_dyn : seq_lens);
+  const int L = seq_lens[b];
+  const int pos_b = FUSED ? rope.positions[b] : 0;
+  const int slot_b = FUSED ? rope.slot_mapping[b] : -1;
+  const int* bt = block_tables + (long)b * bt_stride;
+  const int bt_win = lane < bt_stride ? bt[lane] : 0;
+  const int P = p_dyn != nullptr ? max(1, min(pd, Pmax)) : Pmax;
+  if ((p >= P) | ((L | pos_b | (slot_b + 1)) < 0)) return;   // no short-circuit
+  ATRACE(6);
+  const int nq = Hq / Hkv;             // <= 16 (host-checked)
+  const int hq0 = kvh * nq;
   WaveAcc<D> acc;
   wave_acc_init(acc);
   int kv_lo = 0;
@@ -784,23 +959,37 @@ paged_decode_wave_kernel(const bf16_t* __restrict__ q, long q_stride, const bf16
   const int npair = (U0 + U - A0 + 1) / 2;
   const int ub = max(U0, A0 + 2 * (int)(((long)p * npair) / P));
   const int ue = min(U0 + U, A0 + 2 * (int)(((long)(p + 1) * npair) / P));
-  const int* bt = block_tables + (long)b * bt_stride;
   if constexpr (FUSED) {
     constexpr int TPH = D / 16;                 // lanes per head row
     constexpr int RPP = 64 / TPH;               // head rows per pass
     const int sub = lane % TPH;
     const bool writer = p == P - 1;
+    // head rows r0 + lane / TPH, r0 = 0, RPP, ...: the first pass's loads are issued ahead of the
+    // first K/V units (pro_issue); further passes (nq + 2 > RPP) issue their own
+    RopeLane<D, true, QK_NORM, HAS_BIAS, SPLIT> rl;
+    int slot = -1;
+    auto row_head = [&](int r0, int& hs, bool& act, int& h) {
+      hs = r0 + lane / TPH;
+      act = hs < nq + 2;
+      h = hs < nq ? hq0 + hs : (hs == nq ? Hq + kvh : Hq + Hkv + kvh);
+    };
+    auto pro_issue = [&]() {
+      int hs, h;
+      bool act;
+      row_head(0, hs, act, h);
+      rl.issue(rope.src, b, act ? h : 0, act, sub, Hq, Hkv, rope.cos_sin, pos_b);
+      if (writer) slot = slot_b;
+    };
     auto prologue = [&]() {
       for (int i = lane; i < (D / 32) * 64; i += 64)
         if ((i & 15) >= nq) qs[i >> 6][i & 63] = bf16x8{};
       for (int r0 = 0; r0 < nq + 2; r0 += RPP) {        // wave-uniform trip count
-        const int hs = r0 + lane / TPH;
-        const bool act = hs < nq + 2;
-        const int h = hs < nq ? hq0 + hs : (hs == nq ? Hq + kvh : Hq + Hkv + kvh);
+        int hs, h;
+        bool act;
+        row_head(r0, hs, act, h);
+        if (r0 > 0) rl.issue(rope.src, b, act ? h : 0, act, sub, Hq, Hkv, rope.cos_sin, pos_b);
         float a[8], bv[8];
-        rope_lane_values<D, true, QK_NORM, HAS_BIAS, SPLIT>(rope.src, b, act ? h : 0, act, sub,
-                                                           Hq, Hkv, rope.cos_sin,
-                                                           rope.positions[b], a, bv);
+        rl.finish(rope.src, b, act ? h : 0, act, sub, Hq, Hkv, rope.cos_sin, a, bv);
         if (act) {
           bf16x8 oa, ob;
 #pragma unroll
@@ -814,7 +1003,6 @@ paged_decode_wave_kernel(const bf16_t* __restrict__ q, long q_stride, const bf16
             bf16_t* nw = hs == nq ? knew : vnew;
             *reinterpret_cast<bf16x8*>(nw + e0) = oa;
             *reinterpret_cast<bf16x8*>(nw + e1) = ob;
-            const int slot = rope.slot_mapping[b];
             if (slot >= 0)   // for later steps; this one reads the token from LDS
               rope_lane_store_kv<D, true>(const_cast<bf16_t*>(kc), const_cast<bf16_t*>(vc), slot,
                                           bs, Hkv, kvh, hs == nq + 1, sub, oa, ob);
@@ -823,8 +1011,9 @@ paged_decode_wave_kernel(const bf16_t* __restrict__ q, long q_stride, const bf16
       }
       __syncthreads();
     };
-    attn_units_deep<D, EIA_WAVE_NS>(acc, qs, kc, vc, bt, ub, ue, L, kvh, Hkv, bs, scale_log2,
-                                    kv_lo, prologue, writer && L > 0 ? L - 1 : -1, knew, vnew);
+    attn_units_deep<D, EIA_WAVE_NS_FUSED>(acc, qs, kc, vc, bt, bt_win, ub, ue, L, kvh, Hkv, bs, scale_log2,
+                                    kv_lo, pro_issue, prologue, writer && L > 0 ? L - 1 : -1,
+                                    knew, vnew);
   } else {
     const bool cval = c < nq;
     const bf16_t* qp = q + (long)b * q_stride + (long)(hq0 + (cval ? c : 0)) * D + 8 * g;
@@ -835,9 +1024,10 @@ paged_decode_wave_kernel(const bf16_t* __restrict__ q, long q_stride, const bf16
       qs[s][lane] = t;
     }
     __syncthreads();
-    attn_units_deep<D, EIA_WAVE_NS>(acc, qs, kc, vc, bt, ub, ue, L, kvh, Hkv, bs, scale_log2,
-                                    kv_lo, [] {}, -1, nullptr, nullptr);
+    attn_units_deep<D, EIA_WAVE_NS>(acc, qs, kc, vc, bt, bt_win, ub, ue, L, kvh, Hkv, bs, scale_log2,
+                                    kv_lo, [] {}, [] {}, -1, nullptr, nullptr);
   }
+  ATRACE(3);
   // lane (c, g) holds O^T rows d = 16 dt + 4 g + i of query column c; l is lane-partial
   float lt = acc.l;
   lt += __shfl_xor(lt, 16, 64);
@@ -856,6 +1046,7 @@ paged_decode_wave_kernel(const bf16_t* __restrict__ q, long q_stride, const bf16
         *reinterpret_cast<bf16x4*>(op + 16 * dt) = v;
       }
     }
+    ATRACE(5);
     return;
   }
   if (valid) {
