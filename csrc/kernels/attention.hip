@@ -23,18 +23,29 @@
 // g_attn_trace[workgroup][wave][slot] (8 slots per wave, 4 waves per workgroup).
 #ifdef EIA_ATTN_TRACE
 __device__ long long* g_attn_trace;
-#define ATRACE(slot)                                                                            \
+// stamps are kept in registers and stored once at the end (a store per stamp would sit in the
+// in-order vmcnt queue and delay the kernel's own waits)
+#define ATRACE_DECL long long atr_[8] = {0, 0, 0, 0, 0, 0, 0, 0}
+#define ATRACE(slot) (atr_[(slot)] = wall_clock64())
+#define ATRACE_FLUSH()                                                                          \
   do {                                                                                          \
-    if ((threadIdx.x & 63) == 0 && g_attn_trace != nullptr)                                     \
-      g_attn_trace[(((long)blockIdx.z * gridDim.y + blockIdx.y) * gridDim.x + blockIdx.x) * 32 + \
-                   (threadIdx.x >> 6) * 8 + (slot)] = wall_clock64();                           \
+    if ((threadIdx.x & 63) == 0 && g_attn_trace != nullptr) {                                   \
+      long long* tp = g_attn_trace +                                                            \
+          (((long)blockIdx.z * gridDim.y + blockIdx.y) * gridDim.x + blockIdx.x) * 32 +         \
+          (threadIdx.x >> 6) * 8;                                                               \
+      _Pragma("unroll") for (int i_ = 0; i_ < 8; ++i_) tp[i_] = atr_[i_];                       \
+    }                                                                                           \
   } while (0)
 EIA_API int eia_attn_set_trace(void* p) {
   return (int)hipMemcpyToSymbol(HIP_SYMBOL(g_attn_trace), &p, sizeof(p));
 }
 #else
+#define ATRACE_DECL
 #define ATRACE(slot) \
   do {               \
+  } while (0)
+#define ATRACE_FLUSH() \
+  do {                 \
   } while (0)
 #endif
 
@@ -267,25 +278,27 @@ EIA_DEV void compute_unit(WaveAcc<D>& acc, const bf16x8 (&qf)[D / 32], const KVF
 // bases are wave-uniform (one scalar block-table read) and each lane adds a CONSTANT 32-bit
 // byte offset, so the loads take the SGPR-base + VGPR-offset form -- no per-unit 64-bit
 // per-lane pointers held in VGPRs.
-// `pre_issue` puts the prologue's loads in flight right behind the first unit's, and `pre` runs
-// once per wave after them (every wave calls both, also those without units): the fused decode
-// prologue (RoPE, KV write, q -> LDS, barrier) then overlaps the first K/V fetch.  The order
-// matters: the unit's bases wait (vmcnt, in-order) for the block-table window load, which must
-// not sit behind the prologue's slab loads (profiles/attn_trace_r3.md: 6 us of entry latency).  Token `tnew` (this step's, -1: none) is taken from
+// `pre_issue` puts the prologue's loads in flight ahead of the first unit's (vmcnt retires in
+// issue order, so the prologue then waits for its own loads only), and `pre` runs once per wave
+// between the first unit's loads and the loop (every wave calls both, also those without
+// units): the fused decode prologue (RoPE, KV write, q -> LDS, barrier) overlaps the first K/V
+// fetch.  The unit bases come from scalar block-table loads, so nothing vector-loaded is waited
+// for before the K/V loads issue.  Token `tnew` (this step's, -1: none) is taken from
 // knew / vnew in LDS instead of the cache: its K/V stores may still be in flight when the unit
 // holding it is read, so those lanes' fragments are patched after the loads land.
 template <int D, typename PreIssue, typename Pre>
 EIA_DEV void attn_units_lean(WaveAcc<D>& acc, const bf16x8 (&qs)[D / 32][64],
                              const bf16_t* __restrict__ kc, const bf16_t* __restrict__ vc,
-                             const int* __restrict__ bt, int bt_win, int ub, int ue, int w, int L,
+                             const int* __restrict__ bt, int bt0, int bt1, int ub, int ue, int w,
+                             int L,
                              int kvh,
                              int Hkv, int bs, float scale_log2, int kv_lo, int NW,
                              PreIssue&& pre_issue, Pre&& pre, int tnew, const bf16_t* knew,
                              const bf16_t* vnew) {
   // the unit index is wave-uniform; say so, or the per-unit bases become 64-bit VGPR pointers
   int u = __builtin_amdgcn_readfirstlane(ub + w);
+  pre_issue();
   if (u >= ue) {
-    pre_issue();
     pre();
     return;
   }
@@ -299,7 +312,7 @@ EIA_DEV void attn_units_lean(WaveAcc<D>& acc, const bf16x8 (&qs)[D / 32][64],
   auto bases = [&](int uu, const char*& kb, const char*& vb) {
     const int tb = 32 * uu;
     const int bi = __builtin_amdgcn_readfirstlane(tb / bs);
-    const int blk = bi < 64 ? __builtin_amdgcn_readlane(bt_win, bi) : bt[bi];
+    const int blk = bi == 0 ? bt0 : (bi == 1 ? bt1 : bt[bi]);
     const long base = ((long)blk * Hkv + kvh) * hk;
     const int o = __builtin_amdgcn_readfirstlane(tb % bs);
     kb = reinterpret_cast<const char*>(kc + base + (long)o * D);
@@ -324,8 +337,6 @@ EIA_DEV void attn_units_lean(WaveAcc<D>& acc, const bf16x8 (&qs)[D / 32][64],
     ldk(ka0, ka1, kbp);
     ldv(va, vbp);
   }
-  ATRACE(7);
-  pre_issue();
   pre();
   // lanes holding token tnew of unit uc take it from LDS (wave-uniform test)
   auto patch = [&](bf16x8 (&k0)[D / 32], bf16x8 (&k1)[D / 32], bf16x8 (&v)[D / 16], int uc) {
@@ -457,6 +468,7 @@ paged_decode_kernel(const bf16_t* __restrict__ q, long q_stride,
   const int b = blockIdx.x;
   const int kvh = blockIdx.y / NQG, qg = blockIdx.y % NQG;
   const int p = blockIdx.z;
+  ATRACE_DECL;
   ATRACE(0);
   // partitions actually used this call: a HIP graph is captured with grid.z = Pmax and the
   // host writes the step's P (from the batch's longest context) into device memory, so one
@@ -464,23 +476,24 @@ paged_decode_kernel(const bf16_t* __restrict__ q, long q_stride,
   // slowest dispatch dimension, so they trail the real work)
   // The step's P, L and the fused prologue's scalars are independent loads: issued together
   // (one round trip), the surplus-workgroup exit test after them.
-  const int pd = *(p_dyn != nullptr ? p_dyn : seq_lens);   // unconditional: no wait in a branch
+  const int* bt = block_tables + (long)b * bt_stride;
+  const int* pdp = p_dyn != nullptr ? p_dyn : seq_lens;
   const int L = seq_lens[b];
+  // The row's first two block-table entries (every unit of a context <= 2 blocks), scalar loads
+  // beside L: the first units' K/V bases then need no load that waits for L (the entry chain was
+  // kernel args -> L -> block table -> K/V; profiles/attn_trace_r3.md).  A lane-indexed vector
+  // window measured ~4 us slower to arrive than these scalar loads.
+  const int bt0 = bt[0];
+  const int bt1 = bt[bt_stride > 1 ? 1 : 0];
   const int pos_b = FUSED ? rope.positions[b] : 0;
   const int slot_b = FUSED ? rope.slot_mapping[b] : -1;
+  const int pd = *pdp;                                   // unconditional: no wait in a branch
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int c = lane & 15, g = lane >> 4;
-  const int* bt = block_tables + (long)b * bt_stride;
-  // Block-table window: entries [0, 64) of this sequence's row, one per lane, loaded beside L so
-  // the first units' K/V bases need no scalar load that waits for L (the entry chain was
-  // kernel args -> L -> block table -> K/V, three cold round trips before the first K/V byte;
-  // profiles/attn_trace_r3.md).  Entries past the row's live blocks are read, never used.
-  int bt_win = 0;
-  if constexpr (LEAN) bt_win = lane < bt_stride ? bt[lane] : 0;
   const int P = p_dyn != nullptr ? max(1, min(pd, Pmax)) : Pmax;
   // (L | pos | slot + 1) < 0 never holds; testing it keeps the compiler from sinking those loads past the
   // exit branch, which would serialise them behind the p_dyn round trip
-  if ((p >= P) | ((L | pos_b | (slot_b + 1)) < 0)) return;   // no short-circuit
+  if ((p >= P) | ((L | pos_b | (slot_b + 1) | bt0 | bt1) < 0)) return;   // no short-circuit
   ATRACE(6);
   const int G = Hq / Hkv;
   const int hq0 = kvh * G + qg * 16;
@@ -629,7 +642,7 @@ paged_decode_kernel(const bf16_t* __restrict__ q, long q_stride,
   const int ue = min(U0 + U, A0 + 2 * (int)(((long)(p + 1) * npair) / P));
   if constexpr (LEAN) {
     if constexpr (FUSED) {
-      attn_units_lean<D>(acc, qs, kc, vc, bt, bt_win, ub, ue, w, L, kvh, Hkv, bs, scale_log2,
+      attn_units_lean<D>(acc, qs, kc, vc, bt, bt0, bt1, ub, ue, w, L, kvh, Hkv, bs, scale_log2,
                          kv_lo, NW, pro_issue, prologue, writer && L > 0 ? L - 1 : -1, knew, vnew);
       ATRACE(3);
     } else {
@@ -638,7 +651,7 @@ paged_decode_kernel(const bf16_t* __restrict__ q, long q_stride,
         for (int s = 0; s < D / 32; ++s) qs[s][lane] = qf[s];
       }
       __syncthreads();
-      attn_units_lean<D>(acc, qs, kc, vc, bt, bt_win, ub, ue, w, L, kvh, Hkv, bs, scale_log2,
+      attn_units_lean<D>(acc, qs, kc, vc, bt, bt0, bt1, ub, ue, w, L, kvh, Hkv, bs, scale_log2,
                          kv_lo, NW, [] {}, [] {}, -1, nullptr, nullptr);
     }
   } else
@@ -685,6 +698,7 @@ paged_decode_kernel(const bf16_t* __restrict__ q, long q_stride,
     }
   }
   ATRACE(5);
+  ATRACE_FLUSH();
   if (P == 1 || part_cnt == nullptr) return;
   // Fused partition merge: the last of the P workgroups of this (b, kv head, q group) merges
   // the partials (no separate reduce launch).  No __threadfence(): an agent-scope fence
@@ -932,6 +946,7 @@ paged_decode_wave_kernel(const bf16_t* __restrict__ q, long q_stride, const bf16
   __shared__ __align__(16) bf16_t knew[D], vnew[D];
   __shared__ int s_last;
   const int b = blockIdx.x, kvh = blockIdx.y, p = blockIdx.z;
+  ATRACE_DECL;
   ATRACE(0);
   const int lane = threadIdx.x;
   const int c = lane & 15, g = lane >> 4;
@@ -1047,6 +1062,7 @@ paged_decode_wave_kernel(const bf16_t* __restrict__ q, long q_stride, const bf16
       }
     }
     ATRACE(5);
+    ATRACE_FLUSH();
     return;
   }
   if (valid) {

@@ -6,8 +6,8 @@ Loads ``enterprise_inference_amd/_lib/libeia_attn_trace.so`` -- attention.hip bu
 eia_paged_decode_rope call after a 512 MB read sweep (cold Infinity Cache, as in the engine)
 and prints, per trace slot, when the waves reach it (us after the first wave started) and the
 per-wave phase durations:
-  0 entry, 6 entry loads (L, P, position, slot) arrived, 7 first K/V unit loads issued,
-  1 prologue entered, 2 prologue done (barrier), 3 unit loop done, 4 cross-wave merge barrier
+  0 entry, 6 entry loads (L, P, position, slot) arrived, 1 prologue entered (the first unit's
+  K/V loads issued), 2 prologue done (barrier), 3 unit loop done, 4 cross-wave merge barrier
   passed, 5 output written."""
 import argparse
 import ctypes
@@ -86,7 +86,7 @@ def main():
     t = trace.view(B * hkv, 4, 8).cpu().double() / 100.0   # 100 MHz ticks -> us
     t0 = t[:, :, 0][t[:, :, 0] > 0].min()
     names = ["entry", "prologue in", "prologue out", "units done", "merge barrier", "stored",
-             "L arrived", "K/V issued"]
+             "L arrived", "-"]
     print(f"B {B} ctx {L} sk {a.sk}: {B * hkv} workgroups x 4 waves, cold ({a.flush_mb} MB sweep)")
     for sl_ in range(8):
         x = t[:, :, sl_].flatten()
@@ -95,7 +95,7 @@ def main():
             q = torch.quantile(x, torch.tensor([0.0, 0.5, 0.9, 1.0], dtype=torch.float64))
             print(f"  slot {sl_} {names[sl_]:>14}: min {q[0]:6.2f}  p50 {q[1]:6.2f}  p90 {q[2]:6.2f}"
                   f"  max {q[3]:6.2f} us")
-    for a_, b_ in ((0, 6), (6, 7), (7, 1), (1, 2), (2, 3), (3, 4), (4, 5), (0, 5)):
+    for a_, b_ in ((0, 6), (6, 1), (1, 2), (2, 3), (3, 4), (4, 5), (0, 5)):
         ok = (t[:, :, a_] > 0) & (t[:, :, b_] > 0)
         dlt = (t[:, :, b_] - t[:, :, a_])[ok]
         if dlt.numel():
