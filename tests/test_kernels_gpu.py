@@ -502,3 +502,36 @@ def test_paged_prefill_fa_long_and_windowed(sw, ch):
     r = ref.paged_attention_prefill(q.cpu().float(), k.cpu().float(), v.cpu().float(), bt.cpu(),
                                     cu.cpu(), sl.cpu(), D ** -0.5, True, sw, ch)
     _close(o, r, 2e-2, 2e-2, f"prefill fa sw={sw} chunk={ch}")
+
+
+# ----------------------------------------------------------------------------- MALL prefetch
+
+def test_mall_prefetch_fork_join_in_graph():
+    """The Infinity Cache sweep (csrc/kernels/prefetch.hip) on a side-stream branch of a HIP
+    graph: forked after a producer, joined before a consumer, results unchanged; odd sizes
+    (not a multiple of the unrolled stride) and a byte prefix are covered."""
+    from enterprise_inference_amd.ops import prefetch
+    w = torch.randn(4099, 1024, device=DEV, dtype=BF)
+    x = torch.randn(8, 1024, device=DEV, dtype=BF)
+    expect = x.float() @ w.float().t()
+
+    def body():
+        y = x * 1.0                                  # producer on the main stream
+        join = prefetch.fork([(w, None), (w, 12345 * 16)])
+        y = y + 0.0
+        join()
+        return y.float() @ w.float().t()             # consumer after the join
+    body()
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        body()
+        with torch.cuda.graph(g, stream=s):
+            out = body()
+    torch.cuda.current_stream().wait_stream(s)
+    for _ in range(3):
+        g.replay()
+    torch.cuda.synchronize()
+    _close(out, expect, 1e-2, 1e-3, "prefetch fork/join")
