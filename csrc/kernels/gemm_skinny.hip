@@ -652,6 +652,18 @@ int launch_mt(int cfg, const bf16_t* X, long ldx, const bf16_t* W, long ldw, con
       }
 #undef EIA_GL
     }
+    if (cfg & 512) {   // 3 waves: Llama-8B QKV (6144 rows = 64 x 96, x split-K 4 = 256 workgroups)
+      switch (cfg & 31) {
+        case 0: EIA_CFG(1, 3, 2, 256);
+        case 1: EIA_CFG(2, 3, 2, 256);
+        case 4: EIA_CFG(1, 3, 3, 256);
+        case 16: EIA_CFG(1, 3, 2, 128);
+        case 17: EIA_CFG(2, 3, 2, 128);
+        case 20: EIA_CFG(1, 3, 3, 128);
+        case 21: EIA_CFG(2, 3, 3, 128);
+        default: return EIA_BAD_SHAPE;
+      }
+    }
     if (cfg & 256) {   // 7 waves x (gate, up) pairs: 1792 pairs = 256 workgroups (70B gate_up)
       if constexpr (MT <= 4) {
         if (cfg == 256 + 17) EIA_CFG(2, 7, 2, 128);
@@ -745,9 +757,14 @@ int dispatch_mt(int mt, int cfg, const bf16_t* x, long ldx, const bf16_t* w, lon
 constexpr unsigned long long kSpillCfg[9] = {0x0ull, 0x8000a00ull, 0x8000a20ull, 0x8800ba0ull, 0x80000000e800bb0ull, 0x44400000ec00fb2ull, 0x80000000ee80fb2ull, 0x88000000fe80ff3ull, 0xccc00000ff80ffbull};
 
 int check_shape(int N, int K, int sk, int mode, int cfg) {
-  const int nt = (cfg & 1) ? 2 : 1, waves = (cfg & 256) ? 7 : (cfg & 2) ? 4 : 2;
+  const int nt = (cfg & 1) ? 2 : 1;
+  const int waves = (cfg & 512) ? 3 : (cfg & 256) ? 7 : (cfg & 2) ? 4 : 2;
   const int kc = (cfg & 16) ? 128 : 256;
-  if (sk < 1 || cfg < 0 || (cfg & ~(16 | 32 | 64 | 128 | 256)) > 11 || K % (sk * kc) != 0) return EIA_BAD_SHAPE;
+  if (sk < 1 || cfg < 0 || (cfg & ~(16 | 32 | 64 | 128 | 256 | 512)) > 11 || K % (sk * kc) != 0)
+    return EIA_BAD_SHAPE;
+  // 3-wave form: register-staged, plain layout, no SwiGLU pairing, 2-3 stages
+  if ((cfg & 512) && ((cfg & (2 | 8 | 32 | 64 | 128 | 256)) || mode == MODE_SWIGLU))
+    return EIA_BAD_SHAPE;
   // 7-wave form: SwiGLU pairs only, register-staged, plain layout
   if ((cfg & 256) && (mode != MODE_SWIGLU || !(cfg & 1) || (cfg & (2 | 8 | 32 | 64 | 128))))
     return EIA_BAD_SHAPE;
@@ -774,12 +791,15 @@ int check_shape(int N, int K, int sk, int mode, int cfg) {
 // bit 7 -> LDS-DMA ring kernel (with bits 1 and 4; bits 2-3 = ring depth - 2)
 // bit 8 -> 7 waves of (gate, up) pairs per workgroup (SwiGLU only; cfg 273 = + bits 0 and 4):
 //          70B's 1792 pairs are exactly 256 workgroups, where 4-wave workgroups leave 448
+// bit 9 -> 3 waves per workgroup (+ bits 0, 2, 4): Llama-8B's QKV (6144 rows) as 64 x 96-row
+//          tiles x split-K 4 = 256 workgroups, where 4-wave (128-row) tiles leave 192 -- a
+//          decode GEMM streams at a per-CU rate (~20 GB/s), so idle CUs are lost bandwidth
 EIA_API int eia_gemm_skinny(const void* X, long ldx, const void* W, long ldw, const void* bias,
                             void* out, long ldo, int M, int N, int K, int sk, int mode, int cfg,
                             hipStream_t st) {
   if (M < 1 || M > 128) return EIA_BAD_SHAPE;
   if (int rc = check_shape(N, K, sk, mode, cfg)) return rc;
-  if (!(cfg & 384) && ((kSpillCfg[(M + 15) / 16] >> (cfg & 63)) & 1ull)) return EIA_BAD_SHAPE;
+  if (!(cfg & 896) && ((kSpillCfg[(M + 15) / 16] >> (cfg & 63)) & 1ull)) return EIA_BAD_SHAPE;
   // 7-wave form: cfg 273 only (KC 128, 2 stages), spill-free up to 4 row tiles (M <= 64); at
   // 7 waves two share a SIMD, so the register budget is 256
   if ((cfg & 256) && (cfg != 256 + 17 || M > 64)) return EIA_BAD_SHAPE;

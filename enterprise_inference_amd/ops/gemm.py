@@ -37,8 +37,10 @@ MODE_BF16, MODE_SPLIT, MODE_SWIGLU = 0, 1, 2
 # bit0 NT=2, bit1 WAVES=4, bits2-3 pipeline stages-2, bit4 128-deep K chunks (else 256)
 # bit5: an extra wave stages X into LDS (4 compute waves, KC 128): 50, 51, 54, 55, 58, 59
 # bit8: 7 waves of (gate, up) pairs per workgroup, SwiGLU only: 273 (KC 128, 2 stages, M <= 64)
+# bit9: 3 waves per workgroup (QKV-shaped N = 96 k): 512 + (0, 1, 4, 16, 17, 20, 21)
+THREE_WAVE_CFGS = tuple(512 + c for c in (0, 1, 4, 16, 17, 20, 21))
 CFGS = tuple(range(12)) + tuple(range(16, 28)) + (50, 51, 54, 55, 58, 59) + \
-    (146, 147, 150, 151, 154, 155) + (273,)
+    (146, 147, 150, 151, 154, 155) + (273,) + THREE_WAVE_CFGS
 # bit6: tile-packed weights (pack_weight) for the layouts the decode tables use
 PACKED_CFGS = tuple(64 + c for c in (1, 2, 3, 7, 17, 18, 19, 22, 23, 51, 55, 146, 147, 150, 151, 154, 155))
 # bit7: LDS-DMA ring kernel, 4 waves, KC 128: 146 | (NT-1) | (depth-2) << 2 (+64 packed)
@@ -55,7 +57,7 @@ def cfg_kc(cfg: int) -> int:
 
 
 def cfg_waves(cfg: int) -> int:
-    return 7 if cfg & 256 else (4 if cfg & 2 else 2)
+    return 3 if cfg & 512 else (7 if cfg & 256 else (4 if cfg & 2 else 2))
 
 
 def cfg_rows(cfg: int) -> int:
@@ -90,6 +92,8 @@ SPILL_CFGS = {1: (9, 11, 27), 2: (5, 9, 11, 27), 3: (5, 7, 8, 9, 11, 23, 27), 4:
 def valid(N: int, K: int, swiglu: bool, cfg: int, sk: int, M: Optional[int] = None) -> bool:
     if K % (sk * cfg_kc(cfg)):
         return False
+    if cfg & 512:   # 3-wave form: plain GEMMs only
+        return not swiglu and N % cfg_rows(cfg) == 0
     if cfg & 256:   # 7-wave SwiGLU form: cfg 273 only, spill-free up to M = 64
         return (swiglu and cfg == 273 and sk == 1 and (M is None or M <= 64)
                 and (N // 2) % (7 * 16) == 0)
