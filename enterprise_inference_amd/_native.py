@@ -46,6 +46,7 @@ _SIGNATURES = {
     "eia_paged_prefill_fa": [P, L, P, L, P, P, IP, I, IP, IP, IP, I, F, I, I, I, I, I, I, I, S],
     "eia_act_and_mul": [P, P, I, I, L, L, I, S],
     "eia_mall_prefetch": [P, L, I, P, S],
+    "eia_gemm_swiglu_balanced": [P, L, P, L, P, L, I, I, I, P, P, S],
     "eia_act": [P, P, L, I, S],
     "eia_sample": [P, L, I, I, P, P, P, P, P, P, S],
     "eia_apply_penalties": [P, L, P, P, P, I, P, P, P, S],

@@ -128,6 +128,9 @@ def main():
                                   "note": "tuned table routes this shape to hipBLASLt"}), flush=True)
                 continue
             results = []
+            if swiglu and gemm.balanced_ok(M, N, K) and not a.packed:
+                fb = lambda i: gemm.swiglu_balanced(x, ws[i % pool])
+                results.append((graph_time(fb, a.iters), "balanced", 1))
             for cfg, sk in cands:
                 if swiglu:
                     f = lambda i, cfg=cfg: gemm.swiglu_gemm(
@@ -136,7 +139,7 @@ def main():
                     f = lambda i, cfg=cfg, sk=sk: gemm.skinny(
                         x, (wps if cfg & 64 else ws)[i % pool], cfg=cfg, sk=sk)
                 results.append((graph_time(f, a.iters), cfg, sk))
-            results.sort()
+            results.sort(key=lambda r_: r_[0])
             to, cfg, sk = results[0]
             r = {"shape": name, "M": M, "N": N, "K": K, "cfg": cfg, "sk": sk,
                  "ours_us": round(to, 2), "hipblaslt_us": round(tb, 2),
@@ -147,6 +150,8 @@ def main():
                 r["all"] = [(round(t, 1), c, s) for t, c, s in results]
             print(json.dumps(r), flush=True)
             if a.tune:
+                results = [r_ for r_ in results if r_[1] != "balanced"] or results
+                to, cfg, sk = results[0]
                 key = f"{gemm.m_bucket(M)},{N},{K},{int(swiglu)}"
                 # cfg -1 = "use hipBLASLt" (the skinny kernel lost on this shape)
                 tuned[key] = [cfg, sk] if to < tb * 1.02 else [-1, 1]

@@ -85,6 +85,44 @@ def test_swiglu_gemm(M, I, K):
             _check(gemm.swiglu_gemm(x, w, cfg=cfg), ref, f"swiglu M={M} I={I} cfg={cfg}")
 
 
+@pytest.mark.parametrize("M,I,K", [(1, 14336, 4096), (16, 14336, 4096), (33, 14336, 4096),
+                                   (64, 14336, 4096), (65, 14336, 4096), (80, 14336, 4096),
+                                   (35, 28672, 8192)])
+def test_swiglu_balanced(M, I, K):
+    """Half-pair balanced SwiGLU (csrc/kernels/gemm_swiglu_balanced.hip): in-workgroup LDS
+    combine and the cross-workgroup ticket hand-off of straddling pairs vs fp32, twice in a row
+    (the tickets must come back to zero) and inside a HIP graph replayed three times."""
+    from enterprise_inference_amd.ops import gemm
+    torch.manual_seed(M + I)
+    x = torch.randn(M, K, device=DEV, dtype=BF)
+    w = (torch.randn(2 * I, K, device=DEV) * K ** -0.5).to(BF)
+    old, gemm.BALANCED = gemm.BALANCED, True
+    try:
+        assert gemm.balanced_ok(M, 2 * I, K)
+    finally:
+        gemm.BALANCED = old
+    y = _ref(x, w)
+    ref = F.silu(y[:, :I]) * y[:, I:]
+    a = gemm.swiglu_balanced(x, w)
+    b = gemm.swiglu_balanced(x, w)
+    _check(a, ref, f"balanced M={M} I={I}")
+    assert torch.equal(a, b), "balanced SwiGLU not deterministic across calls"
+    _, ticket = gemm._balanced_scratch(x.device, I)
+    torch.cuda.synchronize()
+    assert int(ticket.abs().sum()) == 0, "tickets not reset"
+    g = torch.cuda.CUDAGraph()
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        with torch.cuda.graph(g, stream=s):
+            c = gemm.swiglu_balanced(x, w)
+    torch.cuda.current_stream().wait_stream(s)
+    for _ in range(3):
+        g.replay()
+    torch.cuda.synchronize()
+    assert torch.equal(a, c), "balanced SwiGLU differs under graph replay"
+
+
 @pytest.mark.parametrize("M", [1, 35, 64])
 def test_swiglu_7wave_70b(M):
     """7-wave SwiGLU form (cfg 273) at Llama-70B's single-GPU gate_up shape (1792 pairs = 256
