@@ -122,7 +122,9 @@ class LlamaDecoderLayer(nn.Module):
             h = self.input_layernorm(h)
         else:
             h, residual = self.input_layernorm(h, residual)
-        h = self.self_attn(h, md, kv, prefetch=self._prefetch_ranges(h, md))
+        pf = self._prefetch_ranges(h, md)
+        # (attention subclasses, e.g. Llama-4's, take no prefetch hook)
+        h = self.self_attn(h, md, kv, prefetch=pf) if pf else self.self_attn(h, md, kv)
         h, residual = self.post_attention_layernorm(h, residual)
         return self.mlp(h), residual
 
