@@ -209,9 +209,10 @@ class ModelRunner:
         self.d_g_hdr = torch.zeros(self.hdr_len, dtype=torch.int32, device=dev)
         self.d_g_bt = torch.zeros(S * mb, dtype=torch.int32, device=dev)
         self.d_e_buf = torch.zeros(self.e_size, dtype=torch.int32, device=dev)
-        self.d_s_f32 = torch.zeros(3 * S, dtype=torch.float32, device=dev)
-        self.d_s_i32 = torch.zeros(S, dtype=torch.int32, device=dev)
-        self.d_s_i64 = torch.zeros(S, dtype=torch.int64, device=dev)
+        # per-row sampling parameters, one region (one H2D copy per step): temp|top_p|min_p
+        # (f32 [3S]), top_k (i32 [S]), seeds (i64 [S], 8-B aligned at word 4S)
+        self.d_s_all = torch.zeros(6 * S, dtype=torch.int32, device=dev)
+        self.d_s_f32, self.d_s_i32, self.d_s_i64 = self._sampling_views(self.d_s_all)
         # sampled tokens of the last launched step (device) + their host copies
         self.d_tok = torch.zeros(S, dtype=torch.int32, device=dev)
         self.h_tok = [torch.zeros(S, dtype=torch.int32, pin_memory=pin) for _ in range(2)]
@@ -225,15 +226,22 @@ class ModelRunner:
         self.part_cnt = torch.zeros(S * self.num_heads, dtype=torch.int32,
                                     device=dev) if self.is_gpu else None
 
+    def _sampling_views(self, buf: torch.Tensor):
+        S = self.max_num_seqs
+        return (buf[:3 * S].view(torch.float32), buf[3 * S:4 * S], buf[4 * S:6 * S].view(torch.int64))
+
     def _pinned_set(self, pin: bool) -> Dict[str, torch.Tensor]:
         S, mb = self.max_num_seqs, self.maxb
+        s_all = torch.zeros(6 * S, dtype=torch.int32, pin_memory=pin)
+        s_f32, s_i32, s_i64 = self._sampling_views(s_all)
         return {
             "g_hdr": torch.zeros(self.hdr_len, dtype=torch.int32, pin_memory=pin),
             "g_bt": torch.zeros(S * mb, dtype=torch.int32, pin_memory=pin),
             "e_buf": torch.zeros(self.e_size, dtype=torch.int32, pin_memory=pin),
-            "s_f32": torch.zeros(3 * S, dtype=torch.float32, pin_memory=pin),   # temp|top_p|min_p
-            "s_i32": torch.zeros(S, dtype=torch.int32, pin_memory=pin),         # top_k
-            "s_i64": torch.zeros(S, dtype=torch.int64, pin_memory=pin),         # seeds
+            "s_all": s_all,
+            "s_f32": s_f32,   # temp|top_p|min_p
+            "s_i32": s_i32,   # top_k
+            "s_i64": s_i64,   # seeds
         }
 
     def _use_pinned(self, k: int) -> None:
@@ -746,9 +754,7 @@ class ModelRunner:
     def _sampling_tensors(self, n: int):
         S = self.max_num_seqs
         if self.is_gpu:
-            self.d_s_f32.copy_(self.s_f32, non_blocking=True)
-            self.d_s_i32[:n].copy_(self.s_i32[:n], non_blocking=True)
-            self.d_s_i64[:n].copy_(self.s_i64[:n], non_blocking=True)
+            self.d_s_all.copy_(self.s_all, non_blocking=True)     # one 24*S-byte copy
             F_, K_, SD = self.d_s_f32, self.d_s_i32, self.d_s_i64
         else:
             F_, K_, SD = self.s_f32, self.s_i32, self.s_i64
