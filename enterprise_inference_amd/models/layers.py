@@ -301,6 +301,15 @@ class ParallelLMHead(nn.Module):
     def forward(self, h: torch.Tensor) -> torch.Tensor:
         return self.gather(self.forward_local(h))
 
+    def forward_f32(self, h: torch.Tensor) -> torch.Tensor:
+        """fp32 logits [T, vocab]: one rank, unpadded vocabulary and a decode-sized batch write
+        them from the GEMM's fp32 accumulators (no bf16 round trip, no conversion kernel)."""
+        if state.tp_size() == 1 and self.per_rank == self.vocab:
+            out = gemm.linear_f32(h, self.weight)
+            if out is not None:
+                return out
+        return self.forward(h).float()
+
 
 class RMSNorm(nn.Module):
     def __init__(self, dim: int, eps: float, dtype=torch.bfloat16, device=None):

@@ -182,7 +182,7 @@ class LlamaForCausalLM(nn.Module):
         return h
 
     def compute_logits(self, h: torch.Tensor) -> torch.Tensor:
-        return self.lm_head(h).float()
+        return self.lm_head.forward_f32(h)
 
     def compute_logits_local(self, h: torch.Tensor) -> torch.Tensor:
         """TP: this rank's vocab shard of the logits (model dtype, no gather)."""

@@ -256,6 +256,23 @@ def swiglu_balanced(x: torch.Tensor, w_gate_up: torch.Tensor) -> torch.Tensor:
     return out
 
 
+def linear_f32(x: torch.Tensor, w: torch.Tensor) -> Optional[torch.Tensor]:
+    """x @ w^T with fp32 output straight from the skinny kernel's accumulators (the LM head:
+    the sampler reads fp32 logits, so this skips the bf16 store and the separate bf16 -> fp32
+    conversion kernel).  None when the shape does not run the skinny kernel without split-K."""
+    if x.dim() != 2 or not skinny_ok(x, w):
+        return None
+    M, K = x.shape
+    N = w.shape[0]
+    cfg, sk = choose(M, N, K, False)
+    if sk != 1:
+        return None
+    out = torch.empty(M, N, dtype=torch.float32, device=x.device)
+    check(lib().eia_gemm_skinny(ptr(x), x.stride(0), ptr(w), w.stride(0), None, ptr(out), N, M, N,
+                                K, 1, MODE_SPLIT, cfg, stream(x)), "gemm_skinny_f32")
+    return out
+
+
 def swiglu_gemm(x: torch.Tensor, w_gate_up: torch.Tensor, cfg: Optional[int] = None) -> torch.Tensor:
     """silu(x Wg^T) * (x Wu^T) with W = [gate; up] stacked on dim 0 (K7)."""
     M, K = x.shape
