@@ -458,16 +458,43 @@ paged_decode_kernel(const bf16_t* __restrict__ q, long q_stride,
                     int* __restrict__ part_cnt,
                     float scale_log2, int Hq, int Hkv, int bs, int Pmax, int NQG,
                     int sliding_window, int chunk_size, const int* __restrict__ p_dyn,
-                    DecodeRope rope) {
+                    const int* __restrict__ tail, DecodeRope rope) {
   constexpr int NW = 4;
   __shared__ int s_last;
   __shared__ float sm[NW][16];
   __shared__ float sl[NW][16];
   __shared__ __align__(16) float so[NW][D][17];
 
-  const int b = blockIdx.x;
-  const int kvh = blockIdx.y / NQG, qg = blockIdx.y % NQG;
-  const int p = blockIdx.z;
+  // Tail split (`tail` = device int (row << 8) | parts, needs part_cnt): rows >= `row` of a P-1
+  // step are split over `parts` partitions (grid.z >= parts) and merged in-kernel.  A grid of
+  // 2 workgroups per CU plus a few (B 65 x 8 KV heads = 520 on 256 CUs) puts a third whole item
+  // on some CUs, which then finish ~1.5x later than the rest (profiles/attn_batch_balance_r3.md);
+  // split, the surplus rows add only light pieces.  The dispatch order is remapped: partition 0
+  // of every item first, row-major (all heads of a row adjacent), so the whole-item rows
+  // dispatch first, two per CU; then partitions >= 1 from the LAST row down, so the tail rows'
+  // pieces dispatch right behind (instead of after a whole grid.z slice of workgroups that exit
+  // at once) and fill third slots.
+  int b, yb, p;
+  if (tail != nullptr) {
+    const int X = gridDim.x, Y = gridDim.y;
+    const int lin = blockIdx.x + X * (blockIdx.y + Y * blockIdx.z);
+    if (lin < X * Y) {
+      b = lin / Y;
+      yb = lin - b * Y;
+      p = 0;
+    } else {
+      const int e = lin - X * Y, R = Y * ((int)gridDim.z - 1);
+      const int r = e / R, rem = e - r * R;
+      b = X - 1 - r;
+      p = 1 + rem / Y;
+      yb = rem - (p - 1) * Y;
+    }
+  } else {
+    b = blockIdx.x;
+    yb = blockIdx.y;
+    p = blockIdx.z;
+  }
+  const int kvh = yb / NQG, qg = yb % NQG;
   ATRACE_DECL;
   ATRACE(0);
   // partitions actually used this call: a HIP graph is captured with grid.z = Pmax and the
@@ -488,12 +515,18 @@ paged_decode_kernel(const bf16_t* __restrict__ q, long q_stride,
   const int pos_b = FUSED ? rope.positions[b] : 0;
   const int slot_b = FUSED ? rope.slot_mapping[b] : -1;
   const int pd = *pdp;                                   // unconditional: no wait in a branch
+  const int tv = *(tail != nullptr ? tail : pdp);
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int c = lane & 15, g = lane >> 4;
-  const int P = p_dyn != nullptr ? max(1, min(pd, Pmax)) : Pmax;
-  // (L | pos | slot + 1) < 0 never holds; testing it keeps the compiler from sinking those loads past the
-  // exit branch, which would serialise them behind the p_dyn round trip
-  if ((p >= P) | ((L | pos_b | (slot_b + 1) | bt0 | bt1) < 0)) return;   // no short-circuit
+  const int Pstep = p_dyn != nullptr ? max(1, min(pd, Pmax)) : Pmax;
+  const int trow = tail != nullptr && part_cnt != nullptr ? (tv >> 8) : 0x7fffffff;
+  // a split row takes at most one partition per 64-token pair (the partition boundaries below)
+  const int P = (Pstep == 1) & (b >= trow) & (L > 0)
+                    ? max(1, min(min(tv & 255, Pmax), ((L + 31) / 32 + 1) / 2))
+                    : Pstep;
+  // (L | pos | slot + 1 | tv) < 0 never holds; testing it keeps the compiler from sinking those
+  // loads past the exit branch, which would serialise them behind the p_dyn round trip
+  if ((p >= P) | ((L | pos_b | (slot_b + 1) | bt0 | bt1 | tv) < 0)) return;   // no short-circuit
   ATRACE(6);
   const int G = Hq / Hkv;
   const int hq0 = kvh * G + qg * 16;
@@ -1488,7 +1521,7 @@ EIA_API int eia_paged_decode(const void* q, long q_stride, const void* k_cache, 
                      0, st, (const bf16_t*)q, q_stride, (const bf16_t*)k_cache,                \
                      (const bf16_t*)v_cache, block_tables, bt_stride, seq_lens, (bf16_t*)out,     \
                      out_stride, part_o, part_ml, part_cnt, sl2, Hq, Hkv, bs, P, NQG,             \
-                     sliding_window, chunk_size, p_dyn, none);
+                     sliding_window, chunk_size, p_dyn, nullptr, none);
 #define DEC(DD)                                                                             \
   if (lean) { DEC_V(DD, true) } else { DEC_V(DD, false) }                                  \
   if (P > 1 && part_cnt == nullptr)                                                         \
@@ -1509,7 +1542,8 @@ EIA_API int eia_paged_decode(const void* q, long q_stride, const void* k_cache, 
 // GEMM output of T >= B rows (split-K slabs `part` [sk][T][(Hq+2Hkv)*D], or bf16 rows `qkv`),
 // this step's k/v land in the cache, out [B][Hq*D] receives the attention.  NEOX RoPE only.
 // Returns EIA_UNSUPPORTED for shapes the fused form does not cover (the caller then runs the
-// two kernels).
+// two kernels).  `tail` (device int, (row << 8) | parts; used when P > 1 and part_cnt is given):
+// the tail split of paged_decode_kernel for steps whose p_dyn is 1.
 EIA_API int eia_paged_decode_rope(const void* qkv, long qkv_stride, const float* part, int sk,
                                   const void* bias, const void* q_norm_w, const void* k_norm_w,
                                   float eps, const int* positions, const float* cos_sin,
@@ -1518,7 +1552,7 @@ EIA_API int eia_paged_decode_rope(const void* qkv, long qkv_stride, const float*
                                   void* out, long out_stride, float* part_o, float* part_ml,
                                   int* part_cnt, float scale, int B, int Hq, int Hkv, int D, int bs,
                                   int P, int sliding_window, int chunk_size, const int* p_dyn,
-                                  hipStream_t st) {
+                                  const int* tail, hipStream_t st) {
   if (B < 0 || B > T || Hkv <= 0 || Hq % Hkv != 0 || P < 1) return EIA_BAD_SHAPE;
   if (P > 1 && (part_o == nullptr || part_ml == nullptr)) return EIA_BAD_SHAPE;
   if ((q_norm_w == nullptr) != (k_norm_w == nullptr)) return EIA_BAD_SHAPE;
@@ -1547,7 +1581,8 @@ EIA_API int eia_paged_decode_rope(const void* qkv, long qkv_stride, const float*
     hipLaunchKernelGGL((paged_decode_kernel<DD, true, true, SP, QN, HB>), grid, dim3(256), 0, st,  \
                        nullptr, 0L, (const bf16_t*)k_cache, (const bf16_t*)v_cache, block_tables,  \
                        bt_stride, seq_lens, (bf16_t*)out, out_stride, part_o, part_ml, part_cnt,    \
-                       sl2, Hq, Hkv, bs, P, 1, sliding_window, chunk_size, p_dyn, rope);
+                       sl2, Hq, Hkv, bs, P, 1, sliding_window, chunk_size, p_dyn,            \
+                       P > 1 && part_cnt != nullptr ? tail : nullptr, rope);
 #define DEC_FQ(DD, SP)                                                                           \
   if (q_norm_w) { if (bias) { DEC_F(DD, SP, true, true) } else { DEC_F(DD, SP, true, false) } }  \
   else { if (bias) { DEC_F(DD, SP, false, true) } else { DEC_F(DD, SP, false, false) } }

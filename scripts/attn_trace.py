@@ -45,7 +45,7 @@ def main():
     P_, I_, L_, F_ = ctypes.c_void_p, ctypes.c_int, ctypes.c_long, ctypes.c_float
     lib.eia_paged_decode_rope.argtypes = [P_, L_, P_, I_, P_, P_, P_, F_, P_, P_, P_, I_, P_, P_,
                                           P_, I_, P_, P_, L_, P_, P_, P_, F_, I_, I_, I_, I_, I_,
-                                          I_, I_, I_, P_, P_]
+                                          I_, I_, I_, P_, P_, P_]
     lib.eia_attn_set_trace.argtypes = [P_]
     del _native
     dev, bf = "cuda", torch.bfloat16
@@ -76,7 +76,7 @@ def main():
                                        pos.data_ptr(), cs.data_ptr(), slot.data_ptr(), B,
                                        k.data_ptr(), v.data_ptr(), bt.data_ptr(), bt.stride(0),
                                        sl.data_ptr(), out.data_ptr(), out.stride(0), None, None,
-                                       None, d ** -0.5, B, hq, hkv, d, bs, 1, 0, 0, None, st)
+                                       None, d ** -0.5, B, hq, hkv, d, bs, 1, 0, 0, None, None, st)
         assert rc == 0, rc
     for _ in range(3):
         torch.sum(flush, 0, out=acc)
