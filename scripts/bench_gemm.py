@@ -92,6 +92,9 @@ def main():
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--tune", action="store_true")
     ap.add_argument("--sweep", action="store_true", help="time every candidate (no table write)")
+    ap.add_argument("--check", action="store_true",
+                    help="sweep, and report the tuning table's pick against the best (regret) at "
+                         "each M -- the table is timed at one M per 16-row bucket")
     ap.add_argument("--out", default=None, help="also write the tuning table here")
     ap.add_argument("--persist", action="store_true",
                     help="also copy the table into the PVC tuning cache ($EIA_CACHE_DIR)")
@@ -116,7 +119,7 @@ def main():
             else:
                 base = lambda i: F.linear(x, ws[i % pool])
             tb = graph_time(base, a.iters)
-            cands = candidates(M, N, K, swiglu) if (a.tune or a.sweep) else \
+            cands = candidates(M, N, K, swiglu) if (a.tune or a.sweep or a.check) else \
                 [c for c in [gemm.choose(M, N, K, swiglu)] if c[0] >= 0]
             if a.packed:
                 cands = [(c, sk) for c in gemm.PACKED_CFGS for sk in {s for _, s in cands}
@@ -148,6 +151,18 @@ def main():
                  "runner_up": [(round(t, 1), c, s) for t, c, s in results[1:4]]}
             if a.all:
                 r["all"] = [(round(t, 1), c, s) for t, c, s in results]
+            if a.check:
+                pick = gemm.choose(M, N, K, swiglu)
+                tp = next((t for t, c, s_ in results if (c, s_) == tuple(pick)), None)
+                if tp is None and pick[0] >= 0:   # table pick outside the candidate list
+                    f = (lambda i: gemm.swiglu_gemm(x, ws[i % pool], cfg=pick[0])) if swiglu else \
+                        (lambda i: gemm.skinny(x, ws[i % pool], cfg=pick[0], sk=pick[1]))
+                    tp = graph_time(f, a.iters)
+                if pick[0] < 0:
+                    tp = tb
+                r["table_pick"] = list(pick)
+                r["table_us"] = round(tp, 2)
+                r["regret_pct"] = round(100.0 * (tp / min(to, tb) - 1.0), 1)
             print(json.dumps(r), flush=True)
             if a.tune:
                 results = [r_ for r_ in results if r_[1] != "balanced"] or results

@@ -22,6 +22,27 @@ def _check(out, ref, msg):
     assert (err <= tol).all(), f"{msg}: max err {err.max().item():.4g}"
 
 
+@pytest.mark.parametrize("M", [1, 33, 65, 128])
+@pytest.mark.parametrize("N,K", [(128256, 4096), (32000, 4096), (4096, 4096)])
+def test_linear_f32_logits(M, N, K):
+    """LM-head form: fp32 [M, N] straight from the skinny kernel's accumulators (no bf16
+    rounding) vs the fp32 reference; the ParallelLMHead path must take it (native, not a
+    silent .float() of the bf16 GEMM)."""
+    from enterprise_inference_amd.ops import gemm
+    torch.manual_seed(M + N)
+    x = torch.randn(M, K, device=DEV, dtype=BF)
+    w = (torch.randn(N, K, device=DEV) * K ** -0.5).to(BF)
+    out = gemm.linear_f32(x, w)
+    if out is None:   # shape outside the skinny table's single-split forms
+        pytest.skip("no single-split skinny form for this shape")
+    assert out.dtype == torch.float32 and out.shape == (M, N)
+    ref = _ref(x, w)
+    err = (out - ref).abs()
+    assert (err <= 1e-3 + 1e-3 * ref.abs()).all(), f"max err {err.max().item():.4g}"
+    # tighter than any bf16-rounded output could be at |logit| ~ 1-4
+    assert err.max().item() < 4e-3
+
+
 @pytest.mark.parametrize("M", [1, 5, 16, 33, 65, 100, 128])
 @pytest.mark.parametrize("N,K", [(4096, 4096), (6144, 4096), (4096, 14336), (1280, 8192), (384, 768)])
 def test_skinny_linear(M, N, K):
