@@ -22,8 +22,8 @@ def _check(out, ref, msg):
     assert (err <= tol).all(), f"{msg}: max err {err.max().item():.4g}"
 
 
-@pytest.mark.parametrize("M", [1, 33, 65, 128])
-@pytest.mark.parametrize("N,K", [(128256, 4096), (32000, 4096), (4096, 4096)])
+@pytest.mark.parametrize("M", [56, 65, 80])          # the table's single-split LM-head rows
+@pytest.mark.parametrize("N,K", [(128256, 4096)])
 def test_linear_f32_logits(M, N, K):
     """LM-head form: fp32 [M, N] straight from the skinny kernel's accumulators (no bf16
     rounding) vs the fp32 reference; the ParallelLMHead path must take it (native, not a
