@@ -38,6 +38,8 @@ SHAPES = {  # name: (N, K, swiglu)
     "qkv_405b_tp8": (2304, 16384, False), "o_405b_tp8": (16384, 2048, False),
     "gate_up_405b_tp8": (13312, 16384, True), "down_405b_tp8": (16384, 6656, False),
     "lm_head_405b_tp8": (16032, 16384, False),
+    # Mistral-7B / Mixtral-8x7B LM heads (their attention projections are the 8B shapes)
+    "lm_head_mistral": (32768, 4096, False), "lm_head_mixtral": (32000, 4096, False),
     # gate_up grid-size probes (8B K): 196 / 224 (the real shape) / 256 four-pair workgroups
     "gu_probe_196": (25088, 4096, True), "gu_probe_256": (32768, 4096, True),
 }
