@@ -67,44 +67,65 @@ topk_kernel(const void* __restrict__ logits, int is_bf16, int T, int E, int k, i
   topk_select(v, wave, lane, E, k, renorm, scoring, w_out, id_out);
 }
 
-// Router GEMM fused into the top-k: one wave per token computes its E logits (x row . router
-// row e, fp32 accumulate, rounded to bf16 like the unfused bf16 Linear) from 16-B loads of x
-// and of the router weight (E x H, L2-resident), reduces them across the wave and selects.
-// Replaces a hipBLASLt launch for an N = 8 GEMM (13.7 us per layer on Mixtral decode,
-// profiles/rocprof_r2_mixtral.md) and the logits round trip.
+// Router GEMM fused into the top-k: one 256-thread workgroup per token computes its E logits
+// (x row . router row e, fp32 accumulate, rounded to bf16 like the unfused bf16 Linear) from
+// 16-B loads of x and of the router weight (E x H, L2-resident), all of a thread's loads in
+// flight at once (H <= 2048 x RC), reduced across the wave and the 4 waves (LDS), and wave 0
+// selects.  Replaces a hipBLASLt launch for an N = 8 GEMM (13.7 us per layer on Mixtral decode,
+// profiles/rocprof_r2_mixtral.md) and the logits round trip.  (One wave per token -- 17
+// workgroups for 65 tokens, one serial L2 round trip per 512 columns -- took 34 us:
+// profiles/rocprof_r3_mixtral_steps.md.)
 template <int EM>
 __global__ void __launch_bounds__(256)
 route_kernel(const bf16_t* __restrict__ x, long ldx, const bf16_t* __restrict__ wr, int H, int T,
              int E, int k, int renorm, int scoring, float* __restrict__ w_out,
              int* __restrict__ id_out) {
-  const int wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
-  const int lane = threadIdx.x & 63;
-  if (wave >= T) return;
+  constexpr int RC = 4;                  // column chunks of 2048 per thread, loads unrolled
+  __shared__ float red[4][EM];
+  const int t = blockIdx.x;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   float acc[EM];
 #pragma unroll
   for (int e = 0; e < EM; ++e) acc[e] = 0.f;
-  const bf16_t* xr = x + (long)wave * ldx;
-  for (int c = lane * 8; c < H; c += 512) {
-    const bf16x8 xv = *reinterpret_cast<const bf16x8*>(xr + c);
-    float xf[8];
+  const bf16_t* xr = x + (long)t * ldx;
+  for (int c0 = threadIdx.x * 8; c0 < H; c0 += 2048 * RC) {
+    bf16x8 xv[RC];
 #pragma unroll
-    for (int j = 0; j < 8; ++j) xf[j] = bf2f(xv[j]);
+    for (int r = 0; r < RC; ++r) {
+      const int c = c0 + 2048 * r;
+      if (c < H) xv[r] = *reinterpret_cast<const bf16x8*>(xr + c);
+    }
 #pragma unroll
     for (int e = 0; e < EM; ++e) {
       if (e < E) {
-        const bf16x8 wv = *reinterpret_cast<const bf16x8*>(wr + (long)e * H + c);
+        bf16x8 wv[RC];
 #pragma unroll
-        for (int j = 0; j < 8; ++j) acc[e] = fmaf(xf[j], bf2f(wv[j]), acc[e]);
+        for (int r = 0; r < RC; ++r) {
+          const int c = c0 + 2048 * r;
+          if (c < H) wv[r] = *reinterpret_cast<const bf16x8*>(wr + (long)e * H + c);
+        }
+#pragma unroll
+        for (int r = 0; r < RC; ++r) {
+          if (c0 + 2048 * r < H) {
+#pragma unroll
+            for (int j = 0; j < 8; ++j) acc[e] = fmaf(bf2f(xv[r][j]), bf2f(wv[r][j]), acc[e]);
+          }
+        }
       }
     }
   }
-  float v = -INFINITY;
 #pragma unroll
   for (int e = 0; e < EM; ++e) {
-    const float tot = wave_sum(acc[e]);
-    if (lane == e && e < E) v = bf2f(f2bf(tot));
+    if (e < E) {
+      const float tot = wave_sum(acc[e]);
+      if (lane == 0) red[w][e] = tot;
+    }
   }
-  topk_select(v, wave, lane, E, k, renorm, scoring, w_out, id_out);
+  __syncthreads();
+  if (w != 0) return;
+  float v = -INFINITY;
+  if (lane < E) v = bf2f(f2bf(red[0][lane] + red[1][lane] + red[2][lane] + red[3][lane]));
+  topk_select(v, t, lane, E, k, renorm, scoring, w_out, id_out);
 }
 
 // Single workgroup: counts per expert, exclusive scan, scatter.  n = T*k entries.
@@ -183,7 +204,7 @@ EIA_API int eia_moe_route(const void* x, long ldx, const void* wr, int H, int T,
                           int renorm, int scoring, float* w_out, int* id_out, hipStream_t st) {
   if (E < 1 || E > 64 || k < 1 || k > E || H % 8 != 0 || (ldx % 8)) return EIA_BAD_SHAPE;
   if (T == 0) return EIA_OK;
-  const dim3 grid((T + 3) / 4), block(256);
+  const dim3 grid(T), block(256);
   const bf16_t* xp = static_cast<const bf16_t*>(x);
   const bf16_t* wp = static_cast<const bf16_t*>(wr);
   if (E <= 8)
