@@ -134,6 +134,7 @@ align_kernel(const int* __restrict__ ids, int n, int E, int e_lo, int e_hi,
              int* __restrict__ offs, int* __restrict__ row_idx, int* __restrict__ inv, int k) {
   __shared__ int cnt[256];
   __shared__ int cur[256];
+  __shared__ int s_tot;
   for (int e = threadIdx.x; e < E; e += blockDim.x) cnt[e] = 0;
   __syncthreads();
   for (int i = threadIdx.x; i < n; i += blockDim.x) {
@@ -150,8 +151,12 @@ align_kernel(const int* __restrict__ ids, int n, int E, int e_lo, int e_hi,
       acc += cnt[e];
     }
     offs[El] = acc;
+    s_tot = acc;
   }
   __syncthreads();
+  // rows past the local entries (expert parallelism: other ranks' experts) read as token 0;
+  // the scatter below never writes them, so this replaces a separate zero-fill launch
+  for (int i = s_tot + threadIdx.x; i < (n > 0 ? n : 1); i += blockDim.x) row_idx[i] = 0;
   for (int i = threadIdx.x; i < n; i += blockDim.x) {
     const int e = ids[i];
     if (e >= e_lo && e < e_hi) {

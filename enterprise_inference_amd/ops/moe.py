@@ -148,8 +148,8 @@ def _fused_moe_grouped(x, w13, w2, topk_w, topk_ids, e_lo, e_hi, mfma: bool = Fa
 def _align(topk_ids, El, e_lo, e_hi, n, dev, st):
     E_total = max(e_hi, int(El + e_lo))
     offs = torch.empty(El + 1, dtype=torch.int32, device=dev)
-    # zero-filled: with expert parallelism the align kernel writes only the local rows
-    row_idx = torch.zeros(max(1, n), dtype=torch.int32, device=dev)
+    # with expert parallelism the align kernel scatters only the local rows and zeroes the rest
+    row_idx = torch.empty(max(1, n), dtype=torch.int32, device=dev)
     inv = torch.empty(max(1, n), dtype=torch.int32, device=dev)
     check(lib().eia_moe_align(ptr(topk_ids), n, E_total, e_lo, e_hi, ptr(offs), ptr(row_idx),
                               ptr(inv), topk_ids.shape[1], st), "moe_align")
