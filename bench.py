@@ -53,6 +53,9 @@ BASELINE_TOK_S = {  # third_party/IBM/docs/sizing-guide.md (Gaudi 3, vLLM 0.7.2)
     ("meta-llama/Llama-3.3-70B-Instruct", 128, 128): (1120.0, 4),
     ("meta-llama/Llama-3.1-405B-Instruct", 128, 128): (493.0, 8),
 }
+BASELINE_TTFT_P90_MS = {  # same rows (chatbot 128/128): p90 TTFT on Gaudi 3
+    "meta-llama/Llama-3.1-8B-Instruct": 1300.0, "meta-llama/Llama-3.3-70B-Instruct": 613.0,
+    "meta-llama/Llama-3.1-405B-Instruct": 1072.0}
 METRIC = "output tokens/sec (node) + p50 TTFT via OpenAI endpoint, Llama-3-8B/70B"
 
 
@@ -82,6 +85,18 @@ def parse():
     ap.add_argument("--startup-timeout", type=float, default=1500)
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--verbose", action="store_true")
+    ap.add_argument("--closed-loop-s", type=float, default=8.0,
+                    help="endpoint mode: after the burst rounds, a closed-loop window of this "
+                         "many seconds (every user resubmits on completion; 0 = off)")
+    ap.add_argument("--closed-loop-warm-s", type=float, default=3.0,
+                    help="closed-loop ramp before the measured window")
+    ap.add_argument("--extras", default="auto", choices=["auto", "on", "off"],
+                    help="after the headline, also run BASELINE config #3 (Llama-3.3-70B at "
+                         "TP=N, 35 users) and at N=8 config #5 (8B + Mistral-7B co-deploy); "
+                         "auto = endpoint mode with N >= 2.  Reported under extra keys, "
+                         "`value` is the headline only")
+    ap.add_argument("--extra-budget-s", type=float, default=1500.0,
+                    help="wall-clock budget for all extra configurations together")
     return ap.parse_args()
 
 
@@ -133,16 +148,34 @@ def _client_worker(conn, url: str, model: str, max_tokens: int, temperature: flo
             return (False, 0.0, 0.0, 0, "stream ended without usage/[DONE]")
         return (True, (first or t1) - t0, t1 - t0, int(usage["completion_tokens"]), "")
 
+    async def closed(session, spec):
+        """Closed loop: `n` users, each resubmits the moment its stream ends, until t_stop.
+        Returns (wall start, ok, ttft, e2e, tokens, err) per request."""
+        rng = random.Random(spec["seed"])
+
+        async def user():
+            out = []
+            while time.time() < spec["t_stop"]:
+                p = [rng.randrange(1000, spec["vocab"]) for _ in range(spec["input_len"])]
+                t = time.time()
+                out.append((t,) + await one(session, p))
+            return out
+        rs = await asyncio.gather(*(user() for _ in range(spec["n"])))
+        return [r for u in rs for r in u]
+
     async def main():
         conn_limit = aiohttp.TCPConnector(limit=0, force_close=False)
         to = aiohttp.ClientTimeout(total=timeout)
         async with aiohttp.ClientSession(connector=conn_limit, timeout=to) as session:
             loop = asyncio.get_running_loop()
             while True:
-                prompts = await loop.run_in_executor(None, conn.recv)
-                if prompts is None:
+                msg = await loop.run_in_executor(None, conn.recv)
+                if msg is None:
                     return
-                res = await asyncio.gather(*(one(session, p) for p in prompts))
+                if isinstance(msg, dict):
+                    conn.send(await closed(session, msg))
+                    continue
+                res = await asyncio.gather(*(one(session, p) for p in msg))
                 conn.send(res)
 
     asyncio.run(main())
@@ -151,6 +184,7 @@ def _client_worker(conn, url: str, model: str, max_tokens: int, temperature: flo
 class ClientPool:
     def __init__(self, n: int, url: str, model: str, max_tokens: int, temperature: float,
                  timeout: float = 3600.0):
+        # (the timeout bounds every request; extra configs pass their remaining budget)
         import multiprocessing as mp
 
         ctx = mp.get_context("spawn")
@@ -168,6 +202,20 @@ class ClientPool:
         shares = [prompts[i::n] for i in range(n)]
         for c, s in zip(self.conns, shares):
             c.send(s)
+        out = []
+        for c in self.conns:
+            out += c.recv()
+        return out
+
+    def closed_loop(self, users: int, t_stop: float, input_len: int, vocab: int, seed: int):
+        """Start the closed-loop users (split over the client processes); collect() later."""
+        n = len(self.conns)
+        for i, c in enumerate(self.conns):
+            k = users // n + (1 if i < users % n else 0)
+            c.send({"n": k, "t_stop": t_stop, "input_len": input_len, "vocab": vocab,
+                    "seed": seed * 131 + i})
+
+    def collect(self):
         out = []
         for c in self.conns:
             out += c.recv()
@@ -260,15 +308,17 @@ class Replica:
     """One serving replica: an OpenAI server on GPUs [first_gpu, first_gpu + tp) plus the
     client processes holding its --users concurrent streams."""
 
-    def __init__(self, args, idx: int, first_gpu: int, model: str, logdir: str):
+    def __init__(self, args, idx: int, first_gpu: int, model: str, logdir: str,
+                 tag: str = "", request_timeout: float = 3600.0):
         self.args, self.idx, self.model = args, idx, model
-        self.log_path = os.path.join(logdir, f"bench_server_rank{first_gpu}.log")
+        self.log_path = os.path.join(logdir, f"bench_server{tag}_rank{first_gpu}.log")
         port = _free_port()
         self.base = f"http://127.0.0.1:{port}"
+        self._closed = False
         self.proc = start_server(args, first_gpu, port, self.log_path, model)
         self.pool = ClientPool(max(1, min(args.client_procs, args.users)),
                                self.base + "/v1/completions", model, args.output_len,
-                               args.temperature)
+                               args.temperature, request_timeout)
         from enterprise_inference_amd.models.catalog import resolve_name
         from enterprise_inference_amd.models.loader import resolve_model_config
         self.vocab = min(resolve_model_config(resolve_name(model)).vocab_size, 128000)
@@ -329,7 +379,30 @@ class Replica:
                 "engine_busy_s": stats1["step_time_s"] - stats0["step_time_s"],
                 "num_blocks": stats1["num_blocks"]}
 
+    def closed_loop(self, dur: float, warm: float) -> dict:
+        """Steady-state arrival: every user resubmits on completion.  Throughput = engine
+        generation tokens over the measured window (stats read at its edges); TTFT / TPOT of
+        the requests that STARTED inside the window."""
+        a = self.args
+        t_meas0 = time.time() + warm
+        t_meas1 = t_meas0 + dur
+        self.pool.closed_loop(a.users, t_meas1, a.input_len, self.vocab, a.seed + 17)
+        time.sleep(max(0.0, t_meas0 - time.time()))
+        s0, w0 = self.stats(), time.time()
+        time.sleep(max(0.0, t_meas1 - time.time()))
+        s1, w1 = self.stats(), time.time()
+        res = self.pool.collect()
+        inside = [r for r in res if t_meas0 <= r[0] < t_meas1]
+        ok = [r for r in inside if r[1] and r[4] == a.output_len]
+        return {"gen_tokens": s1["num_generation_tokens"] - s0["num_generation_tokens"],
+                "window_s": w1 - w0, "ttft": [r[2] for r in ok],
+                "tpot": [(r[3] - r[2]) / (r[4] - 1) for r in ok if r[4] > 1],
+                "requests": len(inside), "failed": len(inside) - len(ok)}
+
     def close(self) -> None:
+        if self._closed:
+            return
+        self._closed = True
         self.pool.close()
         stop_server(self.proc)
 
@@ -392,7 +465,17 @@ def run_endpoint(args) -> int:
         elapsed = time.time() - t0
         stats1 = [r.stats() for r in reps]
         summ = [r.summary(elapsed, s0, s1) for r, s0, s1 in zip(reps, stats0, stats1)]
-        _report(args, summ, n_gpus=n_rep * args.tp, via="endpoint")
+        closed = None
+        if args.closed_loop_s > 0:
+            closed = [None] * len(reps)
+            _parallel([(lambda i=i, r=r: closed.__setitem__(
+                i, r.closed_loop(args.closed_loop_s, args.closed_loop_warm_s)))
+                for i, r in enumerate(reps)])
+        for r in reps:
+            r.close()
+        n_gpus = n_rep * args.tp
+        extras = run_extras(args, n_gpus, logdir) if want_extras(args, n_gpus) else None
+        _report(args, summ, n_gpus=n_gpus, via="endpoint", closed=closed, extras=extras)
         failed = [f for g in summ for f in g["failed"]]
         if failed:
             print(f"error: {len(failed)} failed requests, e.g. {failed[0]}", file=sys.stderr)
@@ -417,8 +500,12 @@ def _run_endpoint_torchrun(args) -> int:
         rep = Replica(args, rank // args.tp, local, model, logdir)
     dist = None
     if world > 1:
+        import datetime
+
         import torch.distributed as dist
-        dist.init_process_group("gloo", rank=rank, world_size=world)
+        # long timeout: the other ranks wait in a barrier while rank 0 runs the extra configs
+        dist.init_process_group("gloo", rank=rank, world_size=world,
+                                timeout=datetime.timedelta(seconds=args.extra_budget_s + 3600))
     try:
         if rep:
             rep.wait()
@@ -440,14 +527,27 @@ def _run_endpoint_torchrun(args) -> int:
         if dist is not None:
             dist.barrier()
         local_stats = rep.summary(elapsed, stats0, rep.stats()) if rep else None
+        local_closed = None
+        if rep and args.closed_loop_s > 0:
+            local_closed = rep.closed_loop(args.closed_loop_s, args.closed_loop_warm_s)
         if dist is not None:
             gathered = [None] * world
-            dist.all_gather_object(gathered, local_stats)
+            dist.all_gather_object(gathered, (local_stats, local_closed))
         else:
-            gathered = [local_stats]
-        summ = [g for g in gathered if g is not None]
+            gathered = [(local_stats, local_closed)]
+        summ = [g[0] for g in gathered if g[0] is not None]
+        closed = [g[1] for g in gathered if g[1] is not None] or None
+        if rep is not None:
+            rep.close()                       # free the GPUs for the extra configurations
+        if dist is not None:
+            dist.barrier()
+        extras = None
+        if rank == 0 and want_extras(args, world):
+            extras = run_extras(args, world, logdir)
+        if dist is not None:
+            dist.barrier()
         if rank == 0:
-            _report(args, summ, n_gpus=world, via="endpoint")
+            _report(args, summ, n_gpus=world, via="endpoint", closed=closed, extras=extras)
         failed = [f for g in summ for f in g["failed"]]
         if failed and rank == 0:
             print(f"error: {len(failed)} failed requests, e.g. {failed[0]}", file=sys.stderr)
@@ -457,6 +557,74 @@ def _run_endpoint_torchrun(args) -> int:
             rep.close()
         if dist is not None:
             dist.destroy_process_group()
+
+
+# --------------------------------------------------------------------------- extra configs
+
+def want_extras(args, n_gpus: int) -> bool:
+    if args.extras == "off" or args.mode != "endpoint":
+        return False
+    return args.extras == "on" or n_gpus >= 2
+
+
+def _extra(a, slots, n_gpus: int, deadline: float, logdir: str) -> dict:
+    """One extra configuration: replicas (first GPU, model) started, warmed, timed; any
+    failure (OOM, startup error, budget exhausted) is recorded instead of raised."""
+    reps = []
+    try:
+        left = deadline - time.time()
+        if left < 120:
+            return {"error": "skipped: extra budget exhausted"}
+        a.startup_timeout = min(a.startup_timeout, left)
+        for i, (g, m) in enumerate(slots):
+            reps.append(Replica(a, i, g, m, logdir, tag="_extra", request_timeout=max(60, left)))
+        _parallel([r.wait for r in reps])
+        _parallel([(lambda r=r: r.rounds(a.warmup, False)) for r in reps])
+        stats0 = [r.stats() for r in reps]
+        _parallel([r.sync for r in reps])
+        t0 = time.time()
+        _parallel([(lambda r=r: r.rounds(a.steps, True)) for r in reps])
+        _parallel([r.sync for r in reps])
+        elapsed = time.time() - t0
+        stats1 = [r.stats() for r in reps]
+        summ = [r.summary(elapsed, s0, s1) for r, s0, s1 in zip(reps, stats0, stats1)]
+        d = _summary(a, summ, n_gpus, "endpoint")
+        keep = ("value", "vs_baseline", "ms_per_step", "ttft_p50_ms", "ttft_p90_ms",
+                "tpot_p50_ms", "tpot_p90_ms", "failed_requests", "init_s",
+                "baseline_tok_s_per_replica", "per_model", "engine_tok_s")
+        r = {k: d[k] for k in keep if k in d}
+        r.update(model=d["config"]["model"], users_per_replica=a.users,
+                 parallelism=d["config"]["parallelism"], steps=a.steps,
+                 input_len=a.input_len, output_len=a.output_len)
+        return r
+    except BaseException as e:  # noqa: BLE001 - recorded, never fails the headline
+        return {"error": repr(e)[-600:]}
+    finally:
+        for r in reps:
+            try:
+                r.close()
+            except Exception:  # noqa: BLE001
+                pass
+
+
+def run_extras(args, n_gpus: int, logdir: str) -> dict:
+    """BASELINE.json config #3 (Llama-3.3-70B, one replica over all N GPUs, 35 users -- the
+    sizing guide's 70B row, third_party/IBM/docs/sizing-guide.md:69) and, on 8 GPUs, config #5
+    (4 x Llama-3.1-8B + 4 x Mistral-7B replicas on disjoint GPUs, 65 users each)."""
+    import copy
+    deadline = time.time() + args.extra_budget_s
+    out = {}
+    a3 = copy.copy(args)
+    a3.model, a3.tp, a3.users = "meta-llama/Llama-3.3-70B-Instruct", n_gpus, 35
+    a3.steps, a3.warmup, a3.co_deploy = 2, 1, False
+    out[f"config3_llama70b_tp{n_gpus}"] = _extra(a3, [(0, a3.model)], n_gpus, deadline, logdir)
+    if n_gpus == 8:
+        a5 = copy.copy(args)
+        a5.tp, a5.co_deploy, a5.steps, a5.warmup = 1, True, 2, 1
+        models = replica_models(a5, 8)
+        out["config5_codeploy_8b_mistral7b"] = _extra(a5, list(enumerate(models)), 8, deadline,
+                                                      logdir)
+    return out
 
 
 # --------------------------------------------------------------------------- engine mode
@@ -586,8 +754,28 @@ def _gather_report(args, dist, local_stats, rank, world, via: str):
         _report(args, [g for g in gathered if g is not None], world, via)
 
 
-def _report(args, reps, n_gpus: int, via: str):
+def _report(args, reps, n_gpus: int, via: str, closed=None, extras=None):
     """ONE JSON line for the whole job: ``reps`` holds one summary per serving replica."""
+    out = _summary(args, reps, n_gpus, via)
+    if closed:
+        tt = sorted(x for c in closed for x in c["ttft"])
+        tp = sorted(x for c in closed for x in c["tpot"])
+        out["closed_loop"] = {
+            "tok_s": round(sum(c["gen_tokens"] / max(c["window_s"], 1e-9) for c in closed), 2),
+            "window_s": round(max(c["window_s"] for c in closed), 2),
+            "users_per_replica": args.users,
+            "requests": sum(c["requests"] for c in closed),
+            "failed_requests": sum(c["failed"] for c in closed),
+            "ttft_p50_ms": None if not tt else round(1000 * _pct(tt, 50), 2),
+            "ttft_p90_ms": None if not tt else round(1000 * _pct(tt, 90), 2),
+            "tpot_p50_ms": None if not tp else round(1000 * _pct(tp, 50), 3),
+            "tpot_p90_ms": None if not tp else round(1000 * _pct(tp, 90), 3)}
+    if extras is not None:
+        out["extra_configs"] = extras
+    print(json.dumps(out), flush=True)
+
+
+def _summary(args, reps, n_gpus: int, via: str) -> dict:
     from enterprise_inference_amd.models.catalog import resolve_name
 
     tokens = sum(g["tokens"] for g in reps)
@@ -635,7 +823,8 @@ def _report(args, reps, n_gpus: int, via: str):
         "e2e_p50_ms": ms(_pct(e2e, 50)),
         "total_tok_s": round(value * (args.input_len + args.output_len) / args.output_len, 2),
         "baseline_tok_s_per_replica": None if base is None else base[0],
-        "baseline_ttft_p90_ms_gaudi3": 1300.0 if base is not None and base[1] == 1 else None,
+        "baseline_ttft_p90_ms_gaudi3": None if base is None else
+        BASELINE_TTFT_P90_MS.get(models[0]),
         "failed_requests": sum(len(g["failed"]) for g in reps),
         "init_s": round(max(g["init_s"] for g in reps), 1),
     }
@@ -651,7 +840,7 @@ def _report(args, reps, n_gpus: int, via: str):
                                         for g in reps), 2)
         out["engine_busy_frac"] = round(busy / elapsed, 3)
         out["engine_steps"] = sum(g["engine_steps"] for g in reps)
-    print(json.dumps(out), flush=True)
+    return out
 
 
 def main() -> int:

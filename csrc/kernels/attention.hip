@@ -458,42 +458,14 @@ paged_decode_kernel(const bf16_t* __restrict__ q, long q_stride,
                     int* __restrict__ part_cnt,
                     float scale_log2, int Hq, int Hkv, int bs, int Pmax, int NQG,
                     int sliding_window, int chunk_size, const int* __restrict__ p_dyn,
-                    const int* __restrict__ tail, DecodeRope rope) {
+                    DecodeRope rope) {
   constexpr int NW = 4;
   __shared__ int s_last;
   __shared__ float sm[NW][16];
   __shared__ float sl[NW][16];
   __shared__ __align__(16) float so[NW][D][17];
 
-  // Tail split (`tail` = device int (row << 8) | parts, needs part_cnt): rows >= `row` of a P-1
-  // step are split over `parts` partitions (grid.z >= parts) and merged in-kernel.  A grid of
-  // 2 workgroups per CU plus a few (B 65 x 8 KV heads = 520 on 256 CUs) puts a third whole item
-  // on some CUs, which then finish ~1.5x later than the rest (profiles/attn_batch_balance_r3.md);
-  // split, the surplus rows add only light pieces.  The dispatch order is remapped: partition 0
-  // of every item first, row-major (all heads of a row adjacent), so the whole-item rows
-  // dispatch first, two per CU; then partitions >= 1 from the LAST row down, so the tail rows'
-  // pieces dispatch right behind (instead of after a whole grid.z slice of workgroups that exit
-  // at once) and fill third slots.
-  int b, yb, p;
-  if (tail != nullptr) {
-    const int X = gridDim.x, Y = gridDim.y;
-    const int lin = blockIdx.x + X * (blockIdx.y + Y * blockIdx.z);
-    if (lin < X * Y) {
-      b = lin / Y;
-      yb = lin - b * Y;
-      p = 0;
-    } else {
-      const int e = lin - X * Y, R = Y * ((int)gridDim.z - 1);
-      const int r = e / R, rem = e - r * R;
-      b = X - 1 - r;
-      p = 1 + rem / Y;
-      yb = rem - (p - 1) * Y;
-    }
-  } else {
-    b = blockIdx.x;
-    yb = blockIdx.y;
-    p = blockIdx.z;
-  }
+  const int b = blockIdx.x, yb = blockIdx.y, p = blockIdx.z;
   const int kvh = yb / NQG, qg = yb % NQG;
   ATRACE_DECL;
   ATRACE(0);
@@ -515,18 +487,12 @@ paged_decode_kernel(const bf16_t* __restrict__ q, long q_stride,
   const int pos_b = FUSED ? rope.positions[b] : 0;
   const int slot_b = FUSED ? rope.slot_mapping[b] : -1;
   const int pd = *pdp;                                   // unconditional: no wait in a branch
-  const int tv = *(tail != nullptr ? tail : pdp);
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int c = lane & 15, g = lane >> 4;
-  const int Pstep = p_dyn != nullptr ? max(1, min(pd, Pmax)) : Pmax;
-  const int trow = tail != nullptr && part_cnt != nullptr ? (tv >> 8) : 0x7fffffff;
-  // a split row takes at most one partition per 64-token pair (the partition boundaries below)
-  const int P = (Pstep == 1) & (b >= trow) & (L > 0)
-                    ? max(1, min(min(tv & 255, Pmax), ((L + 31) / 32 + 1) / 2))
-                    : Pstep;
-  // (L | pos | slot + 1 | tv) < 0 never holds; testing it keeps the compiler from sinking those
+  const int P = p_dyn != nullptr ? max(1, min(pd, Pmax)) : Pmax;
+  // (L | pos | slot + 1) < 0 never holds; testing it keeps the compiler from sinking those
   // loads past the exit branch, which would serialise them behind the p_dyn round trip
-  if ((p >= P) | ((L | pos_b | (slot_b + 1) | bt0 | bt1 | tv) < 0)) return;   // no short-circuit
+  if ((p >= P) | ((L | pos_b | (slot_b + 1) | bt0 | bt1) < 0)) return;   // no short-circuit
   ATRACE(6);
   const int G = Hq / Hkv;
   const int hq0 = kvh * G + qg * 16;
@@ -790,355 +756,6 @@ paged_decode_reduce_kernel(const float* __restrict__ part_o, const float* __rest
     }
     out[(long)b * out_stride + (long)h * D + d] = f2bf(Ls > 0.f ? O / Ls : 0.f);
   }
-}
-
-// Unit loop of one wave that owns a whole (partition of a) context: NS register sets of K/V
-// rotate so NS-1 units stay in flight while one is multiplied (the wave has no siblings to hide
-// its load latency), and the partition's block-table entries are read once up front into a
-// lane-indexed register (readlane per unit) instead of one dependent scalar load per unit.
-template <int D, int NS, typename PreIssue, typename Pre>
-EIA_DEV void attn_units_deep(WaveAcc<D>& acc, const bf16x8 (&qs)[D / 32][64],
-                             const bf16_t* __restrict__ kc, const bf16_t* __restrict__ vc,
-                             const int* __restrict__ bt, int bt_win, int ub, int ue, int L,
-                             int kvh, int Hkv, int bs, float scale_log2, int kv_lo,
-                             PreIssue&& pre_issue, Pre&& pre, int tnew, const bf16_t* knew,
-                             const bf16_t* vnew) {
-  if (ub >= ue) {
-    pre_issue();
-    pre();
-    return;
-  }
-  const int lane = threadIdx.x & 63;
-  const int c = lane & 15, g = lane >> 4;
-  const long hk = (long)bs * D;
-  const unsigned koff = (unsigned)(((8 * (c >> 2) + (c & 3)) * D + 8 * g) * 2);
-  const unsigned voff = (unsigned)((8 * g + c * bs) * 2);
-  const int upb = bs / 32;                           // units per block
-  // lane window of block-table entries [wbase, wbase + 64): the caller's window (entries
-  // [0, 64), loaded beside L at kernel entry) until a unit lies past it
-  int wbase = 0;
-  int wblk = bt_win;
-  auto block_of = [&](int uu) -> int {
-    const int bi = uu / upb;
-    if (bi - wbase >= 64) {                          // wave-uniform: slide the window
-      wbase = bi;
-      wblk = bt[wbase + lane];                       // entries past the row end: never used
-    }
-    return __builtin_amdgcn_readlane(wblk, bi - wbase);
-  };
-  // named register sets (an indexed array of them is demoted to scratch by hipcc)
-  bf16x8 ak0[D / 32], ak1[D / 32], av[D / 16], bk0[D / 32], bk1[D / 32], bv[D / 16];
-  bf16x8 ck0[D / 32], ck1[D / 32], cv[D / 16], dk0[D / 32], dk1[D / 32], dv[D / 16];
-  bf16x8 ek0[D / 32], ek1[D / 32], ev[D / 16], fk0[D / 32], fk1[D / 32], fv[D / 16];
-  auto load = [&](bf16x8 (&k0)[D / 32], bf16x8 (&k1)[D / 32], bf16x8 (&v)[D / 16], int uu) {
-    const int blk = block_of(uu);
-    const long base = ((long)blk * Hkv + kvh) * hk;
-    const int o = (32 * uu) % bs;
-    const char* kb = reinterpret_cast<const char*>(kc + base + (long)o * D);
-    const char* vb = reinterpret_cast<const char*>(vc + base + o);
-#pragma unroll
-    for (int s = 0; s < D / 32; ++s) {
-      k0[s] = *reinterpret_cast<const bf16x8*>(kb + koff + 64 * s);
-      k1[s] = *reinterpret_cast<const bf16x8*>(kb + koff + 8 * D + 64 * s);
-    }
-#pragma unroll
-    for (int dt = 0; dt < D / 16; ++dt)
-      v[dt] = *reinterpret_cast<const bf16x8*>(vb + (long)dt * 32 * bs + voff);
-  };
-  auto patch = [&](bf16x8 (&k0)[D / 32], bf16x8 (&k1)[D / 32], bf16x8 (&v)[D / 16], int uc) {
-    const int o = tnew - 32 * uc;
-    if (o < 0 || o >= 32) return;
-    const int tr0 = 8 * (c >> 2) + (c & 3);
-    if (tr0 == o || tr0 + 4 == o) {
-#pragma unroll
-      for (int s2 = 0; s2 < D / 32; ++s2) {
-        const bf16x8 kn = *reinterpret_cast<const bf16x8*>(knew + 8 * g + 32 * s2);
-        if (tr0 == o) k0[s2] = kn; else k1[s2] = kn;
-      }
-    }
-    if (g == (o >> 3)) {
-#pragma unroll
-      for (int dt = 0; dt < D / 16; ++dt) {
-        const bf16_t xv = vnew[16 * dt + c];
-#pragma unroll
-        for (int j = 0; j < 8; ++j)
-          if (j == (o & 7)) v[dt][j] = xv;
-      }
-    }
-  };
-  auto step = [&](bf16x8 (&k0)[D / 32], bf16x8 (&k1)[D / 32], bf16x8 (&v)[D / 16],
-                  bf16x8 (&nk0)[D / 32], bf16x8 (&nk1)[D / 32], bf16x8 (&nv)[D / 16], int uc) {
-    load(nk0, nk1, nv, min(uc + NS - 1, ue - 1));    // clamped: static vmcnt accounting
-    __builtin_amdgcn_sched_barrier(0);
-    patch(k0, k1, v, uc);
-    f32x4 s0, s1;
-    {
-      bf16x8 qf[D / 32];
-#pragma unroll
-      for (int s = 0; s < D / 32; ++s) qf[s] = qs[s][lane];
-      qk_unit<D>(s0, s1, qf, k0, k1);
-    }
-    softmax_pv<D>(acc, s0, s1, v, 32 * uc, L, scale_log2, 0x7fffffff, kv_lo);
-    __builtin_amdgcn_sched_barrier(0);
-  };
-  static_assert(NS >= 3 && NS <= 6, "wave decode pipeline: 3 to 6 register sets");
-  // the first NS-1 units' loads, then the prologue's (behind them: the window readlane above
-  // waits, in-order, only for the window load)
-  load(ak0, ak1, av, ub);
-  load(bk0, bk1, bv, min(ub + 1, ue - 1));
-  if constexpr (NS >= 4) load(ck0, ck1, cv, min(ub + 2, ue - 1));
-  if constexpr (NS >= 5) load(dk0, dk1, dv, min(ub + 3, ue - 1));
-  if constexpr (NS == 6) load(ek0, ek1, ev, min(ub + 4, ue - 1));
-  pre_issue();
-  pre();
-  int u = ub;
-  if constexpr (NS == 6) {
-    for (;;) {
-      step(ak0, ak1, av, fk0, fk1, fv, u);
-      if (++u >= ue) return;
-      step(bk0, bk1, bv, ak0, ak1, av, u);
-      if (++u >= ue) return;
-      step(ck0, ck1, cv, bk0, bk1, bv, u);
-      if (++u >= ue) return;
-      step(dk0, dk1, dv, ck0, ck1, cv, u);
-      if (++u >= ue) return;
-      step(ek0, ek1, ev, dk0, dk1, dv, u);
-      if (++u >= ue) return;
-      step(fk0, fk1, fv, ek0, ek1, ev, u);
-      if (++u >= ue) return;
-    }
-  } else if constexpr (NS == 5) {
-    for (;;) {
-      step(ak0, ak1, av, ek0, ek1, ev, u);
-      if (++u >= ue) return;
-      step(bk0, bk1, bv, ak0, ak1, av, u);
-      if (++u >= ue) return;
-      step(ck0, ck1, cv, bk0, bk1, bv, u);
-      if (++u >= ue) return;
-      step(dk0, dk1, dv, ck0, ck1, cv, u);
-      if (++u >= ue) return;
-      step(ek0, ek1, ev, dk0, dk1, dv, u);
-      if (++u >= ue) return;
-    }
-  } else if constexpr (NS == 4) {
-    for (;;) {
-      step(ak0, ak1, av, dk0, dk1, dv, u);
-      if (++u >= ue) return;
-      step(bk0, bk1, bv, ak0, ak1, av, u);
-      if (++u >= ue) return;
-      step(ck0, ck1, cv, bk0, bk1, bv, u);
-      if (++u >= ue) return;
-      step(dk0, dk1, dv, ck0, ck1, cv, u);
-      if (++u >= ue) return;
-    }
-  } else {
-    for (;;) {
-      step(ak0, ak1, av, ck0, ck1, cv, u);
-      if (++u >= ue) return;
-      step(bk0, bk1, bv, ak0, ak1, av, u);
-      if (++u >= ue) return;
-      step(ck0, ck1, cv, bk0, bk1, bv, u);
-      if (++u >= ue) return;
-    }
-  }
-}
-
-// ------------------------------------------------------------------- decode, one wave per item
-// Wave form: every (sequence, KV head, partition) is ONE 64-thread workgroup that walks all of
-// its 32-token units itself (next unit in flight while the current one is multiplied) and
-// normalises its own output -- no cross-wave LDS merge, no workgroup barrier after the
-// prologue.  The 4-wave form splits a short context (ctx 192 = 6 units) over four waves that
-// each see 1-2 units: every wave then pays the full load latency once or twice and the
-// workgroup a 34 KB LDS merge, and co-resident workgroups contend for issue slots
-// (profiles/pmc_decode_attn_r2.md: SQ_WAIT_INST_ANY 43 % of wave cycles at B = 65).  Here the
-// per-unit latency is pipelined along the wave's own unit stream and B * Hkv * P independent
-// waves spread over the CUs.  FUSED: the K4 prologue (split-K reduce / bias / qk-norm / RoPE /
-// KV write, q into LDS) runs on the wave's 64 lanes, D/16 lanes per head row.
-// One wave per SIMD (512 registers): NS = 6 register sets keep five 32-token units in flight
-// from the first instruction on -- a short context (ctx <= 160) is fetched in ONE round trip
-// and a long one streams five units deep -- and the fused prologue holds a whole split-K group
-// of slabs beside them.  B * Hkv * P <= 1024 waves still run in one round.
-// The fused form keeps one set fewer: its prologue's slab registers would otherwise spill.
-#ifndef EIA_WAVE_NS
-#define EIA_WAVE_NS 6      // K/V register sets of the wave form (NS-1 units in flight)
-#endif
-#ifndef EIA_WAVE_NS_FUSED
-#define EIA_WAVE_NS_FUSED 5
-#endif
-
-template <int D, bool FUSED, bool SPLIT, bool QK_NORM, bool HAS_BIAS>
-__global__ void __launch_bounds__(64, 1)
-paged_decode_wave_kernel(const bf16_t* __restrict__ q, long q_stride, const bf16_t* kc,
-                         const bf16_t* vc, const int* __restrict__ block_tables, int bt_stride,
-                         const int* __restrict__ seq_lens, bf16_t* __restrict__ out,
-                         long out_stride, float* __restrict__ part_o, float* __restrict__ part_ml,
-                         int* __restrict__ part_cnt, float scale_log2, int Hq, int Hkv, int bs,
-                         int Pmax, int sliding_window, int chunk_size,
-                         const int* __restrict__ p_dyn, DecodeRope rope) {
-  __shared__ bf16x8 qs[D / 32][64];
-  __shared__ __align__(16) bf16_t knew[D], vnew[D];
-  __shared__ int s_last;
-  const int b = blockIdx.x, kvh = blockIdx.y, p = blockIdx.z;
-  ATRACE_DECL;
-  ATRACE(0);
-  const int lane = threadIdx.x;
-  const int c = lane & 15, g = lane >> 4;
-  // entry loads in one round trip (see paged_decode_kernel): P, L, the prologue scalars and the
-  // block-table window [0, 64)
-  const int pd = *(p_dyn != nullptr ? p_dyn : seq_lens);
-  const int L = seq_lens[b];
-  const int pos_b = FUSED ? rope.positions[b] : 0;
-  const int slot_b = FUSED ? rope.slot_mapping[b] : -1;
-  const int* bt = block_tables + (long)b * bt_stride;
-  const int bt_win = lane < bt_stride ? bt[lane] : 0;
-  const int P = p_dyn != nullptr ? max(1, min(pd, Pmax)) : Pmax;
-  if ((p >= P) | ((L | pos_b | (slot_b + 1)) < 0)) return;   // no short-circuit
-  ATRACE(6);
-  const int nq = Hq / Hkv;             // <= 16 (host-checked)
-  const int hq0 = kvh * nq;
-  WaveAcc<D> acc;
-  wave_acc_init(acc);
-  int kv_lo = 0;
-  if (L > 0 && sliding_window > 0) kv_lo = max(kv_lo, L - sliding_window);
-  if (L > 0 && chunk_size > 0) kv_lo = max(kv_lo, ((L - 1) / chunk_size) * chunk_size);
-  const int U0 = kv_lo / 32;
-  const int U = (L + 31) / 32 - U0;
-  const int A0 = U0 & ~1;
-  const int npair = (U0 + U - A0 + 1) / 2;
-  const int ub = max(U0, A0 + 2 * (int)(((long)p * npair) / P));
-  const int ue = min(U0 + U, A0 + 2 * (int)(((long)(p + 1) * npair) / P));
-  if constexpr (FUSED) {
-    constexpr int TPH = D / 16;                 // lanes per head row
-    constexpr int RPP = 64 / TPH;               // head rows per pass
-    const int sub = lane % TPH;
-    const bool writer = p == P - 1;
-    // head rows r0 + lane / TPH, r0 = 0, RPP, ...: the first pass's loads are issued ahead of the
-    // first K/V units (pro_issue); further passes (nq + 2 > RPP) issue their own
-    RopeLane<D, true, QK_NORM, HAS_BIAS, SPLIT> rl;
-    int slot = -1;
-    auto row_head = [&](int r0, int& hs, bool& act, int& h) {
-      hs = r0 + lane / TPH;
-      act = hs < nq + 2;
-      h = hs < nq ? hq0 + hs : (hs == nq ? Hq + kvh : Hq + Hkv + kvh);
-    };
-    auto pro_issue = [&]() {
-      int hs, h;
-      bool act;
-      row_head(0, hs, act, h);
-      rl.issue(rope.src, b, act ? h : 0, act, sub, Hq, Hkv, rope.cos_sin, pos_b);
-      if (writer) slot = slot_b;
-    };
-    auto prologue = [&]() {
-      for (int i = lane; i < (D / 32) * 64; i += 64)
-        if ((i & 15) >= nq) qs[i >> 6][i & 63] = bf16x8{};
-      for (int r0 = 0; r0 < nq + 2; r0 += RPP) {        // wave-uniform trip count
-        int hs, h;
-        bool act;
-        row_head(r0, hs, act, h);
-        if (r0 > 0) rl.issue(rope.src, b, act ? h : 0, act, sub, Hq, Hkv, rope.cos_sin, pos_b);
-        float a[8], bv[8];
-        rl.finish(rope.src, b, act ? h : 0, act, sub, Hq, Hkv, rope.cos_sin, a, bv);
-        if (act) {
-          bf16x8 oa, ob;
-#pragma unroll
-          for (int j = 0; j < 8; ++j) { oa[j] = f2bf(a[j]); ob[j] = f2bf(bv[j]); }
-          int e0, e1;
-          rope_lane_offsets<D, true>(sub, e0, e1);
-          if (hs < nq) {
-            qs[e0 / 32][16 * ((e0 % 32) / 8) + hs] = oa;
-            qs[e1 / 32][16 * ((e1 % 32) / 8) + hs] = ob;
-          } else if (writer) {
-            bf16_t* nw = hs == nq ? knew : vnew;
-            *reinterpret_cast<bf16x8*>(nw + e0) = oa;
-            *reinterpret_cast<bf16x8*>(nw + e1) = ob;
-            if (slot >= 0)   // for later steps; this one reads the token from LDS
-              rope_lane_store_kv<D, true>(const_cast<bf16_t*>(kc), const_cast<bf16_t*>(vc), slot,
-                                          bs, Hkv, kvh, hs == nq + 1, sub, oa, ob);
-          }
-        }
-      }
-      __syncthreads();
-    };
-    attn_units_deep<D, EIA_WAVE_NS_FUSED>(acc, qs, kc, vc, bt, bt_win, ub, ue, L, kvh, Hkv, bs, scale_log2,
-                                    kv_lo, pro_issue, prologue, writer && L > 0 ? L - 1 : -1,
-                                    knew, vnew);
-  } else {
-    const bool cval = c < nq;
-    const bf16_t* qp = q + (long)b * q_stride + (long)(hq0 + (cval ? c : 0)) * D + 8 * g;
-#pragma unroll
-    for (int s = 0; s < D / 32; ++s) {
-      bf16x8 t = *reinterpret_cast<const bf16x8*>(qp + 32 * s);
-      if (!cval) t = bf16x8{};
-      qs[s][lane] = t;
-    }
-    __syncthreads();
-    attn_units_deep<D, EIA_WAVE_NS>(acc, qs, kc, vc, bt, bt_win, ub, ue, L, kvh, Hkv, bs, scale_log2,
-                                    kv_lo, [] {}, [] {}, -1, nullptr, nullptr);
-  }
-  ATRACE(3);
-  // lane (c, g) holds O^T rows d = 16 dt + 4 g + i of query column c; l is lane-partial
-  float lt = acc.l;
-  lt += __shfl_xor(lt, 16, 64);
-  lt += __shfl_xor(lt, 32, 64);
-  const bool valid = c < nq;
-  const int hq = hq0 + c;
-  if (P == 1) {
-    if (valid) {
-      const float inv = lt > 0.f ? 1.f / lt : 0.f;
-      bf16_t* op = out + (long)b * out_stride + (long)hq * D + 4 * g;
-#pragma unroll
-      for (int dt = 0; dt < D / 16; ++dt) {
-        bf16x4 v;
-#pragma unroll
-        for (int i = 0; i < 4; ++i) v[i] = f2bf(acc.o[dt][i] * inv);
-        *reinterpret_cast<bf16x4*>(op + 16 * dt) = v;
-      }
-    }
-    ATRACE(5);
-    ATRACE_FLUSH();
-    return;
-  }
-  if (valid) {
-    const long pi = ((long)b * Hq + hq) * Pmax + p;
-    // agent-scope (sc1) stores: coherent for the merging wave on another XCD
-#pragma unroll
-    for (int dt = 0; dt < D / 16; ++dt)
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-        __hip_atomic_store(part_o + pi * D + 16 * dt + 4 * g + i, acc.o[dt][i], __ATOMIC_RELAXED,
-                           __HIP_MEMORY_SCOPE_AGENT);
-    if (g == 0) {
-      __hip_atomic_store(part_ml + 2 * pi, acc.m, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __hip_atomic_store(part_ml + 2 * pi + 1, lt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-  }
-  if (part_cnt == nullptr) return;                 // separate reduce kernel
-  __builtin_amdgcn_s_waitcnt(0);
-  __syncthreads();
-  int* cnt = part_cnt + (long)b * Hkv + kvh;
-  if (lane == 0)
-    s_last = __hip_atomic_fetch_add(cnt, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == P - 1;
-  __syncthreads();
-  if (!s_last) return;
-  auto ld = [](const float* ptr_) {
-    return __hip_atomic_load(ptr_, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  };
-  for (int idx = lane; idx < nq * D; idx += 64) {
-    const int cq = idx / D, d = idx % D;
-    const long base = ((long)b * Hq + hq0 + cq) * Pmax;
-    float M = NEG_INF;
-    for (int pp = 0; pp < P; ++pp) M = fmaxf(M, ld(part_ml + 2 * (base + pp)));
-    float Ls = 0.f, O = 0.f;
-    if (M != NEG_INF) {
-      for (int pp = 0; pp < P; ++pp) {
-        const float f = exp2f(ld(part_ml + 2 * (base + pp)) - M);
-        Ls += ld(part_ml + 2 * (base + pp) + 1) * f;
-        O += ld(part_o + (base + pp) * D + d) * f;
-      }
-    }
-    out[(long)b * out_stride + (long)(hq0 + cq) * D + d] = f2bf(Ls > 0.f ? O / Ls : 0.f);
-  }
-  if (lane == 0) __hip_atomic_store(cnt, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 // ---------------------------------------------------------------------------------- prefill
@@ -1468,14 +1085,6 @@ paged_prefill_lds_kernel(const bf16_t* __restrict__ q, long q_stride,
 
 // ---------------------------------------------------------------------------------- launchers
 
-static int decode_wave_env() {
-  static const int v = [] {
-    const char* e = getenv("EIA_DECODE_WAVE");
-    return e != nullptr ? atoi(e) : 0;
-  }();
-  return v;
-}
-
 static int decode_lean_env() {
   static const int v = [] {
     const char* e = getenv("EIA_DECODE_LEAN");
@@ -1499,21 +1108,6 @@ EIA_API int eia_paged_decode(const void* q, long q_stride, const void* k_cache, 
   const int lean_env = decode_lean_env();
   // lean form: whole 32-token units inside a block (bs % 32 == 0), uniform per-unit bases
   const bool lean = (lean_env >= 0 ? lean_env != 0 : true) && bs % 32 == 0 && D <= 128;
-  if (decode_wave_env() != 0 && lean && G <= 16 && (D == 64 || D == 128)) {
-    const DecodeRope none{};
-#define DEC_W(DD)                                                                              \
-    hipLaunchKernelGGL((paged_decode_wave_kernel<DD, false, false, false, false>),             \
-                       dim3(B, Hkv, P), dim3(64), 0, st, (const bf16_t*)q, q_stride,           \
-                       (const bf16_t*)k_cache, (const bf16_t*)v_cache, block_tables, bt_stride, \
-                       seq_lens, (bf16_t*)out, out_stride, part_o, part_ml, part_cnt, sl2, Hq,  \
-                       Hkv, bs, P, sliding_window, chunk_size, p_dyn, none);                   \
-    if (P > 1 && part_cnt == nullptr)                                                          \
-      hipLaunchKernelGGL((paged_decode_reduce_kernel<DD>), dim3(B, Hq), dim3(DD), 0, st,       \
-                         part_o, part_ml, (bf16_t*)out, out_stride, Hq, P, p_dyn);
-    if (D == 128) { DEC_W(128) } else { DEC_W(64) }
-#undef DEC_W
-    EIA_LAUNCH_CHECK();
-  }
   dim3 grid(B, Hkv * NQG, P);
   const DecodeRope none{};
 #define DEC_V(DD, LEAN_)                                                                     \
@@ -1521,7 +1115,7 @@ EIA_API int eia_paged_decode(const void* q, long q_stride, const void* k_cache, 
                      0, st, (const bf16_t*)q, q_stride, (const bf16_t*)k_cache,                \
                      (const bf16_t*)v_cache, block_tables, bt_stride, seq_lens, (bf16_t*)out,     \
                      out_stride, part_o, part_ml, part_cnt, sl2, Hq, Hkv, bs, P, NQG,             \
-                     sliding_window, chunk_size, p_dyn, nullptr, none);
+                     sliding_window, chunk_size, p_dyn, none);
 #define DEC(DD)                                                                             \
   if (lean) { DEC_V(DD, true) } else { DEC_V(DD, false) }                                  \
   if (P > 1 && part_cnt == nullptr)                                                         \
@@ -1542,8 +1136,7 @@ EIA_API int eia_paged_decode(const void* q, long q_stride, const void* k_cache, 
 // GEMM output of T >= B rows (split-K slabs `part` [sk][T][(Hq+2Hkv)*D], or bf16 rows `qkv`),
 // this step's k/v land in the cache, out [B][Hq*D] receives the attention.  NEOX RoPE only.
 // Returns EIA_UNSUPPORTED for shapes the fused form does not cover (the caller then runs the
-// two kernels).  `tail` (device int, (row << 8) | parts; used when P > 1 and part_cnt is given):
-// the tail split of paged_decode_kernel for steps whose p_dyn is 1.
+// two kernels).
 EIA_API int eia_paged_decode_rope(const void* qkv, long qkv_stride, const float* part, int sk,
                                   const void* bias, const void* q_norm_w, const void* k_norm_w,
                                   float eps, const int* positions, const float* cos_sin,
@@ -1552,7 +1145,7 @@ EIA_API int eia_paged_decode_rope(const void* qkv, long qkv_stride, const float*
                                   void* out, long out_stride, float* part_o, float* part_ml,
                                   int* part_cnt, float scale, int B, int Hq, int Hkv, int D, int bs,
                                   int P, int sliding_window, int chunk_size, const int* p_dyn,
-                                  const int* tail, hipStream_t st) {
+                                  hipStream_t st) {
   if (B < 0 || B > T || Hkv <= 0 || Hq % Hkv != 0 || P < 1) return EIA_BAD_SHAPE;
   if (P > 1 && (part_o == nullptr || part_ml == nullptr)) return EIA_BAD_SHAPE;
   if ((q_norm_w == nullptr) != (k_norm_w == nullptr)) return EIA_BAD_SHAPE;
@@ -1569,20 +1162,11 @@ EIA_API int eia_paged_decode_rope(const void* qkv, long qkv_stride, const float*
                                (const bf16_t*)q_norm_w, (const bf16_t*)k_norm_w, eps},
                         positions, cos_sin, slot_mapping};
   dim3 grid(B, Hkv, P);
-  const bool wave = decode_wave_env() != 0;
 #define DEC_F(DD, SP, QN, HB)                                                                    \
-  if (wave)                                                                                      \
-    hipLaunchKernelGGL((paged_decode_wave_kernel<DD, true, SP, QN, HB>), grid, dim3(64), 0, st,   \
-                       nullptr, 0L, (const bf16_t*)k_cache, (const bf16_t*)v_cache,              \
-                       block_tables, bt_stride, seq_lens, (bf16_t*)out, out_stride, part_o,       \
-                       part_ml, part_cnt, sl2, Hq, Hkv, bs, P, sliding_window, chunk_size, p_dyn, \
-                       rope);                                                                    \
-  else                                                                                           \
     hipLaunchKernelGGL((paged_decode_kernel<DD, true, true, SP, QN, HB>), grid, dim3(256), 0, st,  \
                        nullptr, 0L, (const bf16_t*)k_cache, (const bf16_t*)v_cache, block_tables,  \
                        bt_stride, seq_lens, (bf16_t*)out, out_stride, part_o, part_ml, part_cnt,    \
-                       sl2, Hq, Hkv, bs, P, 1, sliding_window, chunk_size, p_dyn,            \
-                       P > 1 && part_cnt != nullptr ? tail : nullptr, rope);
+                       sl2, Hq, Hkv, bs, P, 1, sliding_window, chunk_size, p_dyn, rope);
 #define DEC_FQ(DD, SP)                                                                           \
   if (q_norm_w) { if (bias) { DEC_F(DD, SP, true, true) } else { DEC_F(DD, SP, true, false) } }  \
   else { if (bias) { DEC_F(DD, SP, false, true) } else { DEC_F(DD, SP, false, false) } }

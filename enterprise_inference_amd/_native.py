@@ -41,12 +41,10 @@ _SIGNATURES = {
     "eia_rope_qkv_cache": [P, L, P, I, IP, P, IP, P, P, P, P, P, P, F, I, I, I, I, I, I, S],
     "eia_paged_decode": [P, L, P, P, IP, I, IP, P, L, P, P, P, F, I, I, I, I, I, I, I, I, IP, S],
     "eia_paged_decode_rope": [P, L, P, I, P, P, P, F, IP, P, IP, I, P, P, IP, I, IP, P, L, P, P, P,
-                              F, I, I, I, I, I, I, I, I, IP, IP, S],
+                              F, I, I, I, I, I, I, I, I, IP, S],
     "eia_paged_prefill": [P, L, P, L, P, P, IP, I, IP, IP, IP, I, F, I, I, I, I, I, I, I, I, I, S],
     "eia_paged_prefill_fa": [P, L, P, L, P, P, IP, I, IP, IP, IP, I, F, I, I, I, I, I, I, I, S],
     "eia_act_and_mul": [P, P, I, I, L, L, I, S],
-    "eia_mall_prefetch": [P, L, I, P, S],
-    "eia_gemm_swiglu_balanced": [P, L, P, L, P, L, I, I, I, P, P, S],
     "eia_act": [P, P, L, I, S],
     "eia_sample": [P, L, I, I, P, P, P, P, P, P, S],
     "eia_apply_penalties": [P, L, P, P, P, I, P, P, P, S],

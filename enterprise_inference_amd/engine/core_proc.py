@@ -196,7 +196,11 @@ def core_main(fd: int) -> int:
         return 1
     from ..utils.gc_tuning import tune_after_startup
     tune_after_startup()
-    sock.sendall(encode_frame(("ready", {"num_blocks": engine.num_blocks, "pid": os.getpid()})))
+    from ..parallel import custom_allreduce as _car
+    ready = {"num_blocks": engine.num_blocks, "pid": os.getpid()}
+    if cfg.parallel.tensor_parallel_size > 1:
+        ready["custom_allreduce"] = {k: v for k, v in _car.STATUS.items() if k != "tuning"}
+    sock.sendall(encode_frame(("ready", ready)))
     log_requests = bool(opts.get("log_requests"))
     fault = opts.get("fault", "")
     crash_after = int(fault.split(":")[1]) if fault.startswith("crash_after:") else None
@@ -497,6 +501,8 @@ class MPEngineClient:
             self.info = msg[1]
             if self.metrics is not None:
                 self.metrics.set_healthy(True)
+                if "custom_allreduce" in self.info:
+                    self.metrics.set_custom_allreduce(self.info["custom_allreduce"])
             logger.info("engine core ready: %s", self.info)
             self._ready_evt.set()
         elif kind == "dead":

@@ -450,12 +450,6 @@ class ModelRunner:
             return 1
         return attn_ops.decode_partitions(B, self.num_kv_heads, self.num_heads, max_len)
 
-    def _tail_possible(self, Bp: int) -> bool:
-        """Some batch of <= Bp rows gets the fused decode kernel's tail split
-        (ops/attention.py decode_tail)."""
-        return (attn_ops.DECODE_TAIL_P >= 2 and Bp * self.num_kv_heads > self.num_cus and
-                self.num_heads // self.num_kv_heads <= 16)
-
     def _prepare_graph(self, bm: BlockManager, decodes: List[ScheduledSeq], Bp: int) -> dict:
         S = self.max_num_seqs
         hdr = self.g_hdr.numpy()
@@ -475,8 +469,6 @@ class ModelRunner:
             hdr[so + n:so + Bp] = -1
         max_len = int(hdr[3 * S:3 * S + n].max()) if n else 1
         hdr[4 * S] = min(self._decode_partitions(Bp, max_len), self.graph_P.get(Bp, 1))
-        tail = attn_ops.decode_tail(n, self.num_kv_heads, self.num_heads, self.num_cus)
-        hdr[4 * S + 1] = attn_ops.DECODE_TAIL_OFF if tail is None else tail
         return StepPlan("graph", Bp=Bp, nd=n)
 
     def _upload_graph(self, Bp: int) -> None:  # noqa: D401 - H2D of the graph header
@@ -491,7 +483,7 @@ class ModelRunner:
             positions=d[S:S + Bp], decode_block_tables=self.d_g_bt[:Bp * self.maxb].view(Bp, self.maxb),
             decode_seq_lens=d[3 * S:3 * S + Bp], decode_partitions=P, decode_part_o=self.part_o,
             decode_part_ml=self.part_ml, decode_part_cnt=self.part_cnt,
-            decode_p_dyn=d[4 * S:4 * S + 1], decode_tail=d[4 * S + 1:4 * S + 2])
+            decode_p_dyn=d[4 * S:4 * S + 1])
         return d[:Bp], md
 
     def _graph_forward(self, Bp: int, P: int) -> torch.Tensor:
@@ -911,7 +903,6 @@ class ModelRunner:
         hdr[2 * S:3 * S] = -1
         hdr[3 * S:4 * S] = 1
         hdr[4 * S] = 1
-        hdr[4 * S + 1] = attn_ops.DECODE_TAIL_OFF
         hdr[self.src_off:] = -1
         self.d_g_hdr.copy_(hdr)
         self.d_g_bt.zero_()
@@ -920,8 +911,6 @@ class ModelRunner:
         with torch.cuda.stream(stream):
             for bi, Bp in enumerate(sorted(buckets, reverse=True)):
                 P = self._decode_partitions(Bp, self.cfg.scheduler.max_model_len)
-                if self._tail_possible(Bp):
-                    P = max(P, attn_ops.DECODE_TAIL_P)   # grid.z room for the tail split
                 self.graph_P[Bp] = P          # upper bound; the step's P is read on device
                 # warm-up (hipBLASLt heuristics, allocator); VLLM_SKIP_WARMUP: first bucket only
                 for _ in range((1 if bi == 0 else 0) if self.cfg.skip_warmup else 2):

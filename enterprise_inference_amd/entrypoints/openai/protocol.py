@@ -121,6 +121,9 @@ class _SamplingFields(OpenAIBase):
             from ...engine.grammar import validate_grammar
             validate_grammar(self.guided_grammar)      # reject unsupported grammars with a 400
         max_tokens = self.max_tokens if self.max_tokens is not None else default_max_tokens
+        min_p = self.min_p if self.min_p is not None else gd.get("min_p", 0.0)
+        repetition_penalty = self.repetition_penalty if self.repetition_penalty is not None \
+            else gd.get("repetition_penalty", 1.0)
         if self.use_beam_search:
             # beam search ranks candidates by log-prob: deterministic, unfiltered rows (an
             # explicit non-zero temperature / top_p / top_k is a client error)
@@ -129,13 +132,19 @@ class _SamplingFields(OpenAIBase):
             temperature = 0.0
             top_p = 1.0 if self.top_p is None else top_p
             top_k = -1 if self.top_k is None else top_k
+            # the model's generation defaults are sampling settings: they do not apply to beams
+            min_p = 0.0 if self.min_p is None else min_p
+            repetition_penalty = 1.0 if self.repetition_penalty is None else repetition_penalty
+            if self.stop:
+                # beams end on EOS / stop_token_ids only (hypotheses are ranked on token ids)
+                raise ValueError("use_beam_search does not support stop strings; "
+                                 "use stop_token_ids")
         return SamplingParams(
             n=self.n or 1, best_of=self.best_of, temperature=temperature, top_p=top_p,
-            top_k=top_k, min_p=self.min_p if self.min_p is not None else gd.get("min_p", 0.0),
+            top_k=top_k, min_p=min_p,
             presence_penalty=self.presence_penalty or 0.0,
             frequency_penalty=self.frequency_penalty or 0.0,
-            repetition_penalty=self.repetition_penalty if self.repetition_penalty is not None
-            else gd.get("repetition_penalty", 1.0),
+            repetition_penalty=repetition_penalty,
             seed=self.seed, stop=self.stop, stop_token_ids=self.stop_token_ids,
             ignore_eos=self.ignore_eos, max_tokens=max(1, max_tokens), min_tokens=self.min_tokens,
             logprobs=logprobs, skip_special_tokens=self.skip_special_tokens,

@@ -64,6 +64,10 @@ class EngineMetrics:
                                    registry=r)
         self.engine_healthy = Gauge("eia:engine_healthy", "1 while the engine loop is alive", L,
                                     registry=r)
+        self.custom_ar = Gauge("eia:custom_allreduce_active",
+                               "1 when TP collectives use the custom xGMI kernel, 0 when the "
+                               "init self-test / setup sent them to RCCL (label: reason)",
+                               L + ["reason"], registry=r)
         self._last_prompt = 0
         self._last_gen = 0
         self._last_preempt = 0
@@ -112,6 +116,11 @@ class EngineMetrics:
         for c in out.outputs:
             self.success.labels(model_name=self.model_name,
                                 finished_reason=c.finish_reason or "abort").inc()
+
+    def set_custom_allreduce(self, status: dict) -> None:
+        self.custom_ar.labels(model_name=self.model_name,
+                              reason=str(status.get("reason", "?"))).set(
+            1 if status.get("active") else 0)
 
     def set_healthy(self, ok: bool) -> None:
         self._l(self.engine_healthy).set(1 if ok else 0)

@@ -19,7 +19,6 @@ import torch.nn.functional as F
 
 from ..config import ModelConfig
 from ..ops import activation, gemm  # noqa: F401
-from ..ops import prefetch as prefetch_ops
 from ..ops.attention import AttentionMetadata, attention, decode_rope_attention
 from ..ops.rotary import RotaryCache, rope_qkv_cache
 from ..parallel import state
@@ -58,12 +57,9 @@ class LlamaAttention(nn.Module):
             if cfg.extra["no_rope_layers"][layer_idx]:
                 self.chunk_size = cfg.attention_chunk_size
 
-    def forward(self, h: torch.Tensor, md: AttentionMetadata, kv: KVCache,
-                prefetch=None) -> torch.Tensor:
+    def forward(self, h: torch.Tensor, md: AttentionMetadata, kv: KVCache) -> torch.Tensor:
         T = h.shape[0]
         qkv = gemm.linear(h, self.qkv_proj.weight, defer_reduce=True)   # split-K summed in K4
-        # weights for the GEMMs after attention, swept into the Infinity Cache beside it
-        join = prefetch_ops.fork(prefetch) if prefetch else None
         qn = None if self.q_norm is None else self.q_norm.weight
         kn = None if self.k_norm is None else self.k_norm.weight
         # pure decode: K4 (reduce/bias/qk-norm/RoPE/KV write) runs inside the attention kernel
@@ -77,8 +73,6 @@ class LlamaAttention(nn.Module):
                                bias=self.qkv_proj.bias, q_norm_w=qn, k_norm_w=kn,
                                norm_eps=self.cfg.rms_norm_eps)
             o = attention(q, kv[0], kv[1], md, self.scale, self.sliding_window, self.chunk_size)
-        if join is not None:
-            join()
         return self.o_proj(o.view(-1, self.num_heads * self.head_dim)[:T], defer_reduce=True)
 
 
@@ -104,27 +98,13 @@ class LlamaDecoderLayer(nn.Module):
         self.input_layernorm = RMSNorm(cfg.hidden_size, cfg.rms_norm_eps, dtype, device)
         self.post_attention_layernorm = RMSNorm(cfg.hidden_size, cfg.rms_norm_eps, dtype, device)
 
-    def _prefetch_ranges(self, h, md):
-        """Pure-decode GPU steps on one rank (EIA_MALL_PREFETCH): the O projection and a
-        prefix of gate_up, read into the Infinity Cache while attention runs."""
-        if not (prefetch_ops.ENABLED and h.is_cuda and md.num_prefill_tokens == 0
-                and h.shape[0] <= gemm.MAX_M and state.tp_size() == 1):
-            return None
-        ranges = [(self.self_attn.o_proj.weight, None)]
-        gu = getattr(self.mlp, "gate_up_proj", None)
-        if prefetch_ops.GATE_MB and gu is not None:
-            ranges.append((gu.weight, prefetch_ops.GATE_MB << 20))
-        return ranges
-
     def forward(self, h, residual, md, kv):
         if residual is None:
             residual = h
             h = self.input_layernorm(h)
         else:
             h, residual = self.input_layernorm(h, residual)
-        pf = self._prefetch_ranges(h, md)
-        # (attention subclasses, e.g. Llama-4's, take no prefetch hook)
-        h = self.self_attn(h, md, kv, prefetch=pf) if pf else self.self_attn(h, md, kv)
+        h = self.self_attn(h, md, kv)
         h, residual = self.post_attention_layernorm(h, residual)
         return self.mlp(h), residual
 

@@ -23,6 +23,7 @@ non-causal tokens per tile, once per image -- not a hot path).
 from __future__ import annotations
 
 import base64
+import contextlib
 import io
 import os
 import math
@@ -76,7 +77,16 @@ def _remote_media_policy():
     return not off, (doms or None), priv
 
 
-def _check_url(url: str) -> None:
+def _non_public(ip) -> bool:
+    return (ip.is_private or ip.is_loopback or ip.is_link_local or ip.is_reserved or
+            ip.is_multicast or ip.is_unspecified)
+
+
+def _check_url(url: str):
+    """Apply the media policy to ``url``.  Returns the one validated address the fetch must
+    dial (``None`` when private targets are allowed and the name is resolved by the client
+    as usual).  Resolving once and connecting to exactly that address closes the DNS
+    rebinding window between the check and the connection."""
     import ipaddress
     import socket
     from urllib.parse import urlparse
@@ -84,30 +94,76 @@ def _check_url(url: str) -> None:
     enabled, domains, allow_private = _remote_media_policy()
     if not enabled:
         raise ValueError("remote image URLs are disabled on this server")
-    host = (urlparse(url).hostname or "").lower()
+    u = urlparse(url)
+    if u.scheme not in ("http", "https"):
+        raise ValueError("image URL must be http(s)")
+    host = (u.hostname or "").lower()
     if not host:
         raise ValueError("image URL has no host")
     if domains is not None and not any(host == d or host.endswith("." + d) for d in domains):
         raise ValueError(f"image host {host!r} is not in the allowed media domains")
-    if not allow_private:
-        for info in socket.getaddrinfo(host, None):
-            ip = ipaddress.ip_address(info[4][0])
-            if ip.is_private or ip.is_loopback or ip.is_link_local or ip.is_reserved:
-                raise ValueError(f"image host {host!r} resolves to a non-public address")
+    if allow_private:
+        return None
+    addrs = [ipaddress.ip_address(info[4][0].split("%")[0])
+             for info in socket.getaddrinfo(host, u.port or (443 if u.scheme == "https" else 80),
+                                            type=socket.SOCK_STREAM)]
+    if not addrs:
+        raise ValueError(f"image host {host!r} does not resolve")
+    for ip in addrs:
+        if _non_public(ip):
+            raise ValueError(f"image host {host!r} resolves to a non-public address")
+    return addrs[0]
+
+
+def _pinned_request(url: str, ip):
+    """(url with the host replaced by the validated address, headers, extensions): the TCP
+    connection goes to ``ip`` while Host, TLS SNI and certificate checks use the name."""
+    from urllib.parse import urlparse, urlunparse
+
+    u = urlparse(url)
+    host = u.hostname
+    lit = f"[{ip}]" if ip.version == 6 else str(ip)
+    netloc = lit + (f":{u.port}" if u.port else "")
+    hdr_host = (f"[{host}]" if ":" in host else host) + (f":{u.port}" if u.port else "")
+    ext = {"sni_hostname": host} if u.scheme == "https" else {}
+    return urlunparse(u._replace(netloc=netloc)), {"Host": hdr_host}, ext
+
+
+@contextlib.contextmanager
+def _open_stream(url: str, headers: dict, extensions: dict, timeout: float):
+    """One streamed GET (no redirect following) with per-request transport extensions."""
+    import httpx
+
+    with httpx.Client(timeout=timeout, follow_redirects=False) as client:
+        req = client.build_request("GET", url, headers=headers, extensions=extensions)
+        r = client.send(req, stream=True)
+        try:
+            yield r
+        finally:
+            r.close()
 
 
 def fetch_image_bytes(url: str, max_bytes: Optional[int] = None, timeout: float = 30.0) -> bytes:
     """Download an image URL with the media policy above and a byte cap (streamed: a huge or
     endless body is cut off at ``max_bytes`` instead of being buffered).  Redirects are
-    followed by hand so every hop passes the same checks."""
-    import httpx
+    followed by hand so every hop passes the same checks, and every hop connects to the
+    address its check validated (no second DNS lookup an attacker's resolver could answer
+    with an internal address)."""
+    import ipaddress
 
     cap = MAX_IMAGE_BYTES if max_bytes is None else max_bytes
     for _ in range(5):
-        _check_url(url)
-        with httpx.stream("GET", url, timeout=timeout, follow_redirects=False) as r:
-            if r.is_redirect:
-                url = str(r.next_request.url) if r.next_request else r.headers["location"]
+        ip = _check_url(url)
+        target, headers, ext = (url, {}, {}) if ip is None else _pinned_request(url, ip)
+        with _open_stream(target, headers, ext, timeout) as r:
+            if ip is not None:      # defence in depth: the peer really is the checked address
+                stream = r.extensions.get("network_stream")
+                peer = stream.get_extra_info("server_addr") if stream is not None else None
+                if peer and ipaddress.ip_address(str(peer[0]).split("%")[0]) != ip:
+                    raise ValueError("image fetch connected to an unexpected address")
+            if r.is_redirect:      # relative locations resolve against the NAME, not the IP
+                from urllib.parse import urljoin
+                url = urljoin(url, r.headers["location"])
                 continue
             r.raise_for_status()
             n = int(r.headers.get("content-length") or 0)

@@ -127,34 +127,6 @@ def decode_partitions(batch: int, num_kv_heads: int, num_heads: int, max_len: in
     return max(1, min(p, max_parts, max_len // 128))
 
 
-# Tail split of the fused decode kernel (csrc/kernels/attention.hip paged_decode_kernel): a
-# P-1 step whose (row, KV head) items overflow a whole number of workgroup rounds by a little
-# (B 65 x 8 heads = 520 = 2 x 256 + 8) splits the surplus rows over this many partitions.
-# Off by default: measured no faster on MI355X (engine 25.9 -> 27.3 us per layer at B 65;
-# profiles/attn_batch_balance_r3.md) -- the surplus partitions' early-exit workgroups and the
-# extra prologues cost what the balance saves.
-DECODE_TAIL_P = int(os.environ.get("EIA_DECODE_TAIL", "0"))
-DECODE_TAIL_OFF = 0x7fffff00 | 1
-
-
-def decode_tail(batch: int, num_kv_heads: int, num_heads: int, cus: int = 256,
-                parts: Optional[int] = None) -> Optional[int]:
-    """Packed (row << 8) | parts for the fused decode kernel's tail split, or None.
-
-    Items = batch x KV heads (one workgroup each) run 2 per CU; when they exceed a multiple of
-    the CU count by at most half a round, the rows past that multiple are split (their pieces
-    then fill third slots instead of whole items doubling some CUs' time --
-    profiles/attn_batch_balance_r3.md).  Needs G <= 16 (one query group per KV head)."""
-    parts = DECODE_TAIL_P if parts is None else parts
-    if parts < 2 or num_heads // num_kv_heads > 16:
-        return None
-    items = batch * num_kv_heads
-    r = items % cus
-    if items <= cus or r == 0 or r > cus // 2:
-        return None
-    return (((items - r) // num_kv_heads) << 8) | min(parts, 255)
-
-
 @dataclasses.dataclass
 class AttentionMetadata:
     num_decode: int
@@ -169,7 +141,6 @@ class AttentionMetadata:
     decode_part_ml: Optional[torch.Tensor] = None
     decode_part_cnt: Optional[torch.Tensor] = None      # zeroed int32 [Bd*Hkv*ceil(G/16)]
     decode_p_dyn: Optional[torch.Tensor] = None         # device int32 [1]: partitions this step
-    decode_tail: Optional[torch.Tensor] = None          # device int32 [1]: decode_tail() packed
     # prefill part
     prefill_block_tables: Optional[torch.Tensor] = None  # [Sp, maxb] int32
     prefill_seq_lens: Optional[torch.Tensor] = None      # [Sp] int32 (context + new)
@@ -338,9 +309,7 @@ def decode_rope_attention(qkv, md: AttentionMetadata, k_cache: torch.Tensor,
         ptr(md.decode_part_cnt) if (P > 1 and md.decode_part_cnt is not None) else None,
         float(scale), B, num_heads, num_kv_heads, head_dim, k_cache.shape[2], P,
         sliding_window or 0, chunk_size or 0,
-        ptr(md.decode_p_dyn) if (P > 1 and md.decode_p_dyn is not None) else None,
-        ptr(md.decode_tail) if (P > 1 and md.decode_tail is not None and
-                                md.decode_part_cnt is not None) else None, stream(o))
+        ptr(md.decode_p_dyn) if (P > 1 and md.decode_p_dyn is not None) else None, stream(o))
     if rc == EIA_UNSUPPORTED:
         return None
     check(rc, "paged_decode_rope")

@@ -221,41 +221,6 @@ def skinny(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = None
     return s if defer_reduce else s.materialize()
 
 
-# Balanced SwiGLU (csrc/kernels/gemm_swiglu_balanced.hip): half-pair work units so every CU
-# streams the same bytes (Llama-8B: 896 pairs = 3.5 per CU).  Opt-in (EIA_SWIGLU_BALANCED=1):
-# correct, but 59.6 vs 48.4 us at M 65 (profiles/gemm_gu_probe_r3.log) -- seven waves streaming
-# half-K 128-deep chunks move ~15 GB/s per CU against the 4-pair form's ~22.
-BALANCED = os.environ.get("EIA_SWIGLU_BALANCED", "0") == "1"
-_BAL_SCRATCH = {}
-
-
-def balanced_ok(M: int, N: int, K: int) -> bool:
-    I = N // 2
-    return (BALANCED and 1 <= M <= 80 and N % 2 == 0 and I % 16 == 0
-            and ((I // 16) * 2) % 56 == 0 and K % 256 == 0)
-
-
-def _balanced_scratch(dev: torch.device, I: int):
-    key = (dev, I)
-    if key not in _BAL_SCRATCH:
-        pairs = I // 16
-        # slot per pair and half: 2 tiles x 5 m-tiles x 4 floats x 64 lanes; tickets zeroed once
-        _BAL_SCRATCH[key] = (torch.empty(pairs * 2 * 2 * 5 * 4 * 64, dtype=torch.float32, device=dev),
-                             torch.zeros(pairs, dtype=torch.int32, device=dev))
-    return _BAL_SCRATCH[key]
-
-
-def swiglu_balanced(x: torch.Tensor, w_gate_up: torch.Tensor) -> torch.Tensor:
-    M, K = x.shape
-    N = w_gate_up.shape[0]
-    part, ticket = _balanced_scratch(x.device, N // 2)
-    out = torch.empty(M, N // 2, dtype=torch.bfloat16, device=x.device)
-    check(lib().eia_gemm_swiglu_balanced(ptr(x), x.stride(0), ptr(w_gate_up), w_gate_up.stride(0),
-                                         ptr(out), out.stride(0), M, N, K, ptr(part), ptr(ticket),
-                                         stream(x)), "gemm_swiglu_balanced")
-    return out
-
-
 def linear_f32(x: torch.Tensor, w: torch.Tensor) -> Optional[torch.Tensor]:
     """x @ w^T with fp32 output straight from the skinny kernel's accumulators (the LM head:
     the sampler reads fp32 logits, so this skips the bf16 store and the separate bf16 -> fp32
@@ -277,9 +242,6 @@ def swiglu_gemm(x: torch.Tensor, w_gate_up: torch.Tensor, cfg: Optional[int] = N
     """silu(x Wg^T) * (x Wu^T) with W = [gate; up] stacked on dim 0 (K7)."""
     M, K = x.shape
     N = w_gate_up.shape[0]
-    if cfg is None and balanced_ok(M, N, K) and w_gate_up.stride(1) == 1 and \
-            w_gate_up.stride(0) % 8 == 0 and x.stride(0) % 8 == 0:
-        return swiglu_balanced(x, w_gate_up)
     if cfg is None:
         cfg = choose(M, N, K, True)[0]
     out = torch.empty(M, N // 2, dtype=torch.bfloat16, device=x.device)
@@ -340,13 +302,8 @@ def linear(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = None
     return F.linear(x, w, bias)
 
 
-_EXP_SKIP_NORM = os.environ.get("EIA_EXP_SKIP_NORM", "0") == "1"
-
-
 def splitk_add_rmsnorm(s: SplitK, residual: torch.Tensor, weight: torch.Tensor, eps: float):
     """residual += reduce(s) (+bias); returns (rmsnorm(residual) * weight, residual)."""
-    if _EXP_SKIP_NORM:       # timing experiment only (wrong numerics): the kernel's share
-        return residual, residual
     if s.bias is not None:
         h = s.materialize()
         from .norm import fused_add_rms_norm

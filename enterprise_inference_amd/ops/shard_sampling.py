@@ -3,8 +3,11 @@
 At tensor parallelism each rank holds the logits of its vocab shard only.  Rows without
 top-k / top-p / min-p are sampled per shard and only (value, id) winners cross xGMI
 (``sampling.sample_shard``).  Rows WITH filters used to all-gather the full B x V logits
-(33 MB per step for Llama-3 at B=65); here they cost a few tiny exchanges instead, and pick
-exactly the token the full-row kernel (csrc/kernels/sampling.hip ``sample_kernel``) picks:
+(33 MB per step for Llama-3 at B=65); here they cost a few tiny exchanges instead.  Top-k and
+min-p thresholds match the full-row kernel (csrc/kernels/sampling.hip ``sample_kernel``)
+exactly; the top-p threshold matches it up to the fp32 summation order of the bin masses (the
+shard histograms are summed in rank order, the kernel sums one row), so a token sitting exactly
+on the nucleus boundary can land on either side:
 
   1. global row max m                      <- gather of [B] shard maxima
   2. top-k threshold (k-th largest)         <- gather of each shard's top-kmax values [B, kmax]
@@ -36,13 +39,17 @@ _DIGIT_SHIFTS = (24, 16, 8, 0)
 
 def _pick_digit(H: torch.Tensor, remaining: torch.Tensor):
     """Per row: the digit whose bin reaches ``remaining`` counting mass from the top bin down
-    (sample_kernel's loop; no bin reaches it -> digit 0); returns (digit, mass above it)."""
+    (sample_kernel's radix_select loop); returns (digit, mass above it).  When no bin reaches
+    it (fp32 rounding of the total), the kernel settles on digit 0 with the WHOLE histogram
+    mass subtracted -- mirrored here so later rounds pick the same threshold."""
     rev = H.flip(-1)
     cum = rev.cumsum(-1)
     hit = cum >= remaining[:, None]
-    idx = torch.where(hit.any(-1), hit.to(torch.int32).argmax(-1),
+    any_hit = hit.any(-1)
+    idx = torch.where(any_hit, hit.to(torch.int32).argmax(-1),
                       torch.full_like(remaining, 255, dtype=torch.int64))
     above = cum.gather(1, idx[:, None])[:, 0] - rev.gather(1, idx[:, None])[:, 0]
+    above = torch.where(any_hit, above, H.sum(-1))
     return (255 - idx).to(torch.int64), above
 
 

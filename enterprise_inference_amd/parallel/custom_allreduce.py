@@ -13,6 +13,16 @@ Messages above ``max_bytes`` go to RCCL (parallel/comm.py).
 
 The one-shot/two-shot crossover defaults to 512 KiB (SURVEY §2.12 xGMI arithmetic:
 one-shot moves S per link with one sync, two-shot 2S/W with two).
+
+Before it serves, ``init_custom_allreduce`` checks and sizes the kernel on the real links:
+  * self-test: one-shot, two-shot and the fused add+RMSNorm at three sizes each against
+    RCCL on the same inputs (integer-valued bf16, so every correct sum is exact and the
+    comparison is bit-for-bit); any mismatch on any rank -> every rank falls back to RCCL
+    (agreed over the gloo group, never one-sided), with the reason logged and exported as
+    ``eia:custom_allreduce_active{reason=...}``;
+  * tuning: one-shot, two-shot and RCCL timed at 32 KiB..max_bytes on the current stream;
+    the per-size maxima over the ranks set the one-shot/two-shot crossover and the largest
+    message the custom kernel takes (above it RCCL wins).  EIA_AR_TUNE=0 keeps the defaults.
 """
 
 from __future__ import annotations
@@ -77,6 +87,7 @@ class CustomAllReduce:
         self.world = state.tp_size() if world is None else world
         self.cpu_group = cpu_group if cpu_group is not None else state.tp_cpu_group()
         self.max_bytes = max_bytes
+        self.use_max = max_bytes          # largest message routed here (tune() may lower it)
         self.nblocks = nblocks
         self.oneshot_max = oneshot_max or int(os.environ.get("EIA_AR_ONESHOT_MAX", 512 * 1024))
         self.lib = _native.kernels()
@@ -115,6 +126,38 @@ class CustomAllReduce:
         self.own_sig = sig
         dist.barrier(group=self.cpu_group)
 
+    @classmethod
+    def local_group(cls, world: int, max_bytes: int, nblocks: int = 16):
+        """W 'ranks' inside ONE process on one GPU (each rank's buffers are ordinary in-process
+        allocations; each rank must launch on its own stream): the kernel-level rehearsal of
+        the cross-GPU protocol used by the GPU tests, minus IPC.  Returns W instances; close
+        rank 0's to free every buffer."""
+        lib = _native.kernels()
+        objs = []
+        sigs, datas, own = [], [], []
+        for _ in range(world):
+            for nb, lst in ((lib.eia_ar_signal_bytes(), sigs), (2 * max_bytes, datas)):
+                p = ctypes.c_void_p()
+                rc = lib.eia_ar_alloc(ctypes.byref(p), ctypes.c_long(nb))
+                if rc != 0:
+                    raise RuntimeError(f"eia_ar_alloc({nb}) failed ({rc})")
+                lst.append(p.value)
+                own.append(p.value)
+        for r in range(world):
+            o = cls.__new__(cls)
+            o.rank, o.world, o.cpu_group = r, world, None
+            o.max_bytes = o.use_max = max_bytes
+            o.nblocks = nblocks
+            o.oneshot_max = int(os.environ.get("EIA_AR_ONESHOT_MAX", 512 * 1024))
+            o.lib = lib
+            o._own = own if r == 0 else []
+            o._opened = []
+            o._sig_arr = (ctypes.c_void_p * world)(*sigs)
+            o._data_arr = (ctypes.c_void_p * world)(*datas)
+            o.own_sig = sigs[r]
+            objs.append(o)
+        return objs
+
     def _alloc(self, nbytes: int) -> int:
         p = ctypes.c_void_p()
         rc = self.lib.eia_ar_alloc(ctypes.byref(p), ctypes.c_long(nbytes))
@@ -125,7 +168,7 @@ class CustomAllReduce:
 
     def should_use(self, x: torch.Tensor) -> bool:
         n = x.numel() * x.element_size()
-        return (x.is_cuda and x.dtype == torch.bfloat16 and x.is_contiguous() and n <= self.max_bytes
+        return (x.is_cuda and x.dtype == torch.bfloat16 and x.is_contiguous() and n <= self.use_max
                 and x.numel() % 8 == 0)
 
     def all_reduce(self, x: torch.Tensor, out: Optional[torch.Tensor] = None,
@@ -247,15 +290,172 @@ class ErrorPoller:
             self._event.record()
 
 
-def init_custom_allreduce(max_bytes: int) -> Optional[CustomAllReduce]:
-    if state.tp_size() == 1 or not torch.cuda.is_available():
-        return None
-    if state.tp_size() > CustomAllReduce.MAX_RANKS:
-        return None
+# ----------------------------------------------------------------------------- init checks
+
+STATUS = {"active": False, "reason": "not initialised"}
+
+
+def selftest_cases(max_bytes: int, oneshot_max: int, hidden: int = 4096):
+    """(op, shape, kind) of the init-time self-test: plain all-reduce at a small, a
+    crossover-sized and a large message in both forms, and the fused add+RMSNorm at decode
+    rows in both forms (only shapes the kernel accepts within ``max_bytes``)."""
+    cases = []
+    for nbytes in (16 << 10, oneshot_max, min(4 << 20, max_bytes)):
+        n = max(8, (nbytes // 2) // 8 * 8)
+        if 2 * n <= max_bytes:
+            cases += [("ar", (n,), 0), ("ar", (n,), 1)]
+    for T in (1, 65, 256):
+        if T * hidden * 2 <= max_bytes:
+            cases += [("norm", (T, hidden), 0), ("norm", (T, hidden), 1)]
+    return cases
+
+
+def selftest_inputs(case, rank: int, device, seed: int = 1234):
+    """Integer-valued bf16 inputs in [-4, 4] (rank-dependent), so any correct reduction over
+    <= 8 ranks is exact in bf16 and results compare bit-for-bit; the residual and norm weight
+    are the same on every rank."""
+    op, shape, kind = case
+    g = torch.Generator(device="cpu").manual_seed(seed + 7919 * rank + sum(shape) + kind)
+    x = torch.randint(-4, 5, shape, generator=g).to(torch.bfloat16)
+    if op == "ar":
+        return (x.to(device),)
+    g2 = torch.Generator(device="cpu").manual_seed(seed + sum(shape))
+    res = torch.randint(-8, 9, shape, generator=g2).to(torch.bfloat16)
+    w = (1.0 + torch.rand(shape[1], generator=g2)).to(torch.bfloat16)
+    return x.to(device), res.to(device), w.to(device)
+
+
+def run_self_test(ar, reference, device, cases=None, eps: float = 1e-5) -> Optional[str]:
+    """Every case through ``ar`` and through ``reference(x) -> sum over ranks`` (RCCL);
+    returns None when all match, else a short description of the first mismatches."""
+    from ..ops import norm as norm_ops
+    bad = []
+    for case in cases if cases is not None else selftest_cases(ar.max_bytes, ar.oneshot_max):
+        op, shape, kind = case
+        t = selftest_inputs(case, ar.rank, device)
+        if op == "ar":
+            want = reference(t[0].clone())
+            got = ar.all_reduce(t[0].clone(), kind=kind)
+            ok = torch.equal(got, want)
+            err = 0.0 if ok else float((got.float() - want.float()).abs().max())
+        else:
+            x, res, w = t
+            s = reference(x.clone())
+            r_want = res.clone()
+            want, r_want = norm_ops.fused_add_rms_norm(s, r_want, w, eps)
+            r_got = res.clone()
+            got = ar.add_rmsnorm(x.clone(), r_got, w, eps, twoshot=bool(kind))
+            ok = torch.equal(r_got, r_want) and bool(
+                torch.allclose(got.float(), want.float(), rtol=1e-2, atol=1e-2))
+            err = 0.0 if ok else max(float((r_got.float() - r_want.float()).abs().max()),
+                                     float((got.float() - want.float()).abs().max()))
+        if not ok:
+            bad.append(f"{op}{'/2shot' if kind else '/1shot'} {tuple(shape)} max|err| {err:.3g}")
+    if torch.cuda.is_available():
+        torch.cuda.synchronize()
+    if ar.error_flag():
+        bad.append("barrier spin limit hit during the self-test")
+    return "; ".join(bad[:4]) if bad else None
+
+
+def _time_us(fn, iters: int = 20) -> float:
+    fn()
+    torch.cuda.synchronize()
+    a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    a.record()
+    for _ in range(iters):
+        fn()
+    b.record()
+    b.synchronize()
+    return a.elapsed_time(b) * 1e3 / iters
+
+
+def tune_thresholds(sizes, t_one, t_two, t_rccl, max_bytes: int):
+    """(oneshot_max, use_max) from per-size timings (bytes, us; the max over ranks).
+    one-shot serves every size up to the last one where it still beats two-shot (from the
+    small end, contiguous); the custom kernel takes messages up to the last size where its
+    better form beats RCCL."""
+    oneshot_max = sizes[0]
+    for sz, a, b in zip(sizes, t_one, t_two):
+        if a > b:
+            break
+        oneshot_max = sz
+    use_max = 0
+    for sz, a, b, r in zip(sizes, t_one, t_two, t_rccl):
+        if min(a, b) <= r:
+            use_max = sz
+        else:
+            break
+    return oneshot_max, min(use_max, max_bytes)
+
+
+def run_tuning(ar, rccl_all_reduce, agree_max) -> dict:
+    """Time one-shot / two-shot / RCCL per size on this rank; ``agree_max`` reduces the timing
+    vector to its element-wise max over the ranks (same decision everywhere)."""
+    sizes = [s for s in (32 << 10, 128 << 10, 512 << 10, 1 << 20, 2 << 20, 4 << 20, 8 << 20,
+                         16 << 20, 32 << 20) if s <= ar.max_bytes]
+    rows = []
+    for sz in sizes:
+        x = torch.ones(sz // 2, dtype=torch.bfloat16, device="cuda")
+        rows.append([_time_us(lambda: ar.all_reduce(x, kind=0)),
+                     _time_us(lambda: ar.all_reduce(x, kind=1)),
+                     _time_us(lambda: rccl_all_reduce(x))])
+    t = agree_max(torch.tensor(rows, dtype=torch.float64)).tolist()
+    one, two, rc = [r[0] for r in t], [r[1] for r in t], [r[2] for r in t]
+    oneshot_max, use_max = tune_thresholds(sizes, one, two, rc, ar.max_bytes)
+    return {"sizes": sizes, "oneshot_us": one, "twoshot_us": two, "rccl_us": rc,
+            "oneshot_max": oneshot_max, "use_max": use_max}
+
+
+def init_custom_allreduce(max_bytes: int, factory=None, reference=None, agree=None,
+                          tune: Optional[bool] = None) -> Optional[CustomAllReduce]:
+    """Build the custom all-reduce for this TP group, self-test it against RCCL and size it;
+    returns None (RCCL everywhere) when any rank cannot map the peers or any rank's
+    self-test mismatches.  ``factory`` / ``reference`` / ``agree`` are injection points for
+    the tests (defaults: CustomAllReduce, RCCL on the TP group, MIN/MAX over the gloo group)."""
+    global STATUS
+    cpu_group = None
+    if factory is None:
+        if state.tp_size() == 1 or not torch.cuda.is_available():
+            return None
+        if state.tp_size() > CustomAllReduce.MAX_RANKS:
+            STATUS = {"active": False, "reason": "tp_size > 8"}
+            return None
+        factory = CustomAllReduce
+        cpu_group = state.tp_cpu_group()
+    if reference is None:
+        def reference(x):
+            dist.all_reduce(x, group=state.tp_group())
+            return x
+    if agree is None:
+        def agree(t, op):
+            dist.all_reduce(t, op=op, group=cpu_group or state.tp_cpu_group())
+            return t
     try:
-        ar = CustomAllReduce(max_bytes)
+        ar = factory(max_bytes)
     except Exception as e:   # noqa: BLE001 - RCCL remains correct
         logger.warning("custom all-reduce disabled: %s", e)
+        STATUS = {"active": False, "reason": "setup failed"}
         return None
+    try:
+        why = run_self_test(ar, reference, getattr(ar, "device", "cuda"))
+    except Exception as e:   # noqa: BLE001 - a crashing self-test is a failed one
+        why = f"self-test raised {e!r}"
+    ok = agree(torch.tensor([0 if why else 1], dtype=torch.int32), dist.ReduceOp.MIN)
+    if int(ok.item()) == 0:
+        logger.error("custom all-reduce self-test FAILED (%s); every TP rank uses RCCL",
+                     why or "on another rank")
+        ar.close()
+        STATUS = {"active": False, "reason": "self-test mismatch"}
+        return None
+    info = {}
+    tune = (os.environ.get("EIA_AR_TUNE", "1") != "0") if tune is None else tune
+    if tune and torch.cuda.is_available():
+        info = run_tuning(ar, reference, lambda t: agree(t, dist.ReduceOp.MAX))
+        ar.oneshot_max, ar.use_max = info["oneshot_max"], info["use_max"]
+        logger.info("custom all-reduce tuned: one-shot <= %d B, custom <= %d B (RCCL above)",
+                    ar.oneshot_max, ar.use_max)
+    STATUS = {"active": True, "reason": "ok", "oneshot_max": ar.oneshot_max,
+              "use_max": ar.use_max, **({"tuning": info} if info else {})}
     comm.set_custom_allreduce(ar)
     return ar

@@ -62,8 +62,6 @@ def main():
                     help="allocate a KV pool of this many blocks and spread the batch's blocks "
                          "over it at random (engine-sized pools)")
     ap.add_argument("--p-only", type=int, nargs="*", default=None, help="partition counts to time")
-    ap.add_argument("--tail-parts", type=int, nargs="*", default=[],
-                    help="also time the fused form's tail split with these partition counts")
     ap.add_argument("--fused-sk", type=int, default=0,
                     help="also time the fused RoPE form (eia_paged_decode_rope) fed by sk fp32 "
                          "split-K slabs, as in the engine's pure-decode steps")
@@ -114,20 +112,10 @@ def main():
                 pos = torch.full((B,), L - 1, dtype=torch.int32, device=dev)
                 cs = torch.randn(L + 1, a.d, device=dev)
                 slot = (bt[:, (L - 1) // a.bs].long() * a.bs + (L - 1) % a.bs).to(torch.int32)
-                # (P, tail): tail = the tail split of a P-1 step over a grid.z = P launch
-                variants = [(P, None) for P in (a.p_only or (1, 2))]
-                for parts in a.tail_parts:
-                    tv = attention.decode_tail(B, a.hkv, a.hq, parts=parts)
-                    if tv is not None:
-                        variants.append((parts, tv))
-                if a.tail_parts:   # remap + surplus-partition exits alone (no row split)
-                    variants.append((2, attention.DECODE_TAIL_OFF))
-                for P, tail in variants:
+                for P in (a.p_only or (1, 2)):
                     po = torch.empty(B * a.hq * P * a.d, device=dev)
                     pml = torch.empty(B * a.hq * P * 2, device=dev)
                     cnt = torch.zeros(B * a.hq, dtype=torch.int32, device=dev)
-                    one = torch.ones(1, dtype=torch.int32, device=dev)
-                    td = torch.tensor([tail or 0], dtype=torch.int32, device=dev)
 
                     def fused_call():
                         rc = lib().eia_paged_decode_rope(
@@ -135,13 +123,11 @@ def main():
                             ptr(cs), ptr(slot), B, ptr(k), ptr(v), ptr(bt), bt.stride(0), ptr(sl),
                             ptr(out), out.stride(0), ptr(po) if P > 1 else None,
                             ptr(pml) if P > 1 else None, ptr(cnt) if P > 1 else None,
-                            float(a.d ** -0.5), B, a.hq, a.hkv, a.d, a.bs, P, 0, 0,
-                            ptr(one) if tail else None, ptr(td) if tail else None, stream(out))
+                            float(a.d ** -0.5), B, a.hq, a.hkv, a.d, a.bs, P, 0, 0, None,
+                            stream(out))
                         assert rc == 0, rc
                     t = graph_time(fused_call)
-                    kind = ("rope" if not tail else
-                            "rope-remap" if tail == attention.DECODE_TAIL_OFF else "rope-tail")
-                    res.append((round(t - flush_us, 2), P, kind))
+                    res.append((round(t - flush_us, 2), P, "rope"))
             res.sort(key=lambda r: r[0])
             auto = attention.decode_partitions(B, a.hkv, a.hq, L)
             print(json.dumps({"B": B, "ctx": L, "best_us": res[0][0], "best_P": res[0][1],

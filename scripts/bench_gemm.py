@@ -133,9 +133,6 @@ def main():
                                   "note": "tuned table routes this shape to hipBLASLt"}), flush=True)
                 continue
             results = []
-            if swiglu and gemm.balanced_ok(M, N, K) and not a.packed:
-                fb = lambda i: gemm.swiglu_balanced(x, ws[i % pool])
-                results.append((graph_time(fb, a.iters), "balanced", 1))
             for cfg, sk in cands:
                 if swiglu:
                     f = lambda i, cfg=cfg: gemm.swiglu_gemm(

@@ -64,37 +64,3 @@ def test_swizzled_stores_are_a_permutation():
     v = {(d * 64 + 16 * (j ^ vswz(d))) for d in range(D) for j in range(4)}
     assert len(k) == 32 * D // 8 and max(k) < 32 * D * 2
     assert len(v) == D * 4 and max(v) < D * 64
-
-
-def _tail_remap(lin, X, Y, Z):
-    """Python model of paged_decode_kernel's dispatch remap under the tail split."""
-    if lin < X * Y:
-        return lin // Y, lin % Y, 0
-    e = lin - X * Y
-    R = Y * (Z - 1)
-    r, rem = divmod(e, R)
-    p = 1 + rem // Y
-    return X - 1 - r, rem - (p - 1) * Y, p
-
-
-def test_tail_split_dispatch_remap_is_a_bijection():
-    for X, Y, Z in [(65, 8, 4), (72, 8, 2), (1, 8, 3), (40, 4, 4), (7, 1, 5)]:
-        seen = [_tail_remap(lin, X, Y, Z) for lin in range(X * Y * Z)]
-        assert sorted(seen) == [(b, y, p) for b in range(X) for y in range(Y) for p in range(Z)]
-        # partition 0 row-major first, then the last row's pieces
-        assert seen[:Y] == [(0, y, 0) for y in range(Y)]
-        if Z > 1:
-            assert seen[X * Y] == (X - 1, 0, 1)
-
-
-def test_decode_tail_choice():
-    from enterprise_inference_amd.ops.attention import decode_tail
-    assert decode_tail(65, 8, 32, parts=4) == (64 << 8) | 4      # 520 = 2 x 256 + 8
-    assert decode_tail(72, 8, 32, parts=4) == (64 << 8) | 4
-    assert decode_tail(40, 8, 32, parts=3) == (32 << 8) | 3      # 320 = 256 + 64
-    assert decode_tail(64, 8, 32, parts=4) is None               # exact rounds
-    assert decode_tail(96, 8, 32, parts=4) is None               # 768: 3 per CU, balanced
-    assert decode_tail(90, 8, 32, parts=4) is None               # 720: > half a round over
-    assert decode_tail(16, 8, 32, parts=4) is None               # under one round
-    assert decode_tail(65, 8, 32, parts=1) is None               # disabled
-    assert decode_tail(65, 1, 64, parts=4) is None               # G > 16: no fused form

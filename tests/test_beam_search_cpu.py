@@ -149,3 +149,21 @@ def test_beam_search_via_openai_api(ckpt, tmp_path):
             assert bad.status_code == 400
     finally:
         aeng.shutdown()
+
+
+def test_beam_search_ignores_sampling_generation_defaults():
+    """A model whose generation_config sets min_p / repetition_penalty must still accept a
+    beam-search request that sets neither (they are sampling knobs); stop strings are
+    rejected up front (beams end on token ids only)."""
+    from enterprise_inference_amd.entrypoints.openai.protocol import CompletionRequest
+    gd = {"temperature": 0.6, "top_p": 0.9, "min_p": 0.05, "repetition_penalty": 1.1}
+    req = CompletionRequest(model="m", prompt=[1, 2], use_beam_search=True, best_of=2)
+    sp = req.to_sampling_params(16, None, gd)
+    assert sp.use_beam_search and sp.temperature == 0.0 and sp.min_p == 0.0
+    assert sp.repetition_penalty == 1.0 and sp.top_p == 1.0
+    with pytest.raises(ValueError, match="stop strings"):
+        CompletionRequest(model="m", prompt=[1], use_beam_search=True, best_of=2,
+                          stop=["\n"]).to_sampling_params(16, None, gd)
+    # without beam search the generation defaults still apply
+    sp2 = CompletionRequest(model="m", prompt=[1]).to_sampling_params(16, None, gd)
+    assert sp2.min_p == 0.05 and sp2.repetition_penalty == 1.1

@@ -19,14 +19,16 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 SMALL = ["--steps", "2", "--warmup", "1", "--users", "3", "--input-len", "8",
          "--output-len", "4", "--client-procs", "1", "--max-num-seqs", "8",
          "--max-num-batched-tokens", "64"]
+QUIET = ["--extras", "off", "--closed-loop-s", "0"]
 
 
-def _run(tmp_path, argv, launcher=()):
+def _run(tmp_path, argv, launcher=(), extra=QUIET):
+    argv = list(argv) + list(extra)
     env = dict(os.environ, EIA_FAKE_STEP_MS="2", EIA_BENCH_LOGDIR=str(tmp_path),
                PYTHONPATH=ROOT)
     env.pop("HIP_VISIBLE_DEVICES", None)
     r = subprocess.run([sys.executable, *launcher, os.path.join(ROOT, "bench.py"), *argv, *SMALL],
-                       cwd=ROOT, env=env, capture_output=True, text=True, timeout=400)
+                       cwd=ROOT, env=env, capture_output=True, text=True, timeout=600)
     assert r.returncode == 0, (r.stdout + r.stderr)[-4000:]
     lines = [json.loads(x) for x in r.stdout.splitlines() if x.startswith("{")]
     assert len(lines) == 1, r.stdout
@@ -82,3 +84,47 @@ def test_torchrun_form(tmp_path):
                          "--master-addr", "127.0.0.1", "--master-port", "29637"))
     assert out["n_gpus"] == 2
     assert out["config"]["parallelism"] == "dp2"
+
+
+def test_extra_configs_and_closed_loop(tmp_path):
+    """--gpus 2 (N >= 2): after the headline, config #3 (Llama-3.3-70B over both GPUs, 35
+    users) runs under its own key without touching `value`; the closed-loop window reports
+    steady-state tok/s and TTFT / TPOT percentiles beside the burst rounds."""
+    out = _run(tmp_path, ["--gpus", "2"],
+               extra=["--closed-loop-s", "2", "--closed-loop-warm-s", "0.5"])
+    assert out["config"]["model"] == "meta-llama/Llama-3.1-8B-Instruct"
+    assert out["config"]["parallelism"] == "dp2" and out["value"] > 0
+    ex = out["extra_configs"]
+    c3 = ex["config3_llama70b_tp2"]
+    assert "error" not in c3, c3
+    assert c3["model"] == "meta-llama/Llama-3.3-70B-Instruct"
+    assert c3["parallelism"] == "dp1xtp2" and c3["users_per_replica"] == 35
+    assert c3["value"] > 0 and c3["failed_requests"] == 0
+    assert "baseline_tok_s_per_replica" in c3     # 1120 (4x Gaudi 3) at 128/128
+    assert "config5_codeploy_8b_mistral7b" not in ex          # only at N = 8
+    cl = out["closed_loop"]
+    assert cl["tok_s"] > 0 and cl["requests"] > 0 and cl["failed_requests"] == 0
+    assert cl["ttft_p90_ms"] is not None and cl["tpot_p50_ms"] is not None
+
+
+def test_extra_config_errors_are_recorded(tmp_path, monkeypatch):
+    """A failing extra configuration (here: a server that cannot start) is reported as an
+    error string; the headline line still prints."""
+    sys.path.insert(0, ROOT)
+    import argparse
+
+    import bench
+    a = argparse.Namespace(startup_timeout=5, extra_budget_s=300, mode="endpoint", extras="on",
+                           model="x", tp=1, users=2, steps=1, warmup=1, co_deploy=False,
+                           co_model="y", client_procs=1, output_len=4, input_len=4,
+                           temperature=1.0, seed=0)
+
+    class Boom(bench.Replica):
+        def __init__(self, *args, **kw):
+            raise RuntimeError("server exited with code 1")
+    monkeypatch.setattr(bench, "Replica", Boom)
+    res = bench.run_extras(a, 2, str(tmp_path))
+    assert "server exited" in res["config3_llama70b_tp2"]["error"]
+    assert not bench.want_extras(argparse.Namespace(extras="auto", mode="endpoint"), 1)
+    assert bench.want_extras(argparse.Namespace(extras="auto", mode="endpoint"), 8)
+    assert not bench.want_extras(argparse.Namespace(extras="auto", mode="engine"), 8)

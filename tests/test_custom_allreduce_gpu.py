@@ -290,3 +290,86 @@ def test_error_flag_poller_on_device(tmp_path):
                        timeout=120)
     out = r.stdout + r.stderr
     assert r.returncode == 0 and "ERRFLAG_OK" in out, out[-3000:]
+
+
+SELFTEST = textwrap.dedent("""
+    import os, sys, threading, torch, torch.distributed as dist
+    sys.path.insert(0, os.environ["EIA_ROOT"])
+    from enterprise_inference_amd.parallel import custom_allreduce as cam
+    world = int(sys.argv[1])
+    corrupt = int(sys.argv[2])            # rank whose custom results are perturbed (-1: none)
+    ars = cam.CustomAllReduce.local_group(world, 8 << 20, nblocks=16)
+    if corrupt >= 0:                      # a wrong-but-not-hung reduction on one rank
+        bad = ars[corrupt]
+        orig = bad.all_reduce
+        def wrong(x, out=None, kind=None):
+            y = orig(x, out, kind)
+            y.view(-1)[:1] += 1.0
+            return y
+        bad.all_reduce = wrong
+    slots = [None] * world
+    bar = threading.Barrier(world)
+    def make_ref():
+        def ref(x):                       # in-process all-reduce (rank order, exact here)
+            r = threading.current_thread().rank
+            torch.cuda.current_stream().synchronize()
+            slots[r] = x
+            bar.wait()
+            s = torch.stack([t.float() for t in slots]).sum(0).to(x.dtype)
+            bar.wait()
+            return s
+        return ref
+    agreed = {}
+    def agree(t, op):                     # MIN / MAX over the threads
+        r = threading.current_thread().rank
+        slots[r] = t.clone()
+        bar.wait()
+        st = torch.stack(slots)
+        v = st.min(0).values if op == dist.ReduceOp.MIN else st.max(0).values
+        bar.wait()
+        return v
+    results = [None] * world
+    def body(r):
+        threading.current_thread().rank = r
+        s = torch.cuda.Stream()
+        with torch.cuda.stream(s):
+            results[r] = cam.init_custom_allreduce(8 << 20, factory=lambda mb: ars[r],
+                                                   reference=make_ref(), agree=agree, tune=True)
+        torch.cuda.synchronize()
+    ths = [threading.Thread(target=body, args=(r,)) for r in range(world)]
+    for t in ths: t.start()
+    for t in ths: t.join(timeout=240)
+    active = [res is not None for res in results]
+    print("ACTIVE", active, "STATUS", cam.STATUS.get("reason"),
+          cam.STATUS.get("oneshot_max"), cam.STATUS.get("use_max"), flush=True)
+    tun = cam.STATUS.get("tuning")
+    if tun:
+        print("TUNING", {k: tun[k] for k in ("sizes", "oneshot_us", "twoshot_us")}, flush=True)
+    if any(active):
+        assert all(active), "ranks disagree"
+        errs = [a.error_flag() for a in ars]      # (after a fallback the buffers are freed)
+        print("SPIN_ERR" if any(errs) else "NO_SPIN_ERR", flush=True)
+    else:
+        print("NO_SPIN_ERR", flush=True)
+""")
+
+
+@pytest.mark.parametrize("world,corrupt", [(2, -1), (4, -1), (4, 2)])
+def test_init_self_test_and_fallback(tmp_path, world, corrupt):
+    """init_custom_allreduce on W in-process ranks (one stream each): the self-test (one-shot,
+    two-shot, fused add+RMSNorm at three sizes, vs an exact in-process reference) passes and
+    the tuning pass runs on a healthy kernel; with one rank's reduction perturbed every rank
+    agrees to fall back (no rank keeps the custom kernel)."""
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    f = tmp_path / "selftest.py"
+    f.write_text(SELFTEST)
+    env = dict(os.environ, EIA_ROOT=root, GPU_MAX_HW_QUEUES=str(max(8, 2 * world)))
+    r = subprocess.run([sys.executable, str(f), str(world), str(corrupt)], env=env,
+                       capture_output=True, text=True, timeout=300)
+    out = r.stdout + r.stderr
+    assert r.returncode == 0, out[-3000:]
+    assert "NO_SPIN_ERR" in out, out[-3000:]
+    if corrupt < 0:
+        assert f"ACTIVE {[True] * world} STATUS ok" in out, out[-3000:]
+    else:
+        assert f"ACTIVE {[False] * world} STATUS self-test mismatch" in out, out[-3000:]

@@ -1,0 +1,141 @@
+"""Init-time checks of the custom xGMI all-reduce (parallel/custom_allreduce.py) on the CPU:
+the self-test against the reference reduction, the agreed fallback when ONE rank's reduction
+is wrong (every rank goes back to RCCL, none keeps the custom kernel), the exported status, and
+the timing -> threshold rule.  The custom kernel is replaced by a stand-in that reduces over
+gloo, so what is tested is the protocol around it."""
+
+import socket
+
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from enterprise_inference_amd.parallel import custom_allreduce as cam
+
+
+def _port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+class _GlooAR:
+    """CustomAllReduce stand-in: the same API, sums over gloo; ``wrong`` perturbs its result
+    the way a memory-ordering bug would (one element off, nothing hangs)."""
+
+    device = "cpu"
+
+    def __init__(self, rank, world, wrong=False, max_bytes=8 << 20):
+        self.rank, self.world, self.wrong = rank, world, wrong
+        self.max_bytes = self.use_max = max_bytes
+        self.oneshot_max = 512 * 1024
+        self.closed = False
+
+    def all_reduce(self, x, out=None, kind=None):
+        dist.all_reduce(x)
+        if self.wrong:
+            x.view(-1)[-1] += 1.0
+        return x
+
+    def add_rmsnorm(self, x, residual, weight, eps, twoshot=None):
+        from enterprise_inference_amd.ops import norm
+        s = self.all_reduce(x)
+        out, _ = norm.fused_add_rms_norm(s, residual, weight, eps)
+        return out
+
+    def error_flag(self):
+        return 0
+
+    def close(self):
+        self.closed = True
+
+
+def _worker(rank, world, port, bad_rank, q):
+    try:
+        dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank,
+                                world_size=world)
+        ar = _GlooAR(rank, world, wrong=(rank == bad_rank))
+
+        def reference(x):
+            dist.all_reduce(x)
+            return x
+
+        def agree(t, op):
+            dist.all_reduce(t, op=op)
+            return t
+
+        got = cam.init_custom_allreduce(8 << 20, factory=lambda mb: ar, reference=reference,
+                                        agree=agree, tune=False)
+        from enterprise_inference_amd.parallel import comm
+        q.put((rank, got is not None, ar.closed, cam.STATUS["reason"],
+               comm.get_custom_allreduce() is not None))
+        comm.set_custom_allreduce(None)
+    except Exception as e:   # noqa: BLE001
+        q.put((rank, repr(e), None, None, None))
+    finally:
+        if dist.is_initialized():
+            dist.destroy_process_group()
+
+
+def _run(world, bad_rank):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _port()
+    ps = [ctx.Process(target=_worker, args=(r, world, port, bad_rank, q)) for r in range(world)]
+    for p in ps:
+        p.start()
+    res = sorted(q.get(timeout=120) for _ in ps)
+    for p in ps:
+        p.join(timeout=60)
+    return res
+
+
+@pytest.mark.parametrize("world,bad", [(2, -1), (2, 1), (4, 0)])
+def test_self_test_agreed_fallback(world, bad):
+    res = _run(world, bad)
+    for rank, active, closed, reason, registered in res:
+        assert not isinstance(active, str), active
+        if bad < 0:
+            assert active and registered and not closed and reason == "ok", res
+        else:
+            # the wrong rank AND its healthy peers all fall back together
+            assert not active and not registered and closed, res
+            assert reason == "self-test mismatch", res
+
+
+def test_self_test_cases_are_exact_and_cover_both_forms():
+    cases = cam.selftest_cases(16 << 20, 512 << 10)
+    kinds = {(op, kind) for op, _, kind in cases}
+    assert kinds == {("ar", 0), ("ar", 1), ("norm", 0), ("norm", 1)}
+    assert len({shape for op, shape, _ in cases if op == "ar"}) == 3
+    # integer inputs: the sum over 8 ranks is exact in bf16
+    for case in cases[:2]:
+        xs = [cam.selftest_inputs(case, r, "cpu")[0] for r in range(8)]
+        s32 = torch.stack([x.float() for x in xs]).sum(0)
+        assert torch.equal(s32.to(torch.bfloat16).float(), s32)
+    # shapes beyond the buffer are not tested
+    small = cam.selftest_cases(64 << 10, 32 << 10)
+    assert all(2 * (s[0] if op == "ar" else s[0] * s[1]) <= 64 << 10 for op, s, _ in small)
+
+
+def test_tune_thresholds_rule():
+    sizes = [32 << 10, 128 << 10, 512 << 10, 1 << 20, 2 << 20, 4 << 20]
+    one = [10, 12, 20, 35, 70, 140]
+    two = [14, 15, 18, 25, 40, 75]
+    rccl = [30, 30, 32, 34, 45, 70]
+    o, u = cam.tune_thresholds(sizes, one, two, rccl, 16 << 20)
+    assert o == 128 << 10          # one-shot loses to two-shot from 512 KiB on
+    assert u == 2 << 20            # RCCL wins at 4 MiB
+    o, u = cam.tune_thresholds(sizes, one, two, [1] * 6, 16 << 20)
+    assert u == 0                  # RCCL always faster: nothing routed to the custom kernel
+
+
+def test_status_gauge_rendered():
+    from enterprise_inference_amd.metrics import EngineMetrics
+    m = EngineMetrics("tiny")
+    m.set_custom_allreduce({"active": False, "reason": "self-test mismatch"})
+    text = m.render().decode()
+    assert 'eia:custom_allreduce_active{model_name="tiny",reason="self-test mismatch"} 0.0' in text

@@ -480,53 +480,6 @@ def test_decode_rope_fused_matches_two_kernels(Hq, Hkv, D, bs, bias, qkn, split,
     assert int(cnt.abs().sum()) == 0
 
 
-@pytest.mark.parametrize("B,Pg", [(65, 4), (72, 4), (40, 3), (65, 2)])
-def test_decode_rope_tail_split(B, Pg):
-    """Tail split (rows >= row of a P-1 step split over partitions, merged in-kernel, remapped
-    dispatch order) == the unsplit fused kernel up to the merge's rounding; same K/V cache
-    writes; arrival counters left zeroed (graph replay)."""
-    from enterprise_inference_amd.ops import attention, rotary
-    from enterprise_inference_amd.ops.gemm import SplitK
-    Hq, Hkv, D, bs = 32, 8, 128, 128
-    torch.manual_seed(B + Pg)
-    lens = [random.Random(i * 7 + B).randint(1, 700) for i in range(B)]
-    lens[3] = 0                                                   # graph padding rows
-    lens[-1] = 0
-    lens[-2], lens[-3] = 1, 64
-    nbt = sum(math.ceil(max(l, 1) / bs) for l in lens) + 2
-    k1, v1 = _make_cache(nbt, Hkv, bs, D, fill=True)
-    bt = _random_tables([max(l, 1) for l in lens], bs, nbt).to(DEV)
-    sl = torch.tensor(lens, dtype=torch.int32, device=DEV)
-    pos = torch.tensor([max(l - 1, 0) for l in lens], dtype=torch.int32, device=DEV)
-    slots = torch.tensor([int(bt[i, (l - 1) // bs]) * bs + (l - 1) % bs if l > 0 else -1
-                          for i, l in enumerate(lens)], dtype=torch.int32, device=DEV)
-    N = (Hq + 2 * Hkv) * D
-    qkv = SplitK(torch.randn(4, B, N, device=DEV) * 0.5, 4, B, N, None)
-    rc = rotary.RotaryCache(D, 4096, 500000.0, None, DEV)
-    k2, v2 = k1.clone(), v1.clone()
-    tv = attention.decode_tail(B, Hkv, Hq, parts=Pg)
-    assert tv is not None and (tv >> 8) < B
-    po = torch.empty(B * Hq * Pg * D, device=DEV)
-    pml = torch.empty(B * Hq * Pg * 2, device=DEV)
-    cnt = torch.zeros(B * Hkv, dtype=torch.int32, device=DEV)
-    one = torch.ones(1, dtype=torch.int32, device=DEV)
-    md = attention.AttentionMetadata(num_decode=B, num_prefill_tokens=0, slot_mapping=slots,
-                                     positions=pos, decode_block_tables=bt, decode_seq_lens=sl)
-    o2 = attention.decode_rope_attention(qkv, md, k2, v2, rc, Hq, Hkv, D, D ** -0.5)
-    md.decode_partitions, md.decode_part_o, md.decode_part_ml = Pg, po, pml
-    md.decode_part_cnt, md.decode_p_dyn = cnt, one
-    md.decode_tail = torch.tensor([tv], dtype=torch.int32, device=DEV)
-    for _ in range(2):                                            # replay: counters reset
-        o1 = attention.decode_rope_attention(qkv, md, k1, v1, rc, Hq, Hkv, D, D ** -0.5)
-    torch.cuda.synchronize()
-    assert torch.equal(k1, k2) and torch.equal(v1, v2), "K/V cache writes differ"
-    live = sl > 0
-    row = tv >> 8
-    assert torch.equal(o1[:row][live[:row]], o2[:row][live[:row]]), "unsplit rows must match"
-    _close(o1[live], o2[live], 2e-2, 2e-2, f"tail split B={B} P={Pg}")
-    assert int(cnt.abs().sum()) == 0
-
-
 @pytest.mark.parametrize("sw,ch", [(None, None), (50, None), (None, 64), (200, None)])
 def test_paged_prefill_fa_long_and_windowed(sw, ch):
     """Flash form (v_mfma_f32_32x32x16) on multi-tile prompts with cached context, ragged
@@ -551,34 +504,3 @@ def test_paged_prefill_fa_long_and_windowed(sw, ch):
     _close(o, r, 2e-2, 2e-2, f"prefill fa sw={sw} chunk={ch}")
 
 
-# ----------------------------------------------------------------------------- MALL prefetch
-
-def test_mall_prefetch_fork_join_in_graph():
-    """The Infinity Cache sweep (csrc/kernels/prefetch.hip) on a side-stream branch of a HIP
-    graph: forked after a producer, joined before a consumer, results unchanged; odd sizes
-    (not a multiple of the unrolled stride) and a byte prefix are covered."""
-    from enterprise_inference_amd.ops import prefetch
-    w = torch.randn(4099, 1024, device=DEV, dtype=BF)
-    x = torch.randn(8, 1024, device=DEV, dtype=BF)
-    expect = x.float() @ w.float().t()
-
-    def body():
-        y = x * 1.0                                  # producer on the main stream
-        join = prefetch.fork([(w, None), (w, 12345 * 16)])
-        y = y + 0.0
-        join()
-        return y.float() @ w.float().t()             # consumer after the join
-    body()
-    torch.cuda.synchronize()
-    g = torch.cuda.CUDAGraph()
-    s = torch.cuda.Stream()
-    s.wait_stream(torch.cuda.current_stream())
-    with torch.cuda.stream(s):
-        body()
-        with torch.cuda.graph(g, stream=s):
-            out = body()
-    torch.cuda.current_stream().wait_stream(s)
-    for _ in range(3):
-        g.replay()
-    torch.cuda.synchronize()
-    _close(out, expect, 1e-2, 1e-3, "prefetch fork/join")

@@ -224,6 +224,58 @@ def test_remote_image_policy(monkeypatch):
         stop()
 
 
+def test_remote_image_dns_rebinding_pinned(monkeypatch):
+    """A resolver that answers a public address for the policy check and the metadata
+    address afterwards must not steer the fetch: the request dials the address the check
+    validated (Host header and SNI keep the name), and the name is resolved once."""
+    import contextlib
+    import socket
+
+    from enterprise_inference_amd.models import llama4_vision as lv
+    answers = iter(["93.184.216.34", "169.254.169.254", "169.254.169.254"])
+    lookups = []
+
+    def fake_getaddrinfo(host, port, *a, **k):
+        lookups.append(host)
+        return [(socket.AF_INET, socket.SOCK_STREAM, 6, "", (next(answers), port))]
+
+    seen = {}
+
+    class _Resp:
+        is_redirect = False
+        headers = {"content-length": "3"}
+        extensions = {}
+
+        def raise_for_status(self):
+            pass
+
+        def iter_bytes(self):
+            yield b"abc"
+
+    @contextlib.contextmanager
+    def fake_stream(url, headers, extensions, timeout):
+        seen.update(url=url, headers=headers, ext=extensions)
+        yield _Resp()
+
+    monkeypatch.setattr(socket, "getaddrinfo", fake_getaddrinfo)
+    monkeypatch.setattr(lv, "_open_stream", fake_stream)
+    assert lv.fetch_image_bytes("https://img.example.com:8443/a.png") == b"abc"
+    assert lookups == ["img.example.com"]
+    assert seen["url"] == "https://93.184.216.34:8443/a.png"
+    assert seen["headers"] == {"Host": "img.example.com:8443"}
+    assert seen["ext"] == {"sni_hostname": "img.example.com"}
+
+    # a peer address other than the validated one is refused before the body is read
+    class _Stream:
+        def get_extra_info(self, k):
+            return ("10.0.0.5", 443) if k == "server_addr" else None
+
+    _Resp.extensions = {"network_stream": _Stream()}
+    answers = iter(["93.184.216.34"])
+    with pytest.raises(ValueError, match="unexpected address"):
+        lv.fetch_image_bytes("https://img.example.com/a.png")
+
+
 def test_slow_image_url_does_not_block_event_loop(monkeypatch):
     """The image download runs on a worker thread: while one request waits 1.5 s on a slow
     image URL, the event loop keeps serving other coroutines."""
