@@ -144,3 +144,71 @@ def test_root_path_middleware():
     assert c.get("/Llama-3.1-8B-Instruct/v1/models",
                  headers={"Authorization": "Bearer k"}).json() == {"ok": True}
     assert c.get("/health").status_code == 200
+
+
+# ----------------------------------------------------------------------------- logs stack
+
+def _deep_merge(a, b):
+    out = dict(a)
+    for k, v in b.items():
+        out[k] = _deep_merge(out[k], v) if isinstance(v, dict) and isinstance(out.get(k), dict) \
+            else v
+    return out
+
+
+@pytest.mark.parametrize("overlay", [None, "aws-s3-values.yaml"])
+def test_logs_stack_values(overlay):
+    """Loki SimpleScalable on an object store (MinIO by default, AWS S3 with the overlay), 7-day
+    retention enforced by the compactor, OTLP resource attributes as index labels, the
+    collector's PodMonitor and the tenant header on both the write and the read side."""
+    import yaml
+    base = os.path.join(CHARTS, "observability", "logs-stack")
+    v = yaml.safe_load(open(os.path.join(base, "values.yaml")))
+    if overlay:
+        v = _deep_merge(v, yaml.safe_load(open(os.path.join(base, overlay))))
+    loki = v["loki"]
+    assert loki["deploymentMode"] == "SimpleScalable" and loki["fullnameOverride"] == "loki"
+    assert loki["write"]["replicas"] == loki["loki"]["commonConfig"]["replication_factor"]
+    assert loki["minio"]["enabled"] is (overlay is None)
+    cfg = loki["loki"]
+    assert cfg["schemaConfig"]["configs"][0]["object_store"] == "s3"
+    assert cfg["compactor"]["retention_enabled"] and cfg["compactor"]["delete_request_store"] == "s3"
+    assert cfg["limits_config"]["retention_period"] == "168h"
+    labels = cfg["distributor"]["otlp_config"]["default_resource_attributes_as_index_labels"]
+    assert {"k8s.namespace.name", "k8s.pod.name", "service.name"} <= set(labels)
+    if overlay:
+        aws = cfg["storage_config"]["aws"]
+        assert {"region", "bucketnames", "access_key_id", "secret_access_key"} <= set(aws)
+    otel = v["otelcol-logs"]
+    assert otel["mode"] == "daemonset" and otel["podMonitor"]["enabled"]
+    assert otel["podMonitor"]["extraLabels"]["release"] == "observability"
+    hdr = otel["config"]["extensions"]["headers_setter/tenant"]["headers"][0]
+    assert hdr["key"] == "X-Scope-OrgID" and hdr["value"] == v["tenant"]
+    exp = otel["config"]["exporters"]["otlphttp/loki"]
+    assert exp["endpoint"].startswith("http://loki-write.") and exp["endpoint"].endswith("/otlp")
+    assert exp["auth"]["authenticator"] == "headers_setter/tenant"
+    docs = helm_lite.render_chart(base, [os.path.join(base, overlay)] if overlay else [], {},
+                                  release="logs-stack", namespace="observability")
+    ds = [d for d in docs if d["kind"] == "ConfigMap"][0]
+    body = yaml.safe_load(ds["data"]["loki.yaml"])["datasources"][0]
+    assert body["url"] == "http://loki-read.observability:3100"
+    assert body["jsonData"]["httpHeaderName1"] == "X-Scope-OrgID"
+    assert body["secureJsonData"]["httpHeaderValue1"] == v["tenant"]
+
+
+def test_observability_plays_apply_s3_overlay():
+    """Both observability plays layer aws-s3-values.yaml (+ bucket / region / credentials)
+    exactly when aws_access_key is set, and MinIO otherwise."""
+    import yaml
+    for play in ("deploy-observability.yml", "deploy-observability-openshift.yml"):
+        doc = yaml.safe_load(open(os.path.join(ROOT, "core", "playbooks", play)))[0]
+        vs = doc["vars"]
+        assert "aws_access_key" in vs["logs_s3"]
+        assert "aws-s3-values.yaml" in vs["logs_values_files"] and "if logs_s3" in \
+            vs["logs_values_files"]
+        aws = vs["logs_s3_values"]["loki"]["loki"]["storage_config"]["aws"]
+        assert "aws_secret_key" in aws["secret_access_key"] and "aws_bucket" in aws["bucketnames"]
+        task = [t for t in doc["tasks"] if t.get("name") == "Logs stack (Loki + OTEL collector)"][0]
+        h = task["kubernetes.core.helm"]
+        assert h["values_files"] == "{{ logs_values_files }}"
+        assert "logs_s3_values" in str(h["values"])
