@@ -360,6 +360,13 @@ class Replica:
         return json.loads(_http("GET", self.base + "/eia/stats")[1])
 
     def summary(self, elapsed: float, stats0: dict, stats1: dict) -> dict:
+        if self.args.verbose:
+            nst = max(1, stats1["num_steps"] - stats0["num_steps"])
+            for key in ("phase_times", "loop_times"):
+                a, b = stats0.get(key) or {}, stats1.get(key) or {}
+                print(f"[replica {self.idx}] {key} ms/step: " + json.dumps(
+                    {k: round(1e3 * (b[k] - a.get(k, 0.0)) / nst, 3) for k in b}),
+                    file=sys.stderr)
         tot, ttft, tpot, e2e, failed = 0, [], [], [], []
         for res in self.res:
             for ok, tt, ee, n, err in res:

@@ -20,6 +20,16 @@ struct QkvSrc {
   float eps;
 };
 
+// NEOX rotation of one (x1, x2) pair with explicit FMAs: every kernel that rotates (the K4
+// rope kernel, the fused and the stream-K decode prologues) produces the same bits whatever
+// the compiler's contraction choices around it.
+EIA_DEV void rope_rotate(float& x1, float& x2, float c, float s) {
+  const float r1 = __fmaf_rn(x1, c, -(x2 * s));
+  const float r2 = __fmaf_rn(x2, c, x1 * s);
+  x1 = r1;
+  x2 = r2;
+}
+
 template <int D, bool NEOX>
 EIA_DEV void rope_lane_offsets(int sub, int& e0, int& e1) {
   if (NEOX) { e0 = sub * 8; e1 = D / 2 + sub * 8; }
@@ -159,11 +169,7 @@ struct RopeLane {
     if (!active || h >= nrot || cos_sin == nullptr) return;
     if (NEOX) {
 #pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const float x1 = a[j], x2 = b[j];
-        a[j] = x1 * c[j] - x2 * s[j];
-        b[j] = x2 * c[j] + x1 * s[j];
-      }
+      for (int j = 0; j < 8; ++j) rope_rotate(a[j], b[j], c[j], s[j]);
     } else {
       float ra[8], rb[8];
 #pragma unroll

@@ -131,7 +131,8 @@ def _run_op(engine, op: str):
         return {"num_steps": st.num_steps, "num_generation_tokens": st.num_generation_tokens,
                 "num_prompt_tokens": st.num_prompt_tokens, "num_blocks": engine.num_blocks,
                 "step_time_s": st.step_time_s,
-                "phase_times": dict(engine.phase_times)}
+                "phase_times": dict(engine.phase_times),
+                "loop_times": dict(getattr(engine, "loop_times", {}))}
     raise ValueError(f"unknown engine op {op!r}")
 
 
@@ -207,10 +208,18 @@ def core_main(fd: int) -> int:
     delay = float(fault.split(":")[1]) if fault.startswith("delay_step:") else None
     steps = 0
     rc = 0
+    # host seconds per loop phase (engine.step() has its own breakdown in phase_times): what the
+    # core spends outside the step -- request intake and the per-step output frame
+    lt = engine.loop_times = {"intake": 0.0, "step": 0.0, "frame": 0.0, "send": 0.0}
+    perf = time.perf_counter
     try:
         while True:
             busy = engine.has_unfinished_requests()
-            for msg in intake(reader, busy):
+            ti = perf()
+            msgs = intake(reader, busy)
+            if busy:
+                lt["intake"] += perf() - ti
+            for msg in msgs:
                 k = msg[0]
                 if k == "add":
                     _, rid, prompt, params, ids, arrival, prio = msg[:7]
@@ -236,14 +245,22 @@ def core_main(fd: int) -> int:
             if not engine.has_unfinished_requests():
                 continue
             t0 = time.time()
+            t1 = perf()
             if delay:
                 time.sleep(delay)
             outs = engine.step()
+            t2 = perf()
             steps += 1
             if crash_after is not None and steps >= crash_after:
                 raise RuntimeError("EIA_FAULT_INJECT crash")
             snap = EngineMetrics.engine_snapshot(engine, time.time() - t0)
-            sock.sendall(encode_frame(("out", snap, [_pack(o) for o in outs])))
+            frame = encode_frame(("out", snap, [_pack(o) for o in outs]))
+            t3 = perf()
+            sock.sendall(frame)
+            t4 = perf()
+            lt["step"] += t2 - t1
+            lt["frame"] += t3 - t2
+            lt["send"] += t4 - t3
     except (EOFError, ConnectionError):
         logger.info("API process went away; engine core exiting")
     except SystemExit:
