@@ -28,7 +28,10 @@
 // Measured variants (profiles/prefill_attn_fa_r2.log): 4-wave workgroups (two per CU), other
 // MFMA / exp orders: all within 3 %; a software pipeline holding two tiles' S (QK(i+1) beside
 // the exp work of tile i) and two 32-query sub-blocks per wave (one wave per SIMD) both exceed
-// the register file and spill.
+// the register file and spill.  Round 4 (profiles/prefill_attn_fa_r4.md): raw v_exp_f32, a
+// branch-free mask, tree max / sum chains, static young-half priority and dwordx4 output stores
+// (65x128: 135 -> 174 TFLOP/s); fetching K/V two tiles ahead (+24 VGPRs) was slower at 1x8192
+// (800 vs 757 us) -- the one-tile-ahead fetch is not the bound there.
 #include "eia_common.h"
 
 namespace {
@@ -159,20 +162,27 @@ paged_prefill_fa_kernel(const bf16_t* __restrict__ q, long q_stride, bf16_t* __r
     // element i of half sh is key kb + 32 sh + 16 (i >> 3) + 8 h + (i & 7)
     const bool whole = !window && kb + FKB <= L && (!causal || kb + FKB - 1 <= ctx + wq0);
     if (!whole) {
+      // key kp is visible iff q_lo <= kp <= kmax: one unsigned compare per score, no branches
+      const int kmax = causal ? min(L - 1, qa) : L - 1;
+      const unsigned lim = (unsigned)(kmax - q_lo);
+      const int d0 = kb + 8 * h - q_lo;
 #pragma unroll
       for (int sh = 0; sh < 2; ++sh)
 #pragma unroll
         for (int i = 0; i < 16; ++i) {
-          const int kp = kb + 32 * sh + 16 * (i >> 3) + 8 * h + (i & 7);
-          const bool ok = kp < L && (!causal || kp <= qa) && kp >= q_lo;
-          if (!ok) sacc[sh][i] = (-INFINITY);
+          const unsigned dk = (unsigned)(d0 + 32 * sh + 16 * (i >> 3) + (i & 7));
+          sacc[sh][i] = dk <= lim ? sacc[sh][i] : (-INFINITY);
         }
     }
-    float mx = sacc[0][0];
+    // four independent max3 chains instead of one 16-deep dependent chain
+    float mx4[4];
 #pragma unroll
-    for (int sh = 0; sh < 2; ++sh)
+    for (int c = 0; c < 4; ++c) {
+      mx4[c] = sacc[c >> 1][8 * (c & 1)];
 #pragma unroll
-      for (int i = 0; i < 16; ++i) mx = fmaxf(mx, sacc[sh][i]);
+      for (int j = 1; j < 8; ++j) mx4[c] = fmaxf(mx4[c], sacc[c >> 1][8 * (c & 1) + j]);
+    }
+    const float mx = fmaxf(fmaxf(mx4[0], mx4[1]), fmaxf(mx4[2], mx4[3]));
     const float mt = pair_max(mx) * scale_log2;
     const bool grow = mt > m_run + DEFER_LOG2;
     if (__any(grow)) {                                     // wave-uniform
@@ -184,17 +194,19 @@ paged_prefill_fa_kernel(const bf16_t* __restrict__ q, long q_stride, bf16_t* __r
       for (int dt = 0; dt < FD / 32; ++dt) oacc[dt] *= alpha;
     }
     const float muse = m_run == (-INFINITY) ? 0.f : m_run;
+    // raw v_exp_f32 (exp2f adds a denormal-range fix-up of 3 VALU per score); row sum as four
+    // independent chains
     bf16x8 pb[4];
-    float psum = 0.f;
+    float ps4[4] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int ks = 0; ks < 4; ++ks)
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
-        const float p = exp2f(fmaf(sacc[ks >> 1][8 * (ks & 1) + j], scale_log2, -muse));
+        const float p = __builtin_amdgcn_exp2f(fmaf(sacc[ks >> 1][8 * (ks & 1) + j], scale_log2, -muse));
         pb[ks][j] = f2bf(p);
-        psum += p;
+        ps4[ks] += p;
       }
-    l_run += psum;
+    l_run += (ps4[0] + ps4[1]) + (ps4[2] + ps4[3]);
 #pragma unroll
     for (int dt = 0; dt < FD / 32; ++dt)
 #pragma unroll
@@ -204,6 +216,10 @@ paged_prefill_fa_kernel(const bf16_t* __restrict__ q, long q_stride, bf16_t* __r
       }
   };
 
+  // static priority for the younger half (waves 4-7): it otherwise loses VALU arbitration to
+  // the older half at the start of every segment (guide T5, static form); readfirstlane makes
+  // the condition provably wave-uniform so only those waves execute the s_setprio
+  if (__builtin_amdgcn_readfirstlane(tid) >= FTHREADS / 2) __builtin_amdgcn_s_setprio(1);
   bf16x8 st[4];
   if (ntile > 0) {
     fetch(lo, st);
@@ -223,16 +239,28 @@ paged_prefill_fa_kernel(const bf16_t* __restrict__ q, long q_stride, bf16_t* __r
   const float lt = pair_sum(l_run);
   if (!qvalid) return;
   const float inv = lt > 0.f ? 1.f / lt : 0.f;
-  bf16_t* op = out + tok * out_stride + (long)hq * FD + 4 * h;
+  // Lane (q, h) holds d = 32 dt + 8 j + 4 h + [0, 4): the two lane halves of a query own
+  // alternating 8-B pieces.  One permlane32_swap per dword pairs pieces j / j+1 so each lane
+  // stores 16 contiguous bytes (guide T21): 8 dwordx4 stores per lane instead of 16 dwordx2.
+  // Both lanes of a swap pair hold the same query, so they are valid (or exited) together.
+  bf16_t* op = out + tok * out_stride + (long)hq * FD + 8 * h;
 #pragma unroll
-  for (int dt = 0; dt < FD / 32; ++dt)
+  for (int dt = 0; dt < FD / 32; ++dt) {
+    uint2 pk[4];
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       bf16x4 o4;
 #pragma unroll
       for (int r = 0; r < 4; ++r) o4[r] = f2bf(oacc[dt][4 * j + r] * inv);
-      *reinterpret_cast<bf16x4*>(op + 32 * dt + 8 * j) = o4;
+      pk[j] = __builtin_bit_cast(uint2, o4);
     }
+#pragma unroll
+    for (int j = 0; j < 4; j += 2) {
+      const auto rx = __builtin_amdgcn_permlane32_swap(pk[j].x, pk[j + 1].x, false, false);
+      const auto ry = __builtin_amdgcn_permlane32_swap(pk[j].y, pk[j + 1].y, false, false);
+      *reinterpret_cast<uint4*>(op + 32 * dt + 8 * j) = make_uint4(rx[0], ry[0], rx[1], ry[1]);
+    }
+  }
 }
 
 }  // namespace
@@ -246,7 +274,8 @@ EIA_API int eia_paged_prefill_fa(const void* q, long q_stride, void* out, long o
                                  int Hkv, int D, int bs, int causal, int sliding_window,
                                  int chunk_size, hipStream_t st) {
   if (Hkv <= 0 || Hq % Hkv != 0) return EIA_BAD_SHAPE;
-  if (D != FD || (Hq / Hkv) % 4 != 0 || bs % FKB != 0) return EIA_UNSUPPORTED;
+  if (D != FD || (Hq / Hkv) % 4 != 0 || bs % FKB != 0 || out_stride % 8 != 0)
+    return EIA_UNSUPPORTED;                                 // (16-B output stores)
   if (n_work == 0) return EIA_OK;
   static bool attr = false;   // > 64 KiB of dynamic LDS must be opted into
   if (!attr) {

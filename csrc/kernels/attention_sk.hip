@@ -518,16 +518,32 @@ paged_decode_sk_kernel(SkArgs a) {
     const int slot_a = (TU * ga / G != xf) ? 1 : 0;
     for (int idx = tid; idx < GQ * D; idx += 512) {
       const int cq = idx / D, d = idx % D;
-      float M = -INFINITY;
-      for (int gg = ga; gg <= gb; ++gg)
-        M = fmaxf(M, ld(a.part_ml + 2 * (((long)gg * 2 + (gg == ga ? slot_a : 0)) * GQ + cq)));
-      float Ls = 0.f, O = 0.f;
-      if (M != -INFINITY) {
-        for (int gg = ga; gg <= gb; ++gg) {
+      // pieces in groups of 4 with every load of a group issued before the first use (one
+      // round trip per group, clamped indices; an item rarely spans more than 4 workgroups),
+      // combined with an online max in workgroup order
+      float M = -INFINITY, Ls = 0.f, O = 0.f;
+      for (int g0 = ga; g0 <= gb; g0 += 4) {
+        float pm[4], pl[4], po[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int gg = min(g0 + j, gb);
           const long pi = ((long)gg * 2 + (gg == ga ? slot_a : 0)) * GQ + cq;
-          const float f = exp2f(ld(a.part_ml + 2 * pi) - M);
-          Ls += ld(a.part_ml + 2 * pi + 1) * f;
-          O += ld(a.part_o + pi * D + d) * f;
+          pm[j] = ld(a.part_ml + 2 * pi);
+          pl[j] = ld(a.part_ml + 2 * pi + 1);
+          po[j] = ld(a.part_o + pi * D + d);
+        }
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          if (g0 + j > gb || pm[j] == -INFINITY) continue;
+          if (pm[j] > M) {
+            const float f = exp2f(M - pm[j]);
+            Ls *= f;
+            O *= f;
+            M = pm[j];
+          }
+          const float f = exp2f(pm[j] - M);
+          Ls += pl[j] * f;
+          O += po[j] * f;
         }
       }
       const int b = item / a.Hkv, hq = (item % a.Hkv) * GQ + cq;

@@ -67,6 +67,7 @@ _SIGNATURES = {
     "eia_gemm_skinny": [P, L, P, L, P, P, L, I, I, I, I, I, I, S],
     "eia_splitk_reduce": [P, I, I, I, P, P, L, S],
     "eia_splitk_add_rmsnorm": [P, I, I, I, P, P, F, P, L, S],
+    "eia_splitk_add_rmsnorm_wide": [P, I, I, I, P, P, F, P, L, P, P, S],
     "eia_ar_alloc": [P, L],
     "eia_ar_free": [P],
     "eia_ar_signal_bytes": [],

@@ -130,7 +130,7 @@ def decode_partitions(batch: int, num_kv_heads: int, num_heads: int, max_len: in
 
 # Stream-K short-context decode (csrc/kernels/attention_sk.hip): 2 workgroups per CU, each
 # taking at most SK_UNITS 32-token (item, unit) pairs of the step, one per wave.
-SK_ENABLED = os.environ.get("EIA_DECODE_SK", "1") != "0"
+SK_ENABLED = os.environ.get("EIA_DECODE_SK", "0") != "0"
 SK_UNITS = 8
 
 

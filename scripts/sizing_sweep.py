@@ -75,7 +75,9 @@ def main() -> int:
                "--users", str(users), "--input-len", str(inp), "--output-len", str(outp),
                "--steps", str(args.steps), "--warmup", str(args.warmup),
                "--max-num-seqs", str(max(256, users)),
-               "--max-num-batched-tokens", str(max(8192, inp))]
+               "--max-num-batched-tokens", str(max(8192, inp)),
+               # burst rounds only: a closed-loop window would wait out whole long-output requests
+               "--closed-loop-s", "0"]
         if args.tp > 1:
             cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
                    f"--nproc-per-node={args.tp}", "--master-addr", "127.0.0.1",
