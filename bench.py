@@ -95,7 +95,7 @@ def parse():
                          "TP=N, 35 users) and at N=8 config #5 (8B + Mistral-7B co-deploy); "
                          "auto = endpoint mode with N >= 2.  Reported under extra keys, "
                          "`value` is the headline only")
-    ap.add_argument("--extra-budget-s", type=float, default=1500.0,
+    ap.add_argument("--extra-budget-s", type=float, default=900.0,
                     help="wall-clock budget for all extra configurations together")
     return ap.parse_args()
 
@@ -584,7 +584,8 @@ def _extra(a, slots, n_gpus: int, deadline: float, logdir: str) -> dict:
             return {"error": "skipped: extra budget exhausted"}
         a.startup_timeout = min(a.startup_timeout, left)
         for i, (g, m) in enumerate(slots):
-            reps.append(Replica(a, i, g, m, logdir, tag="_extra", request_timeout=max(60, left)))
+            reps.append(Replica(a, i, g, m, logdir, tag="_extra",
+                                request_timeout=min(300, max(60, left))))
         _parallel([r.wait for r in reps])
         _parallel([(lambda r=r: r.rounds(a.warmup, False)) for r in reps])
         stats0 = [r.stats() for r in reps]

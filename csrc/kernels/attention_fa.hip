@@ -32,6 +32,8 @@
 // branch-free mask, tree max / sum chains, static young-half priority and dwordx4 output stores
 // (65x128: 135 -> 174 TFLOP/s); fetching K/V two tiles ahead (+24 VGPRs) was slower at 1x8192
 // (800 vs 757 us) -- the one-tile-ahead fetch is not the bound there.
+#include <cstdlib>
+
 #include "eia_common.h"
 
 namespace {
@@ -46,7 +48,8 @@ constexpr int KS = FD + 8;           // K row stride (elements)
 constexpr int VS = FKB + 8;          // V^T row stride (elements)
 constexpr int KBUF = FKB * KS, BUF = KBUF + FD * VS;
 constexpr int FA_LDS_BYTES = 2 * BUF * 2;
-constexpr float DEFER_LOG2 = 8.f;    // rescale only when the max grows by > 2^8
+constexpr float DEFER_LOG2 = 8.f;
+    // rescale only when the max grows by > 2^8
 
 EIA_DEV int perm_row(int R) { return (R & ~12) | ((R & 4) << 1) | ((R & 8) >> 1); }
 EIA_DEV float pair_max(float v) {    // max with lane l ^ 32
@@ -58,6 +61,9 @@ EIA_DEV float pair_sum(float v) {
   return __uint_as_float(r[0]) + __uint_as_float(r[1]);
 }
 
+// IL (A/B of the P.V order, EIA_FA_IL): 0 = all exponentials then P.V, 1 = P.V of key half a
+// beside the exponentials of half b, 2 = 1 with a pinned MFMA / V^T read / VALU interleave
+template <int IL>
 __global__ void __launch_bounds__(FTHREADS, 1)
 paged_prefill_fa_kernel(const bf16_t* __restrict__ q, long q_stride, bf16_t* __restrict__ out,
                         long out_stride, const bf16_t* __restrict__ kc,
@@ -194,26 +200,53 @@ paged_prefill_fa_kernel(const bf16_t* __restrict__ q, long q_stride, bf16_t* __r
       for (int dt = 0; dt < FD / 32; ++dt) oacc[dt] *= alpha;
     }
     const float muse = m_run == (-INFINITY) ? 0.f : m_run;
-    // raw v_exp_f32 (exp2f adds a denormal-range fix-up of 3 VALU per score); row sum as four
-    // independent chains
+    // raw v_exp_f32 (exp2f adds a denormal-range fix-up of 3 VALU per score); row sums as four
+    // independent chains.  P^T of key half a (k-steps 0, 1) first; the P.V MFMAs of half a then
+    // run beside the exponentials of half b (independent work the scheduler is told to
+    // interleave: one MFMA, its V^T read and five VALU per gap), and half b's P.V last.
     bf16x8 pb[4];
     float ps4[4] = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-    for (int ks = 0; ks < 4; ++ks)
+    auto expk = [&](int ks) {
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
         const float p = __builtin_amdgcn_exp2f(fmaf(sacc[ks >> 1][8 * (ks & 1) + j], scale_log2, -muse));
         pb[ks][j] = f2bf(p);
         ps4[ks] += p;
       }
-    l_run += (ps4[0] + ps4[1]) + (ps4[2] + ps4[3]);
+    };
+    auto pv = [&](int ks0) {
 #pragma unroll
-    for (int dt = 0; dt < FD / 32; ++dt)
+      for (int dt = 0; dt < FD / 32; ++dt)
 #pragma unroll
-      for (int ks = 0; ks < 4; ++ks) {
-        const bf16x8 vf = *reinterpret_cast<const bf16x8*>(vf0 + 32 * VS * dt + 16 * ks);
-        oacc[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf, pb[ks], oacc[dt], 0, 0, 0);
+        for (int ks = ks0; ks < ks0 + 2; ++ks) {
+          const bf16x8 vf = *reinterpret_cast<const bf16x8*>(vf0 + 32 * VS * dt + 16 * ks);
+          oacc[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf, pb[ks], oacc[dt], 0, 0, 0);
+        }
+    };
+    if constexpr (IL == 0) {
+      expk(0);
+      expk(1);
+      expk(2);
+      expk(3);
+      pv(0);
+      pv(2);
+    } else {
+      expk(0);
+      expk(1);
+      pv(0);
+      expk(2);
+      expk(3);
+      if constexpr (IL == 2) {
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+          __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);   // DS read (V^T fragment)
+          __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);   // MFMA
+          __builtin_amdgcn_sched_group_barrier(0x002, 5, 0);   // VALU
+        }
       }
+      pv(2);
+    }
+    l_run += (ps4[0] + ps4[1]) + (ps4[2] + ps4[3]);
   };
 
   // static priority for the younger half (waves 4-7): it otherwise loses VALU arbitration to
@@ -277,16 +310,26 @@ EIA_API int eia_paged_prefill_fa(const void* q, long q_stride, void* out, long o
   if (D != FD || (Hq / Hkv) % 4 != 0 || bs % FKB != 0 || out_stride % 8 != 0)
     return EIA_UNSUPPORTED;                                 // (16-B output stores)
   if (n_work == 0) return EIA_OK;
-  static bool attr = false;   // > 64 KiB of dynamic LDS must be opted into
-  if (!attr) {
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(paged_prefill_fa_kernel),
-                              hipFuncAttributeMaxDynamicSharedMemorySize, FA_LDS_BYTES);
-    attr = true;
-  }
+  static const int il = [] {
+    const char* e = getenv("EIA_FA_IL");
+    return e != nullptr ? atoi(e) : 0;
+  }();
   dim3 grid(n_work, Hkv * ((Hq / Hkv) / 4));
-  hipLaunchKernelGGL(paged_prefill_fa_kernel, grid, dim3(FTHREADS), FA_LDS_BYTES, st, (const bf16_t*)q,
-                     q_stride, (bf16_t*)out, out_stride, (const bf16_t*)k_cache,
-                     (const bf16_t*)v_cache, block_tables, bt_stride, seq_lens, cu_q, work,
-                     scale * 1.4426950408889634f, Hq, Hkv, bs, causal, sliding_window, chunk_size);
+#define EIA_FA_L(V)                                                                             \
+  {                                                                                             \
+    static bool attr = false;   /* > 64 KiB of dynamic LDS must be opted into */                \
+    if (!attr) {                                                                                \
+      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(paged_prefill_fa_kernel<V>),      \
+                                hipFuncAttributeMaxDynamicSharedMemorySize, FA_LDS_BYTES);      \
+      attr = true;                                                                              \
+    }                                                                                           \
+    hipLaunchKernelGGL(paged_prefill_fa_kernel<V>, grid, dim3(FTHREADS), FA_LDS_BYTES, st,      \
+                       (const bf16_t*)q, q_stride, (bf16_t*)out, out_stride,                    \
+                       (const bf16_t*)k_cache, (const bf16_t*)v_cache, block_tables, bt_stride, \
+                       seq_lens, cu_q, work, scale * 1.4426950408889634f, Hq, Hkv, bs, causal,  \
+                       sliding_window, chunk_size);                                             \
+  }
+  if (il == 1) EIA_FA_L(1) else if (il == 2) EIA_FA_L(2) else EIA_FA_L(0)
+#undef EIA_FA_L
   EIA_LAUNCH_CHECK();
 }
