@@ -219,6 +219,15 @@ def core_main(fd: int) -> int:
             msgs = intake(reader, busy)
             if busy:
                 lt["intake"] += perf() - ti
+            else:
+                # an idle engine's burst: how long its requests took to reach the core after the
+                # API process received them (first -> last arrival, first arrival -> schedule)
+                arr = [m[5] for m in msgs if m[0] == "add"]
+                if arr:
+                    now = time.time()
+                    lt["bursts"] = lt.get("bursts", 0) + 1
+                    lt["burst_spread"] = lt.get("burst_spread", 0.0) + (max(arr) - min(arr))
+                    lt["burst_wait"] = lt.get("burst_wait", 0.0) + (now - min(arr))
             for msg in msgs:
                 k = msg[0]
                 if k == "add":

@@ -19,7 +19,9 @@ for v in "0 0" "0 1" "1 0"; do
   EIA_DECODE_SK=$1 EIA_ADDNORM_WIDE=$2 timeout -k 10 400 python bench.py --mode engine --steps 3 --warmup 1 > gpurun_out/eng_$1$2.log 2>&1 || exit 1
   echo "SK=$1 WIDE=$2 $(tail -1 gpurun_out/eng_$1$2.log | grep -o '"tpot_p50_ms": [0-9.]*')"
 done
-for il in 0 1 2; do
+EIA_FA_IL=3 timeout -k 10 300 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_kernels_gpu.py -k prefill > gpurun_out/pytest_fa3.log 2>&1
+rc=$?; echo "FA_IL=3 tests: $(tail -1 gpurun_out/pytest_fa3.log)"; [[ $rc != 0 ]] && exit $rc
+for il in 0 1 2 3; do
   EIA_FA_IL=$il timeout -k 10 200 python scripts/bench_prefill_attn.py --shapes 1x8192 4x2048 65x128 --qt 32 > gpurun_out/fa_il$il.log 2>&1 || exit 1
   echo "FA_IL=$il"; grep -o '"shape": "[0-9x]*".*"tflops": [0-9.]*' gpurun_out/fa_il$il.log | sed 's/"causal.*"us"/ us/'
 done
