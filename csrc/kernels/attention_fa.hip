@@ -31,9 +31,9 @@
 // the register file and spill.  Round 4 (profiles/prefill_attn_fa_r4.md): raw v_exp_f32, a
 // branch-free mask, tree max / sum chains, static young-half priority and dwordx4 output stores
 // (65x128: 135 -> 174 TFLOP/s); fetching K/V two tiles ahead (+24 VGPRs) was slower at 1x8192
-// (800 vs 757 us) -- the one-tile-ahead fetch is not the bound there.
-#include <cstdlib>
-
+// (800 vs 757 us) -- the one-tile-ahead fetch is not the bound there -- and a software
+// pipeline computing S of tile i+1 beside the exponentials of tile i (three LDS buffers, two S
+// register sets, 256 VGPRs) ran at 0.81x.
 #include "eia_common.h"
 
 namespace {
@@ -61,9 +61,6 @@ EIA_DEV float pair_sum(float v) {
   return __uint_as_float(r[0]) + __uint_as_float(r[1]);
 }
 
-// IL (A/B of the P.V order, EIA_FA_IL): 0 = all exponentials then P.V, 1 = P.V of key half a
-// beside the exponentials of half b, 2 = 1 with a pinned MFMA / V^T read / VALU interleave
-template <int IL>
 __global__ void __launch_bounds__(FTHREADS, 1)
 paged_prefill_fa_kernel(const bf16_t* __restrict__ q, long q_stride, bf16_t* __restrict__ out,
                         long out_stride, const bf16_t* __restrict__ kc,
@@ -200,10 +197,10 @@ paged_prefill_fa_kernel(const bf16_t* __restrict__ q, long q_stride, bf16_t* __r
       for (int dt = 0; dt < FD / 32; ++dt) oacc[dt] *= alpha;
     }
     const float muse = m_run == (-INFINITY) ? 0.f : m_run;
-    // raw v_exp_f32 (exp2f adds a denormal-range fix-up of 3 VALU per score); row sums as four
-    // independent chains.  P^T of key half a (k-steps 0, 1) first; the P.V MFMAs of half a then
-    // run beside the exponentials of half b (independent work the scheduler is told to
-    // interleave: one MFMA, its V^T read and five VALU per gap), and half b's P.V last.
+    // row sums as four independent chains.  P^T of key half a (k-steps 0, 1) first, its P.V
+    // MFMAs next to the exponentials of half b, then half b's P.V: +1-2 % over all exponentials
+    // first (profiles/prefill_attn_fa_r4.md); pinning that interleave with sched_group_barrier
+    // (one V^T read, one MFMA, five VALU per gap) exposed the LDS read latency: -2 %.
     bf16x8 pb[4];
     float ps4[4] = {0.f, 0.f, 0.f, 0.f};
     auto expk = [&](int ks) {
@@ -223,29 +220,12 @@ paged_prefill_fa_kernel(const bf16_t* __restrict__ q, long q_stride, bf16_t* __r
           oacc[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf, pb[ks], oacc[dt], 0, 0, 0);
         }
     };
-    if constexpr (IL == 0) {
-      expk(0);
-      expk(1);
-      expk(2);
-      expk(3);
-      pv(0);
-      pv(2);
-    } else {
-      expk(0);
-      expk(1);
-      pv(0);
-      expk(2);
-      expk(3);
-      if constexpr (IL == 2) {
-#pragma unroll
-        for (int i = 0; i < 8; ++i) {
-          __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);   // DS read (V^T fragment)
-          __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);   // MFMA
-          __builtin_amdgcn_sched_group_barrier(0x002, 5, 0);   // VALU
-        }
-      }
-      pv(2);
-    }
+    expk(0);
+    expk(1);
+    pv(0);
+    expk(2);
+    expk(3);
+    pv(2);
     l_run += (ps4[0] + ps4[1]) + (ps4[2] + ps4[3]);
   };
 
@@ -296,240 +276,6 @@ paged_prefill_fa_kernel(const bf16_t* __restrict__ q, long q_stride, bf16_t* __r
   }
 }
 
-// Software-pipelined form (EIA_FA_IL=3).  In iteration i a wave computes S = K Q^T of tile i+1
-// while it runs the exponentials of tile i (independent MFMA and VALU streams of one wave, told
-// to interleave: one K fragment read, one MFMA, five VALU per gap), then P.V of tile i.  Tiles i
-// and i+1 are both read from LDS during iteration i, so K/V live in THREE buffers: tile i+2 is
-// written into the one last read in iteration i-1 (before the barrier that ended it).  The
-// mask, row max and (rare) rescale of tile i run before the interleaved block.
-constexpr int FA_PIPE_LDS_BYTES = 3 * BUF * 2;
-
-__global__ void __launch_bounds__(FTHREADS, 1)
-paged_prefill_fa_pipe_kernel(const bf16_t* __restrict__ q, long q_stride, bf16_t* __restrict__ out,
-                             long out_stride, const bf16_t* __restrict__ kc,
-                             const bf16_t* __restrict__ vc, const int* __restrict__ block_tables,
-                             int bt_stride, const int* __restrict__ seq_lens,
-                             const int* __restrict__ cu_q, const int* __restrict__ work,
-                             float scale_log2, int Hq, int Hkv, int bs, int causal,
-                             int sliding_window, int chunk_size) {
-  extern __shared__ __align__(16) bf16_t lds[];         // FA_PIPE_LDS_BYTES
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  const int r32 = lane & 31, h = lane >> 5;
-  const int s = work[2 * blockIdx.x], q0 = work[2 * blockIdx.x + 1];
-  const int G = Hq / Hkv, NHG = G / 4;
-  const int kvh = blockIdx.y / NHG, hg = blockIdx.y % NHG;
-  const int hq = kvh * G + hg * 4 + (w & 3);
-  const int qsub = w >> 2;
-  const int qbeg = cu_q[s], qlen = cu_q[s + 1] - qbeg;
-  if (q0 >= qlen) return;                                  // workgroup-uniform
-  const int L = seq_lens[s], ctx = L - qlen;
-  const bool window = sliding_window > 0 || chunk_size > 0;
-  auto lo_of = [&](int qa) {
-    int lo = 0;
-    if (sliding_window > 0) lo = max(lo, qa - sliding_window + 1);
-    if (chunk_size > 0) lo = max(lo, (qa / chunk_size) * chunk_size);
-    return lo;
-  };
-  const int qi = q0 + 32 * qsub + r32;
-  const bool qvalid = qi < qlen;
-  const int qe = min(qi, qlen - 1);
-  const long tok = qbeg + qe;
-  const int qa = ctx + qe;
-  const int q_lo = lo_of(qa);
-  bf16x8 qf[FD / 16];
-  {
-    const bf16_t* qp = q + tok * q_stride + (long)hq * FD + 8 * h;
-#pragma unroll
-    for (int t = 0; t < FD / 16; ++t) qf[t] = *reinterpret_cast<const bf16x8*>(qp + 16 * t);
-  }
-  const int qlast = min(q0 + FQB, qlen) - 1;
-  const int hi = causal ? min(L, ctx + qlast + 1) : L;
-  const int lo = lo_of(ctx + q0) & ~(FKB - 1);
-  const int ntile = (hi - lo + FKB - 1) / FKB;
-  const int wq0 = q0 + 32 * qsub;
-  const bool wave_live = wq0 < qlen;
-  const int wq1 = min(wq0 + 32, qlen) - 1;
-  const int w_hi = !wave_live ? 0 : (causal ? min(L, ctx + wq1 + 1) : L);
-  const int w_lo = wave_live ? lo_of(ctx + wq0) : 0;
-
-  const int* bt = block_tables + (long)s * bt_stride;
-  const int klast = lo + FKB * max(ntile - 1, 0);
-  auto fetch = [&](int t, bf16x8 (&st)[4]) {               // tile t, clamped to the last one
-    const int kb = min(lo + FKB * t, klast);
-    const int blk = bt[kb / bs];
-    const long base = ((long)blk * Hkv + kvh) * (long)bs * FD;
-    const int o = kb % bs;
-    const bf16_t* kp = kc + base + (long)o * FD;
-    const bf16_t* vp = vc + base + o;
-#pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      const int id = tid + FTHREADS * i;
-      st[i] = *reinterpret_cast<const bf16x8*>(kp + 8 * id);
-      st[2 + i] = *reinterpret_cast<const bf16x8*>(vp + (long)(id >> 3) * bs + 8 * (id & 7));
-    }
-  };
-  auto stash = [&](int buf, const bf16x8 (&st)[4]) {
-    bf16_t* kl = lds + buf * BUF;
-    bf16_t* vl = kl + KBUF;
-#pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      const int id = tid + FTHREADS * i;
-      *reinterpret_cast<bf16x8*>(kl + (id >> 4) * KS + 8 * (id & 15)) = st[i];
-      *reinterpret_cast<bf16x8*>(vl + (id >> 3) * VS + 8 * (id & 7)) = st[2 + i];
-    }
-  };
-  auto vis = [&](int t) {                                   // wave-uniform
-    const int kb = lo + FKB * t;
-    return t < ntile && kb < w_hi && kb + FKB > w_lo;
-  };
-
-  f32x16_t oacc[FD / 32];
-#pragma unroll
-  for (int dt = 0; dt < FD / 32; ++dt)
-#pragma unroll
-    for (int i = 0; i < 16; ++i) oacc[dt][i] = 0.f;
-  float m_run = (-INFINITY), l_run = 0.f;
-  const int krow0 = perm_row(r32);
-
-  // per-lane fragment offsets (elements); the buffer base is wave-uniform (readfirstlane) so
-  // every fragment read stays one address register plus an immediate offset
-  const int kl0 = krow0 * KS + 8 * h, vl0 = KBUF + r32 * VS + 8 * h;
-  auto bbase = [&](int t) { return lds + __builtin_amdgcn_readfirstlane((t % 3) * BUF); };
-  auto qk = [&](int t, f32x16_t (&sacc)[2]) {
-    const bf16_t* kf0 = bbase(t) + kl0;
-#pragma unroll
-    for (int sh = 0; sh < 2; ++sh)
-#pragma unroll
-      for (int t = 0; t < FD / 16; ++t) {
-        const bf16x8 kf = *reinterpret_cast<const bf16x8*>(kf0 + 32 * KS * sh + 16 * t);
-        sacc[sh] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf, qf[t], t == 0 ? f32x16_t{} : sacc[sh],
-                                                           0, 0, 0);
-      }
-  };
-  // mask + row max + deferred rescale of tile t; returns the exponent offset
-  auto prep = [&](int t, f32x16_t (&sacc)[2]) {
-    const int kb = lo + FKB * t;
-    const bool whole = !window && kb + FKB <= L && (!causal || kb + FKB - 1 <= ctx + wq0);
-    if (!whole) {
-      const int kmax = causal ? min(L - 1, qa) : L - 1;
-      const unsigned lim = (unsigned)(kmax - q_lo);
-      const int d0 = kb + 8 * h - q_lo;
-#pragma unroll
-      for (int sh = 0; sh < 2; ++sh)
-#pragma unroll
-        for (int i = 0; i < 16; ++i) {
-          const unsigned dk = (unsigned)(d0 + 32 * sh + 16 * (i >> 3) + (i & 7));
-          sacc[sh][i] = dk <= lim ? sacc[sh][i] : (-INFINITY);
-        }
-    }
-    float mx4[4];
-#pragma unroll
-    for (int c = 0; c < 4; ++c) {
-      mx4[c] = sacc[c >> 1][8 * (c & 1)];
-#pragma unroll
-      for (int j = 1; j < 8; ++j) mx4[c] = fmaxf(mx4[c], sacc[c >> 1][8 * (c & 1) + j]);
-    }
-    const float mt = pair_max(fmaxf(fmaxf(mx4[0], mx4[1]), fmaxf(mx4[2], mx4[3]))) * scale_log2;
-    const bool grow = mt > m_run + DEFER_LOG2;
-    if (__any(grow)) {                                     // wave-uniform, rare
-      const float m_new = grow ? mt : m_run;
-      const float alpha = grow ? exp2f(m_run - m_new) : 1.f;
-      m_run = m_new;
-      l_run *= alpha;
-#pragma unroll
-      for (int dt = 0; dt < FD / 32; ++dt) oacc[dt] *= alpha;
-    }
-    return m_run == (-INFINITY) ? 0.f : m_run;
-  };
-  auto expo = [&](const f32x16_t (&sacc)[2], float muse, bf16x8 (&pb)[4]) {
-    float ps4[4] = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-    for (int ks = 0; ks < 4; ++ks)
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const float p = __builtin_amdgcn_exp2f(fmaf(sacc[ks >> 1][8 * (ks & 1) + j], scale_log2, -muse));
-        pb[ks][j] = f2bf(p);
-        ps4[ks] += p;
-      }
-    l_run += (ps4[0] + ps4[1]) + (ps4[2] + ps4[3]);
-  };
-  auto pv = [&](int t, const bf16x8 (&pb)[4]) {
-    const bf16_t* vf0 = bbase(t) + vl0;
-#pragma unroll
-    for (int dt = 0; dt < FD / 32; ++dt)
-#pragma unroll
-      for (int ks = 0; ks < 4; ++ks) {
-        const bf16x8 vf = *reinterpret_cast<const bf16x8*>(vf0 + 32 * VS * dt + 16 * ks);
-        oacc[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf, pb[ks], oacc[dt], 0, 0, 0);
-      }
-  };
-
-  if (__builtin_amdgcn_readfirstlane(tid) >= FTHREADS / 2) __builtin_amdgcn_s_setprio(1);
-  bf16x8 st[4];
-  if (ntile > 0) {
-    fetch(0, st);
-    stash(0, st);
-    fetch(1, st);
-    stash(1, st);
-  }
-  __syncthreads();
-  f32x16_t sA[2], sB[2];
-  if (vis(0)) qk(0, sA);
-  auto iter = [&](int it, f32x16_t (&scur)[2], f32x16_t (&snext)[2]) {
-    fetch(it + 2, st);
-    const bool vc = vis(it), vn = vis(it + 1);
-    if (vc) {
-      const float muse = prep(it, scur);
-      bf16x8 pb[4];
-      if (vn) {
-        qk(it + 1, snext);
-        expo(scur, muse, pb);
-#pragma unroll
-        for (int i = 0; i < 16; ++i) {
-          __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);   // DS read (K fragment)
-          __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);   // MFMA
-          __builtin_amdgcn_sched_group_barrier(0x002, 5, 0);   // VALU
-        }
-      } else {
-        expo(scur, muse, pb);
-      }
-      pv(it, pb);
-    } else if (vn) {
-      qk(it + 1, snext);
-    }
-    if (it + 2 < ntile) stash((it + 2) % 3, st);
-    __syncthreads();
-  };
-  int it = 0;
-  for (; it + 2 <= ntile; it += 2) {
-    iter(it, sA, sB);
-    iter(it + 1, sB, sA);
-  }
-  if (it < ntile) iter(it, sA, sB);
-
-  const float lt = pair_sum(l_run);
-  if (!qvalid) return;
-  const float inv = lt > 0.f ? 1.f / lt : 0.f;
-  bf16_t* op = out + tok * out_stride + (long)hq * FD + 8 * h;
-#pragma unroll
-  for (int dt = 0; dt < FD / 32; ++dt) {
-    uint2 pk[4];
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      bf16x4 o4;
-#pragma unroll
-      for (int r = 0; r < 4; ++r) o4[r] = f2bf(oacc[dt][4 * j + r] * inv);
-      pk[j] = __builtin_bit_cast(uint2, o4);
-    }
-#pragma unroll
-    for (int j = 0; j < 4; j += 2) {
-      const auto rx = __builtin_amdgcn_permlane32_swap(pk[j].x, pk[j + 1].x, false, false);
-      const auto ry = __builtin_amdgcn_permlane32_swap(pk[j].y, pk[j + 1].y, false, false);
-      *reinterpret_cast<uint4*>(op + 32 * dt + 8 * j) = make_uint4(rx[0], ry[0], rx[1], ry[1]);
-    }
-  }
-}
-
 }  // namespace
 
 // work = [seq, first query] pairs with 64-query blocks (attention.prefill_query_block);
@@ -544,38 +290,16 @@ EIA_API int eia_paged_prefill_fa(const void* q, long q_stride, void* out, long o
   if (D != FD || (Hq / Hkv) % 4 != 0 || bs % FKB != 0 || out_stride % 8 != 0)
     return EIA_UNSUPPORTED;                                 // (16-B output stores)
   if (n_work == 0) return EIA_OK;
-  static const int il = [] {
-    const char* e = getenv("EIA_FA_IL");
-    return e != nullptr ? atoi(e) : 0;
-  }();
-  dim3 grid(n_work, Hkv * ((Hq / Hkv) / 4));
-#define EIA_FA_L(V)                                                                             \
-  {                                                                                             \
-    static bool attr = false;   /* > 64 KiB of dynamic LDS must be opted into */                \
-    if (!attr) {                                                                                \
-      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(paged_prefill_fa_kernel<V>),      \
-                                hipFuncAttributeMaxDynamicSharedMemorySize, FA_LDS_BYTES);      \
-      attr = true;                                                                              \
-    }                                                                                           \
-    hipLaunchKernelGGL(paged_prefill_fa_kernel<V>, grid, dim3(FTHREADS), FA_LDS_BYTES, st,      \
-                       (const bf16_t*)q, q_stride, (bf16_t*)out, out_stride,                    \
-                       (const bf16_t*)k_cache, (const bf16_t*)v_cache, block_tables, bt_stride, \
-                       seq_lens, cu_q, work, scale * 1.4426950408889634f, Hq, Hkv, bs, causal,  \
-                       sliding_window, chunk_size);                                             \
+  static bool attr = false;   // > 64 KiB of dynamic LDS must be opted into
+  if (!attr) {
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(paged_prefill_fa_kernel),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, FA_LDS_BYTES);
+    attr = true;
   }
-  if (il == 3) {
-    static bool attr3 = false;
-    if (!attr3) {
-      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(paged_prefill_fa_pipe_kernel),
-                                hipFuncAttributeMaxDynamicSharedMemorySize, FA_PIPE_LDS_BYTES);
-      attr3 = true;
-    }
-    hipLaunchKernelGGL(paged_prefill_fa_pipe_kernel, grid, dim3(FTHREADS), FA_PIPE_LDS_BYTES, st,
-                       (const bf16_t*)q, q_stride, (bf16_t*)out, out_stride,
-                       (const bf16_t*)k_cache, (const bf16_t*)v_cache, block_tables, bt_stride,
-                       seq_lens, cu_q, work, scale * 1.4426950408889634f, Hq, Hkv, bs, causal,
-                       sliding_window, chunk_size);
-  } else if (il == 1) EIA_FA_L(1) else if (il == 2) EIA_FA_L(2) else EIA_FA_L(0)
-#undef EIA_FA_L
+  dim3 grid(n_work, Hkv * ((Hq / Hkv) / 4));
+  hipLaunchKernelGGL(paged_prefill_fa_kernel, grid, dim3(FTHREADS), FA_LDS_BYTES, st, (const bf16_t*)q,
+                     q_stride, (bf16_t*)out, out_stride, (const bf16_t*)k_cache,
+                     (const bf16_t*)v_cache, block_tables, bt_stride, seq_lens, cu_q, work,
+                     scale * 1.4426950408889634f, Hq, Hkv, bs, causal, sliding_window, chunk_size);
   EIA_LAUNCH_CHECK();
 }

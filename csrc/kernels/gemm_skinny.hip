@@ -625,23 +625,38 @@ splitk_add_rmsnorm_wide_kernel(const float* __restrict__ part, int sk_rt, int M,
   if (!s_last) return;
   // last arriver: agent-scope loads of the other chunks' partials and residual pieces (they
   // may sit in another XCD's L2 only as write-through copies: these loads go past our L2)
+  // Every load is issued before its first use, in groups of 8 chunks with the chunk index
+  // clamped (a "register or load" select per chunk makes hipcc branch around each load and wait
+  // vmcnt(0) per element: one serial round trip per chunk, guide 5.4 item 4(c)).
   auto ldf = [](const float* p) { return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); };
   float sum = 0.f;
-  for (int k = 0; k < nch; ++k) sum += k == ch ? tot : ldf(ssp + (long)row * nch + k);
+  for (int k0 = 0; k0 < nch; k0 += 8) {
+    float pv[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) pv[j] = ldf(ssp + (long)row * nch + min(k0 + j, nch - 1));
+#pragma unroll
+    for (int j = 0; j < 8; ++j) sum += k0 + j < nch ? pv[j] : 0.f;
+  }
   const float inv = rsqrtf(sum / (float)H + eps);
   const bf16_t* rrow = residual + (long)row * H;
-#pragma unroll 4
-  for (int k = 0; k < nch; ++k) {
-    const int cc = k * 512 + threadIdx.x * 4;
-    const bf16x4 v = k == ch ? nr
-                             : __builtin_bit_cast(bf16x4, __hip_atomic_load(
-                                   reinterpret_cast<const unsigned long long*>(rrow + cc),
-                                   __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-    const bf16x4 ww = *reinterpret_cast<const bf16x4*>(w + cc);
-    bf16x4 o;
+  for (int k0 = 0; k0 < nch; k0 += 8) {
+    bf16x4 rv[8], wv[8];
 #pragma unroll
-    for (int j = 0; j < 4; ++j) o[j] = f2bf(bf2f(v[j]) * inv * bf2f(ww[j]));
-    *reinterpret_cast<bf16x4*>(out + (long)row * ldo + cc) = o;
+    for (int j = 0; j < 8; ++j) {
+      const int cc = min(k0 + j, nch - 1) * 512 + threadIdx.x * 4;
+      rv[j] = __builtin_bit_cast(bf16x4, __hip_atomic_load(
+                  reinterpret_cast<const unsigned long long*>(rrow + cc), __ATOMIC_RELAXED,
+                  __HIP_MEMORY_SCOPE_AGENT));
+      wv[j] = *reinterpret_cast<const bf16x4*>(w + cc);
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      if (k0 + j >= nch) break;
+      bf16x4 o;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) o[e] = f2bf(bf2f(rv[j][e]) * inv * bf2f(wv[j][e]));
+      *reinterpret_cast<bf16x4*>(out + (long)row * ldo + (k0 + j) * 512 + threadIdx.x * 4) = o;
+    }
   }
   if (threadIdx.x == 0) __hip_atomic_store(cnt + row, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
