@@ -149,3 +149,37 @@ def test_sk_unit_table_overflow_and_empty():
     bt = np.zeros((2, 4), dtype=np.int32)
     assert sk_unit_table(np.array([0, 0]), bt, 8, 128, out) == 0
     assert sk_unit_table(np.array([100, 1]), bt, 8, 128, out) == -1     # 40 units > 4 rows
+
+
+def test_decode_partition_heuristic():
+    """Context partitions per decode batch (ops/attention.py decode_partitions), pinned to the
+    measured rows: short contexts never split; 1-2 items per CU split 4 ways when the items do
+    not divide the CUs (B 35 x 8 KV heads = 280, profiles/attn_long_r4.log) and 2 ways when they
+    do (B 32 = 256); >= 2 items per CU split 2 ways (B 65 ctx 4096); small grids split up to one
+    workgroup per CU."""
+    from enterprise_inference_amd.ops.attention import decode_partitions
+    assert decode_partitions(65, 8, 32, 256) == 1
+    assert decode_partitions(35, 8, 32, 4096) == 4
+    assert decode_partitions(35, 8, 32, 2048) == 4
+    assert decode_partitions(35, 8, 32, 1024) == 2
+    assert decode_partitions(32, 8, 32, 4096) == 2
+    assert decode_partitions(65, 8, 32, 4096) == 2
+    assert decode_partitions(128, 8, 32, 4096) == 1          # >= 4 items per CU
+    assert decode_partitions(16, 8, 32, 4096) == 2
+    assert decode_partitions(1, 8, 32, 4096) == 8
+
+
+def test_addnorm_workspace_not_made_inside_capture(monkeypatch):
+    """The full-chip add+RMSNorm's shared workspace (row counters that must start at zero) is
+    never allocated inside graph capture: a capture that reaches it first falls back to the
+    row-per-workgroup kernel instead."""
+    import torch
+    from enterprise_inference_amd.ops import gemm
+    monkeypatch.setattr(gemm, "_ADDNORM_WS", {})
+    monkeypatch.setattr(torch.cuda, "is_current_stream_capturing", lambda: True)
+    assert gemm._addnorm_ws(torch.device("cpu"), 65, 4096) is None
+    assert gemm._ADDNORM_WS == {}
+    monkeypatch.setattr(torch.cuda, "is_current_stream_capturing", lambda: False)
+    ws = gemm._addnorm_ws(torch.device("cpu"), 65, 4096)
+    assert ws is not None and int(ws[1].abs().sum()) == 0 and ws[0].numel() >= 65 * 8
+    assert gemm._addnorm_ws(torch.device("cpu"), 129, 4096) is None      # > MAX_M rows
