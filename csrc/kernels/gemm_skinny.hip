@@ -564,103 +564,6 @@ splitk_add_rmsnorm_kernel(const float* __restrict__ part, int sk_rt, int M, int 
   }
 }
 
-// Full-chip form of the above: grid (H / 512, M), 128 threads x 4 columns per workgroup.
-// The row-per-workgroup kernel keeps only M (~65) CUs busy and is bound by their per-CU HBM
-// rate (5.4 us at SK 8 / H 4096 in profiles/rocprof_r3b_trace_gaps.md, for an 8.5 MB slab
-// stream the chip moves in ~1.5 us).  Here every workgroup sums one 512-column chunk of its
-// row's slabs (all SK loads in flight), adds and stores the residual, and publishes the chunk's
-// sum of squares; the row's last arriver (agent-scope counter, self-resetting for graph replay)
-// turns the partials into 1/rms in chunk order -- deterministic -- and writes the normalised
-// row.  Residual stores, partials and the last arriver's loads of them are agent-scope atomics
-// (the last arriver may sit on another XCD), the protocol of attention_sk.hip's merge.
-template <int SK>
-__global__ void __launch_bounds__(128)
-splitk_add_rmsnorm_wide_kernel(const float* __restrict__ part, int sk_rt, int M, int H,
-                               bf16_t* __restrict__ residual, const bf16_t* __restrict__ w,
-                               float eps, bf16_t* __restrict__ out, long ldo,
-                               float* __restrict__ ssp, int* __restrict__ cnt) {
-  __shared__ float scratch[2];
-  __shared__ int s_last;
-  const int row = blockIdx.y, ch = blockIdx.x, nch = gridDim.x;
-  const int c = ch * 512 + threadIdx.x * 4;
-  const long total = (long)M * H;
-  const long off = (long)row * H + c;
-  const int sk = SK > 0 ? SK : sk_rt;
-  f32x4 a;
-  if constexpr (SK > 0) {
-    f32x4 p[SK];
-#pragma unroll
-    for (int k = 0; k < SK; ++k) p[k] = *reinterpret_cast<const f32x4*>(part + k * total + off);
-    a = p[0];
-#pragma unroll
-    for (int k = 1; k < SK; ++k) a += p[k];
-  } else {
-    a = *reinterpret_cast<const f32x4*>(part + off);
-    for (int k = 1; k < sk; ++k) a += *reinterpret_cast<const f32x4*>(part + k * total + off);
-  }
-  const bf16x4 rr = *reinterpret_cast<const bf16x4*>(residual + off);
-  bf16x4 nr;
-  float ss = 0.f;
-#pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    nr[j] = f2bf(a[j] + bf2f(rr[j]));
-    const float v = bf2f(nr[j]);
-    ss += v * v;
-  }
-  __hip_atomic_store(reinterpret_cast<unsigned long long*>(residual + off),
-                     __builtin_bit_cast(unsigned long long, nr), __ATOMIC_RELAXED,
-                     __HIP_MEMORY_SCOPE_AGENT);
-  const float tot = block_sum(ss, scratch);
-  if (threadIdx.x == 0) {
-    __hip_atomic_store(ssp + (long)row * nch + ch, tot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  }
-  // publish: the agent-scope (write-through) stores have completed before the arrival count
-  // (no release fence: at agent scope it writes back the whole L2, per workgroup)
-  __builtin_amdgcn_s_waitcnt(0);
-  __syncthreads();
-  if (threadIdx.x == 0)
-    s_last = __hip_atomic_fetch_add(cnt + row, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
-             nch - 1;
-  __syncthreads();
-  if (!s_last) return;
-  // last arriver: agent-scope loads of the other chunks' partials and residual pieces (they
-  // may sit in another XCD's L2 only as write-through copies: these loads go past our L2)
-  // Every load is issued before its first use, in groups of 8 chunks with the chunk index
-  // clamped (a "register or load" select per chunk makes hipcc branch around each load and wait
-  // vmcnt(0) per element: one serial round trip per chunk, guide 5.4 item 4(c)).
-  auto ldf = [](const float* p) { return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); };
-  float sum = 0.f;
-  for (int k0 = 0; k0 < nch; k0 += 8) {
-    float pv[8];
-#pragma unroll
-    for (int j = 0; j < 8; ++j) pv[j] = ldf(ssp + (long)row * nch + min(k0 + j, nch - 1));
-#pragma unroll
-    for (int j = 0; j < 8; ++j) sum += k0 + j < nch ? pv[j] : 0.f;
-  }
-  const float inv = rsqrtf(sum / (float)H + eps);
-  const bf16_t* rrow = residual + (long)row * H;
-  for (int k0 = 0; k0 < nch; k0 += 8) {
-    bf16x4 rv[8], wv[8];
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const int cc = min(k0 + j, nch - 1) * 512 + threadIdx.x * 4;
-      rv[j] = __builtin_bit_cast(bf16x4, __hip_atomic_load(
-                  reinterpret_cast<const unsigned long long*>(rrow + cc), __ATOMIC_RELAXED,
-                  __HIP_MEMORY_SCOPE_AGENT));
-      wv[j] = *reinterpret_cast<const bf16x4*>(w + cc);
-    }
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      if (k0 + j >= nch) break;
-      bf16x4 o;
-#pragma unroll
-      for (int e = 0; e < 4; ++e) o[e] = f2bf(bf2f(rv[j][e]) * inv * bf2f(wv[j][e]));
-      *reinterpret_cast<bf16x4*>(out + (long)row * ldo + (k0 + j) * 512 + threadIdx.x * 4) = o;
-    }
-  }
-  if (threadIdx.x == 0) __hip_atomic_store(cnt + row, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-
 template <int MT, int NT, int WAVES, int S, bool GROUPED, int KC, bool LOADER = false,
           bool PACKED = false>
 int launch_cfg(const bf16_t* X, long ldx, const bf16_t* W, long ldw, const bf16_t* bias, void* out,
@@ -961,26 +864,3 @@ EIA_API int eia_splitk_add_rmsnorm(const float* part, int sk, int M, int H, void
   EIA_LAUNCH_CHECK();
 }
 
-// Full-chip variant: ssp = fp32 workspace [M][H / 512], cnt = int32 [M] zero-initialised once
-// (the kernel leaves it zero).  One stream at a time per workspace.
-EIA_API int eia_splitk_add_rmsnorm_wide(const float* part, int sk, int M, int H, void* residual,
-                                        const void* w, float eps, void* out, long ldo, float* ssp,
-                                        int* cnt, hipStream_t st) {
-  if (H % 512 != 0 || sk < 1 || M < 1 || ldo % 4) return EIA_BAD_SHAPE;
-  bf16_t* res = static_cast<bf16_t*>(residual);
-  const bf16_t* ww = static_cast<const bf16_t*>(w);
-  bf16_t* o = static_cast<bf16_t*>(out);
-  const dim3 grid(H / 512, M);
-#define EIA_SKW(K)                                                                           \
-  hipLaunchKernelGGL((splitk_add_rmsnorm_wide_kernel<K>), grid, dim3(128), 0, st, part, sk, M, \
-                     H, res, ww, eps, o, ldo, ssp, cnt)
-  switch (sk) {
-    case 1: EIA_SKW(1); break;
-    case 2: EIA_SKW(2); break;
-    case 4: EIA_SKW(4); break;
-    case 8: EIA_SKW(8); break;
-    default: EIA_SKW(0); break;
-  }
-#undef EIA_SKW
-  EIA_LAUNCH_CHECK();
-}

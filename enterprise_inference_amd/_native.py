@@ -42,12 +42,6 @@ _SIGNATURES = {
     "eia_paged_decode": [P, L, P, P, IP, I, IP, P, L, P, P, P, F, I, I, I, I, I, I, I, I, IP, S],
     "eia_paged_decode_rope": [P, L, P, I, P, P, P, F, IP, P, IP, I, P, P, IP, I, IP, P, L, P, P, P,
                               F, I, I, I, I, I, I, I, I, IP, S],
-    # table, tu, nwg, qkv, qkv_stride, part, sk, bias, q_norm_w, k_norm_w, eps, positions,
-    # cos_sin, slot_mapping, T, k_cache, v_cache, out, out_stride, part_o, part_ml, cnt, scale,
-    # Hq, Hkv, D, bs, stream
-    "eia_paged_decode_sk": [IP, IP, I, P, L, P, I, P, P, P, F, IP, P, IP, I, P, P, P, L, P, P, IP,
-                            F, I, I, I, I, S],
-    "eia_sk_decode_lds_bytes": [I, I],
     "eia_paged_prefill": [P, L, P, L, P, P, IP, I, IP, IP, IP, I, F, I, I, I, I, I, I, I, I, I, S],
     "eia_paged_prefill_fa": [P, L, P, L, P, P, IP, I, IP, IP, IP, I, F, I, I, I, I, I, I, I, S],
     "eia_act_and_mul": [P, P, I, I, L, L, I, S],
@@ -67,7 +61,6 @@ _SIGNATURES = {
     "eia_gemm_skinny": [P, L, P, L, P, P, L, I, I, I, I, I, I, S],
     "eia_splitk_reduce": [P, I, I, I, P, P, L, S],
     "eia_splitk_add_rmsnorm": [P, I, I, I, P, P, F, P, L, S],
-    "eia_splitk_add_rmsnorm_wide": [P, I, I, I, P, P, F, P, L, P, P, S],
     "eia_ar_alloc": [P, L],
     "eia_ar_free": [P],
     "eia_ar_signal_bytes": [],

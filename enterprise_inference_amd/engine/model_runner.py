@@ -167,7 +167,6 @@ class ModelRunner:
         self.kv_caches: List[Tuple[torch.Tensor, torch.Tensor]] = []
         self.num_blocks = 0
         self.graphs: Dict[int, torch.cuda.CUDAGraph] = {}
-        self.graphs_sk: Dict[int, torch.cuda.CUDAGraph] = {}     # stream-K decode variants
         self.graph_P: Dict[int, int] = {}
         self.graph_pool = None
         self.ar_poller = None            # custom all-reduce error poller (TP>1 on GPUs)
@@ -198,11 +197,6 @@ class ModelRunner:
         # previous step's sampler output holding this row's input token (-1: host id)
         self.hdr_len = 5 * S + 4
         self.src_off = 4 * S + 4
-        # stream-K decode unit table (ops/attention.py sk_unit_table): row 0 = (TU, 0, 0, 0),
-        # then at most SK_UNITS units per workgroup; built from the graph header per step
-        self.sk_nwg = attn_ops.sk_workgroups(self.num_cus)
-        self.sk_cap = self._sk_capable()
-        self.sk_rows = attn_ops.SK_UNITS * self.sk_nwg + 1 if self.sk_cap else 1
         # eager region: packed per step
         self.e_size = 3 * T + 2 * S * mb + 4 * S + 1 + 2 * self.max_work + S + 64
         # Host staging is double-buffered: with overlapped scheduling step k+1 is prepared
@@ -217,7 +211,6 @@ class ModelRunner:
         self.d_g_hdr = torch.zeros(self.hdr_len, dtype=torch.int32, device=dev)
         self.d_g_bt = torch.zeros(S * mb, dtype=torch.int32, device=dev)
         self.d_e_buf = torch.zeros(self.e_size, dtype=torch.int32, device=dev)
-        self.d_g_sk = torch.zeros(self.sk_rows * 4, dtype=torch.int32, device=dev)
         # per-row sampling parameters, one region (one H2D copy per step): temp|top_p|min_p
         # (f32 [3S]), top_k (i32 [S]), seeds (i64 [S], 8-B aligned at word 4S)
         self.d_s_all = torch.zeros(6 * S, dtype=torch.int32, device=dev)
@@ -247,7 +240,6 @@ class ModelRunner:
             "g_hdr": torch.zeros(self.hdr_len, dtype=torch.int32, pin_memory=pin),
             "g_bt": torch.zeros(S * mb, dtype=torch.int32, pin_memory=pin),
             "e_buf": torch.zeros(self.e_size, dtype=torch.int32, pin_memory=pin),
-            "g_sk": torch.zeros(self.sk_rows * 4, dtype=torch.int32, pin_memory=pin),
             "s_all": s_all,
             "s_f32": s_f32,   # temp|top_p|min_p
             "s_i32": s_i32,   # top_k
@@ -479,46 +471,11 @@ class ModelRunner:
         hdr[4 * S] = min(self._decode_partitions(Bp, max_len), self.graph_P.get(Bp, 1))
         return StepPlan("graph", Bp=Bp, nd=n)
 
-    def _sk_capable(self) -> bool:
-        """The stream-K decode kernel serves this model's pure-decode graph steps: fused RoPE
-        decode (NEOX, head dim 64/128, <= 16 q heads per KV head), 32-token-aligned blocks,
-        no sliding-window / chunked-attention layers (their visible range is per layer)."""
-        m = self.cfg.model
-        if not (self.is_gpu and attn_ops.SK_ENABLED and self.pp == 1):
-            return False
-        if self.head_dim not in (64, 128) or self.num_heads // max(1, self.num_kv_heads) > 16:
-            return False
-        if self.block_size % 32 or getattr(m, "sliding_window", None) or \
-                getattr(m, "attention_chunk_size", None):
-            return False
-        return os.environ.get("EIA_DECODE_FUSED_ROPE", "1") != "0"
-
-    def _build_sk(self, Bp: int) -> int:
-        """Unit table of this graph step into the pinned g_sk; returns TU (<= 0: classic)."""
-        S = self.max_num_seqs
-        lens = self.g_hdr.numpy()[3 * S:3 * S + Bp]
-        tab = self.g_sk.numpy().reshape(-1, 4)
-        bt = self.g_bt.numpy()[:Bp * self.maxb].reshape(Bp, self.maxb)
-        TU = attn_ops.sk_unit_table(lens, bt, self.num_kv_heads, self.block_size, tab[1:])
-        if TU > 0:
-            tab[0, 0] = TU
-        return TU
-
-    def _upload_graph(self, Bp: int) -> bool:  # noqa: D401 - H2D of the graph header
-        """Stage the graph step's inputs; True when the stream-K decode graph applies."""
+    def _upload_graph(self, Bp: int) -> None:  # noqa: D401 - H2D of the graph header
         self.d_g_hdr.copy_(self.g_hdr, non_blocking=True)
         self.d_g_bt[:Bp * self.maxb].copy_(self.g_bt[:Bp * self.maxb], non_blocking=True)
-        if not self.sk_cap or Bp not in self.graphs_sk:
-            return False
-        TU = self._build_sk(Bp)
-        if TU <= 0:
-            return False
-        n = 4 * (TU + 1)
-        self.d_g_sk[:n].copy_(self.g_sk[:n], non_blocking=True)
-        return True
 
-    def _graph_metadata(self, Bp: int, P: int,
-                        sk: bool = False) -> Tuple[torch.Tensor, attn_ops.AttentionMetadata]:
+    def _graph_metadata(self, Bp: int, P: int) -> Tuple[torch.Tensor, attn_ops.AttentionMetadata]:
         S = self.max_num_seqs
         d = self.d_g_hdr
         md = attn_ops.AttentionMetadata(
@@ -526,13 +483,12 @@ class ModelRunner:
             positions=d[S:S + Bp], decode_block_tables=self.d_g_bt[:Bp * self.maxb].view(Bp, self.maxb),
             decode_seq_lens=d[3 * S:3 * S + Bp], decode_partitions=P, decode_part_o=self.part_o,
             decode_part_ml=self.part_ml, decode_part_cnt=self.part_cnt,
-            decode_p_dyn=d[4 * S:4 * S + 1],
-            decode_sk=(self.d_g_sk[4:], self.d_g_sk[0:1], self.sk_nwg) if sk else None)
+            decode_p_dyn=d[4 * S:4 * S + 1])
         return d[:Bp], md
 
-    def _graph_forward(self, Bp: int, P: int, sk: bool = False) -> torch.Tensor:
+    def _graph_forward(self, Bp: int, P: int) -> torch.Tensor:
         """Body of a decode graph: in-flight input ids from d_tok, forward, logits."""
-        ids, md = self._graph_metadata(Bp, P, sk)
+        ids, md = self._graph_metadata(Bp, P)
         sampling_ops.fill_ids(ids, self.d_g_hdr[self.src_off:self.src_off + Bp], self.d_tok)
         h = self.model(ids, md, self.kv_caches)
         return self._logits(h)
@@ -722,9 +678,7 @@ class ModelRunner:
             self.apply_swaps(plan.swap)     # before the step's kernels, on the step stream
         if plan["kind"] == "graph":
             Bp = plan["Bp"]
-            if self._upload_graph(Bp):          # same decision on every TP rank (same data)
-                self.graphs_sk[Bp].replay()
-                return self.graph_logits_sk[Bp][:plan["nd"]]
+            self._upload_graph(Bp)
             self.graphs[Bp].replay()
             return self.graph_logits[Bp][:plan["nd"]]
         off = plan["off"]
@@ -942,7 +896,6 @@ class ModelRunner:
         t0 = time.time()
         buckets = buckets or graph_buckets(self.max_num_seqs, self.cfg.scheduler.decode_bs_bucket_step)
         self.graph_logits: Dict[int, torch.Tensor] = {}
-        self.graph_logits_sk: Dict[int, torch.Tensor] = {}
         self.graph_pool = torch.cuda.graph_pool_handle()
         # dummy decode inputs: len 1, slot -1 (no cache write), block 0
         S = self.max_num_seqs
@@ -967,20 +920,6 @@ class ModelRunner:
                     logits = self._graph_forward(Bp, P)
                 self.graphs[Bp] = g
                 self.graph_logits[Bp] = logits
-                if self.sk_cap:
-                    # dummy stream-K table: one unit (len 1, block 0) per (row, KV head)
-                    tab = torch.zeros(Bp * self.num_kv_heads + 1, 4, dtype=torch.int32)
-                    tab[0, 0] = Bp * self.num_kv_heads
-                    tab[1:, 0] = torch.arange(Bp * self.num_kv_heads, dtype=torch.int32)
-                    tab[1:, 3] = 1
-                    self.d_g_sk[:tab.numel()].copy_(tab.view(-1))
-                    if not self.cfg.skip_warmup:
-                        self._graph_forward(Bp, P, sk=True)
-                    gs = torch.cuda.CUDAGraph()
-                    with torch.cuda.graph(gs, pool=self.graph_pool, stream=stream):
-                        logits_sk = self._graph_forward(Bp, P, sk=True)
-                    self.graphs_sk[Bp] = gs
-                    self.graph_logits_sk[Bp] = logits_sk
         torch.cuda.current_stream().wait_stream(stream)
         torch.cuda.synchronize()
         dt = time.time() - t0

@@ -13,7 +13,6 @@ import math
 import os
 from typing import List, Optional, Sequence
 
-import numpy as np
 import torch
 
 from . import reference as ref
@@ -132,48 +131,6 @@ def decode_partitions(batch: int, num_kv_heads: int, num_heads: int, max_len: in
     return max(1, min(p, max_parts, max_len // 128))
 
 
-# Stream-K short-context decode (csrc/kernels/attention_sk.hip): 2 workgroups per CU, each
-# taking at most SK_UNITS 32-token (item, unit) pairs of the step, one per wave.
-SK_ENABLED = os.environ.get("EIA_DECODE_SK", "0") != "0"
-SK_UNITS = 8
-
-
-def sk_workgroups(num_cus: int) -> int:
-    return 2 * num_cus
-
-
-def sk_unit_table(lens: np.ndarray, block_tables: np.ndarray, num_kv_heads: int,
-                  block_size: int, out: np.ndarray) -> int:
-    """Fill ``out[:TU]`` (int32 [>= TU, 4]) with (item = b * Hkv + kvh, unit, physical block,
-    L) for every 32-token unit of every (sequence, KV head) item, in item order; returns TU,
-    or -1 when the table does not fit ``out`` (the caller then takes the classic kernel).
-    Rows with L = 0 (graph padding) have no units."""
-    lens = np.asarray(lens, dtype=np.int64)
-    B = lens.shape[0]
-    U = (lens + 31) // 32
-    per_item = np.repeat(U, num_kv_heads)
-    TU = int(per_item.sum())
-    if TU > out.shape[0]:
-        return -1
-    if TU == 0:
-        return 0
-    item = np.repeat(np.arange(B * num_kv_heads, dtype=np.int64), per_item)
-    first = np.cumsum(per_item) - per_item
-    u = np.arange(TU, dtype=np.int64) - np.repeat(first, per_item)
-    b = item // num_kv_heads
-    t = out[:TU]
-    t[:, 0] = item
-    t[:, 1] = u
-    t[:, 2] = block_tables[b, (u * 32) // block_size]
-    t[:, 3] = lens[b]
-    return TU
-
-
-def sk_wg_of(x: int, TU: int, G: int) -> int:
-    """Workgroup owning global unit x (mirror of the kernel's sk_wg_of)."""
-    return ((x + 1) * G - 1) // TU
-
-
 @dataclasses.dataclass
 class AttentionMetadata:
     num_decode: int
@@ -188,8 +145,6 @@ class AttentionMetadata:
     decode_part_ml: Optional[torch.Tensor] = None
     decode_part_cnt: Optional[torch.Tensor] = None      # zeroed int32 [Bd*Hkv*ceil(G/16)]
     decode_p_dyn: Optional[torch.Tensor] = None         # device int32 [1]: partitions this step
-    # stream-K decode (sk_unit_table): (int32 table [>= TU, 4], int32 [1] TU, workgroups)
-    decode_sk: Optional[tuple] = None
     # prefill part
     prefill_block_tables: Optional[torch.Tensor] = None  # [Sp, maxb] int32
     prefill_seq_lens: Optional[torch.Tensor] = None      # [Sp] int32 (context + new)
@@ -348,23 +303,6 @@ def decode_rope_attention(qkv, md: AttentionMetadata, k_cache: torch.Tensor,
         require(md.decode_part_o is not None and md.decode_part_ml is not None and
                 md.decode_part_o.numel() >= B * num_heads * P * head_dim, "decode workspace")
     o = torch.empty((B, num_heads, head_dim), dtype=torch.bfloat16, device=k_cache.device)
-    if md.decode_sk is not None and not sliding_window and not chunk_size:
-        table, tu, nwg = md.decode_sk
-        G = num_heads // num_kv_heads
-        require(md.decode_part_o is not None and md.decode_part_cnt is not None and
-                md.decode_part_o.numel() >= nwg * 2 * G * head_dim and
-                md.decode_part_ml.numel() >= nwg * 2 * G * 2 and
-                md.decode_part_cnt.numel() >= B * num_kv_heads, "stream-K decode workspace")
-        rc = lib().eia_paged_decode_sk(
-            ptr(table), ptr(tu), nwg, None if split else ptr(qkv), 0 if split else qkv.stride(0),
-            ptr(qkv.part) if split else None, qkv.sk if split else 0, ptr(bias), ptr(q_norm_w),
-            ptr(k_norm_w), float(norm_eps), ptr(md.positions), ptr(rotary.cos_sin),
-            ptr(md.slot_mapping), T, ptr(k_cache), ptr(v_cache), ptr(o), o.stride(0),
-            ptr(md.decode_part_o), ptr(md.decode_part_ml), ptr(md.decode_part_cnt), float(scale),
-            num_heads, num_kv_heads, head_dim, k_cache.shape[2], stream(o))
-        if rc != EIA_UNSUPPORTED:
-            check(rc, "paged_decode_sk")
-            return o
     rc = lib().eia_paged_decode_rope(
         None if split else ptr(qkv), 0 if split else qkv.stride(0),
         ptr(qkv.part) if split else None, qkv.sk if split else 0,

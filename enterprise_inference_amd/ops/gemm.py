@@ -302,28 +302,6 @@ def linear(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = None
     return F.linear(x, w, bias)
 
 
-# Full-chip split-K add+RMSNorm (grid H/512 x M, per-row last arriver); 0 -> the row-per-
-# workgroup kernel.  The workspace (per-chunk sums of squares + self-resetting row counters) is
-# made once per device outside graph capture and shared by every call on that device: decode
-# runs on one stream at a time.
-ADDNORM_WIDE = os.environ.get("EIA_ADDNORM_WIDE", "0") == "1"
-_ADDNORM_WS: dict = {}
-
-
-def _addnorm_ws(device: torch.device, M: int, H: int):
-    key = device.index
-    ws = _ADDNORM_WS.get(key)
-    if ws is None:
-        if torch.cuda.is_current_stream_capturing():
-            return None           # never allocate (or zero) a shared workspace inside a graph
-        ws = (torch.zeros(MAX_M * 64, dtype=torch.float32, device=device),
-              torch.zeros(MAX_M, dtype=torch.int32, device=device))
-        _ADDNORM_WS[key] = ws
-    if M > MAX_M or M * (H // 512) > ws[0].numel():
-        return None
-    return ws
-
-
 def splitk_add_rmsnorm(s: SplitK, residual: torch.Tensor, weight: torch.Tensor, eps: float):
     """residual += reduce(s) (+bias); returns (rmsnorm(residual) * weight, residual)."""
     if s.bias is not None:
@@ -331,13 +309,6 @@ def splitk_add_rmsnorm(s: SplitK, residual: torch.Tensor, weight: torch.Tensor, 
         from .norm import fused_add_rms_norm
         return fused_add_rms_norm(h, residual, weight, eps)
     out = torch.empty(s.M, s.N, dtype=torch.bfloat16, device=residual.device)
-    ws = _addnorm_ws(residual.device, s.M, s.N) if ADDNORM_WIDE and s.N % 512 == 0 else None
-    if ws is not None:
-        check(lib().eia_splitk_add_rmsnorm_wide(ptr(s.part), s.sk, s.M, s.N, ptr(residual),
-                                                ptr(weight), float(eps), ptr(out), out.stride(0),
-                                                ptr(ws[0]), ptr(ws[1]), stream(out)),
-              "splitk_add_rmsnorm_wide")
-        return out, residual
     check(lib().eia_splitk_add_rmsnorm(ptr(s.part), s.sk, s.M, s.N, ptr(residual), ptr(weight),
                                        float(eps), ptr(out), out.stride(0), stream(out)),
           "splitk_add_rmsnorm")

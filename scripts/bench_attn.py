@@ -128,29 +128,6 @@ def main():
                         assert rc == 0, rc
                     t = graph_time(fused_call)
                     res.append((round(t - flush_us, 2), P, "rope"))
-                # stream-K form (csrc/kernels/attention_sk.hip) on the same inputs
-                import numpy as np
-                nwg = attention.sk_workgroups(torch.cuda.get_device_properties(0).multi_processor_count)
-                tab = np.zeros((8 * nwg + 1, 4), dtype=np.int32)
-                TU = attention.sk_unit_table(sl.cpu().numpy(), bt.cpu().numpy(), a.hkv, a.bs,
-                                             tab[1:])
-                if 0 < TU <= 8 * nwg:
-                    tab[0, 0] = TU
-                    dtab = torch.from_numpy(tab).to(dev).view(-1)
-                    G = a.hq // a.hkv
-                    po = torch.empty(max(nwg * 2 * G, B * a.hq) * a.d, device=dev)
-                    pml = torch.empty(max(nwg * 2 * G, B * a.hq) * 2, device=dev)
-                    cnt = torch.zeros(B * a.hkv, dtype=torch.int32, device=dev)
-
-                    def sk_call():
-                        rc = lib().eia_paged_decode_sk(
-                            ptr(dtab[4:]), ptr(dtab[0:1]), nwg, None, 0, ptr(part), a.fused_sk,
-                            None, None, None, 1e-6, ptr(pos), ptr(cs), ptr(slot), B, ptr(k),
-                            ptr(v), ptr(out), out.stride(0), ptr(po), ptr(pml), ptr(cnt),
-                            float(a.d ** -0.5), a.hq, a.hkv, a.d, a.bs, stream(out))
-                        assert rc == 0, rc
-                    t = graph_time(sk_call)
-                    res.append((round(t - flush_us, 2), 1, "stream-k"))
             res.sort(key=lambda r: r[0])
             auto = attention.decode_partitions(B, a.hkv, a.hq, L)
             print(json.dumps({"B": B, "ctx": L, "best_us": res[0][0], "best_P": res[0][1],

@@ -68,89 +68,6 @@ def test_swizzled_stores_are_a_permutation():
 
 # ----------------------------------------------------------------------------- stream-K decode
 
-def _sk_model(lens, Hkv, G, bs=128):
-    """Python model of the stream-K decode kernel's work split (attention_sk.hip): per workgroup
-    the unit range, its segments, which segments are cut (partial) and into which slot, and
-    each cut item's piece count / merger slot rule."""
-    import numpy as np
-
-    from enterprise_inference_amd.ops.attention import sk_unit_table, sk_wg_of
-    B = len(lens)
-    bt = np.arange(B * 64, dtype=np.int32).reshape(B, 64)
-    tab = np.zeros((B * Hkv * 16 + 8, 4), dtype=np.int32)
-    TU = sk_unit_table(np.array(lens), bt, Hkv, bs, tab)
-    G = min(G, TU)         # the kernel's effective grid: every range non-empty
-    pieces = {}            # item -> list of (wg, slot)
-    whole = set()
-    for g in range(G):
-        s0, s1 = TU * g // G, TU * (g + 1) // G
-        n = s1 - s0
-        if n <= 0:
-            continue
-        ent = tab[s0:s1]
-        segs = []
-        for j in range(n):
-            if j == 0 or ent[j, 0] != ent[j - 1, 0]:
-                segs.append([int(ent[j, 0]), j])
-        NS = len(segs)
-        cut_head = ent[0, 1] > 0
-        xf_tail = s0 + (n - 1) - ent[n - 1, 1]
-        cut_tail = xf_tail + (ent[n - 1, 3] + 31) // 32 > s1
-        for j, (item, _) in enumerate(segs):
-            part = (j == 0 and cut_head) or (j == NS - 1 and cut_tail)
-            if part:
-                pieces.setdefault(item, []).append((g, 0 if j == 0 else 1))
-            else:
-                assert item not in whole
-                whole.add(item)
-    return TU, tab, pieces, whole, G
-
-
-def test_sk_unit_table_and_split_cover_every_item_once():
-    import random
-
-    from enterprise_inference_amd.ops.attention import sk_wg_of
-    rnd = random.Random(3)
-    for trial in range(60):
-        B = rnd.randint(1, 70)
-        Hkv = rnd.choice([1, 2, 8])
-        lens = [rnd.choice([0, 1, 31, 32, 33, 64, rnd.randint(1, 300)]) for _ in range(B)]
-        G = rnd.choice([1, 3, 37, 512])
-        TU, tab, pieces, whole, G = _sk_model(lens, Hkv, G)
-        assert TU == Hkv * sum((l + 31) // 32 for l in lens)
-        if TU > 8 * G or TU == 0:
-            continue
-        # table: item order, unit index, physical block, L
-        for x in range(TU):
-            item, u, blk, L = tab[x]
-            b = item // Hkv
-            assert L == lens[b] and 0 <= u < (L + 31) // 32 and blk == b * 64 + (u * 32) // 128
-        items = {i for i in range(B * Hkv) if lens[i // Hkv] > 0}
-        assert whole | set(pieces) == items and not (whole & set(pieces))
-        for item, ps in pieces.items():
-            # the kernel's piece count and merger slot rule agree with the producers
-            xf = int(next(x for x in range(TU) if tab[x, 0] == item))
-            U = (lens[item // Hkv] + 31) // 32
-            ga, gb = sk_wg_of(xf, TU, G), sk_wg_of(xf + U - 1, TU, G)
-            assert [g for g, _ in ps] == list(range(ga, gb + 1)) and len(ps) >= 2
-            slot_a = 1 if TU * ga // G != xf else 0
-            assert ps == [(g, slot_a if g == ga else 0) for g in range(ga, gb + 1)]
-        # at most 8 units per workgroup
-        if TU:
-            assert 1 <= min(TU * (g + 1) // G - TU * g // G for g in range(G))
-            assert max(TU * (g + 1) // G - TU * g // G for g in range(G)) <= 8
-
-
-def test_sk_unit_table_overflow_and_empty():
-    import numpy as np
-
-    from enterprise_inference_amd.ops.attention import sk_unit_table
-    out = np.zeros((4, 4), dtype=np.int32)
-    bt = np.zeros((2, 4), dtype=np.int32)
-    assert sk_unit_table(np.array([0, 0]), bt, 8, 128, out) == 0
-    assert sk_unit_table(np.array([100, 1]), bt, 8, 128, out) == -1     # 40 units > 4 rows
-
-
 def test_decode_partition_heuristic():
     """Context partitions per decode batch (ops/attention.py decode_partitions), pinned to the
     measured rows: short contexts never split; 1-2 items per CU split 4 ways when the items do
@@ -168,18 +85,3 @@ def test_decode_partition_heuristic():
     assert decode_partitions(16, 8, 32, 4096) == 2
     assert decode_partitions(1, 8, 32, 4096) == 8
 
-
-def test_addnorm_workspace_not_made_inside_capture(monkeypatch):
-    """The full-chip add+RMSNorm's shared workspace (row counters that must start at zero) is
-    never allocated inside graph capture: a capture that reaches it first falls back to the
-    row-per-workgroup kernel instead."""
-    import torch
-    from enterprise_inference_amd.ops import gemm
-    monkeypatch.setattr(gemm, "_ADDNORM_WS", {})
-    monkeypatch.setattr(torch.cuda, "is_current_stream_capturing", lambda: True)
-    assert gemm._addnorm_ws(torch.device("cpu"), 65, 4096) is None
-    assert gemm._ADDNORM_WS == {}
-    monkeypatch.setattr(torch.cuda, "is_current_stream_capturing", lambda: False)
-    ws = gemm._addnorm_ws(torch.device("cpu"), 65, 4096)
-    assert ws is not None and int(ws[1].abs().sum()) == 0 and ws[0].numel() >= 65 * 8
-    assert gemm._addnorm_ws(torch.device("cpu"), 129, 4096) is None      # > MAX_M rows

@@ -6,7 +6,6 @@ Run on an MI355X:  python -m pytest tests -m gpu
 import math
 import random
 
-import numpy as np
 import pytest
 import torch
 
@@ -505,78 +504,3 @@ def test_paged_prefill_fa_long_and_windowed(sw, ch):
     _close(o, r, 2e-2, 2e-2, f"prefill fa sw={sw} chunk={ch}")
 
 
-
-
-# ----------------------------------------------------------------------------- stream-K decode
-
-@pytest.mark.parametrize("Hq,Hkv,D,bs,bias,qkn,split", [
-    (32, 8, 128, 128, False, False, True),      # Llama-3-8B decode (split-K QKV)
-    (32, 8, 128, 128, False, False, False),
-    (28, 4, 128, 64, True, False, True),        # Qwen2 (bias)
-    (16, 8, 128, 32, False, True, True),        # Qwen3 (qk-norm)
-    (12, 12, 64, 32, True, True, False),
-    (64, 8, 128, 128, False, False, True)])     # 70B-like G = 8
-@pytest.mark.parametrize("B,maxlen,nwg", [(13, 250, 512), (65, 256, 512), (13, 250, 37),
-                                          (7, 120, 3), (30, 900, 64)])
-def test_decode_sk_matches_fused(Hq, Hkv, D, bs, bias, qkn, split, B, maxlen, nwg):
-    """Stream-K decode (csrc/kernels/attention_sk.hip) == the one-workgroup-per-item fused
-    kernel up to the merge order: same K/V cache writes, outputs within bf16 rounding; items
-    cut over 2..many workgroups (nwg 3 / 37 / 64) merged by the last arriver; counters left at
-    zero (two calls); graph padding rows (L = 0) carry no units."""
-    from enterprise_inference_amd.ops import attention, rotary
-    from enterprise_inference_amd.ops.gemm import SplitK
-    rnd = random.Random(B * 7 + nwg + D)
-    torch.manual_seed(B + nwg + Hq)
-    lens = [rnd.randint(1, maxlen) for _ in range(B)]
-    lens[0], lens[1] = 1, 64
-    if B > 5:
-        lens[2], lens[5] = 33, 0                                  # 33: two units; 0: padding
-    nbt = sum(math.ceil(max(l, 1) / bs) for l in lens) + 2
-    k1, v1 = _make_cache(nbt, Hkv, bs, D, fill=True)
-    bt = _random_tables([max(l, 1) for l in lens], bs, nbt).to(DEV)
-    sl = torch.tensor(lens, dtype=torch.int32, device=DEV)
-    pos = torch.tensor([max(l - 1, 0) for l in lens], dtype=torch.int32, device=DEV)
-    slots = torch.tensor([int(bt[i, (l - 1) // bs]) * bs + (l - 1) % bs if l > 0 else -1
-                          for i, l in enumerate(lens)], dtype=torch.int32, device=DEV)
-    N = (Hq + 2 * Hkv) * D
-    if split:
-        qkv = SplitK(torch.randn(4, B, N, device=DEV) * 0.5, 4, B, N, None)
-    else:
-        qkv = torch.randn(B, N, device=DEV, dtype=BF)
-    b = torch.randn(N, device=DEV, dtype=BF) if bias else None
-    qn = (torch.rand(D, device=DEV) + 0.5).to(BF) if qkn else None
-    kn = (torch.rand(D, device=DEV) + 0.5).to(BF) if qkn else None
-    rc = rotary.RotaryCache(D, 4096, 500000.0, None, DEV)
-    k2, v2 = k1.clone(), v1.clone()
-    G = Hq // Hkv
-    po = torch.empty(max(B * Hq * 8, nwg * 2 * G) * D, device=DEV)
-    pml = torch.empty(max(B * Hq * 8, nwg * 2 * G) * 2, device=DEV)
-    cnt = torch.zeros(B * Hkv, dtype=torch.int32, device=DEV)
-    tab = np.zeros((8 * nwg + 1, 4), dtype=np.int32)
-    TU = attention.sk_unit_table(np.array(lens), bt.cpu().numpy(), Hkv, bs, tab[1:])
-    if TU < 0:       # the table holds 8 units per workgroup: -1 = overflow
-        pytest.skip("more units than the stream-K grid takes (the runner uses the classic kernel)")
-    assert TU == Hkv * sum(math.ceil(l / 32) for l in lens)
-    tab[0, 0] = TU
-    dtab = torch.from_numpy(tab).to(DEV).view(-1)
-    md = attention.AttentionMetadata(num_decode=B, num_prefill_tokens=0, slot_mapping=slots,
-                                     positions=pos, decode_block_tables=bt, decode_seq_lens=sl,
-                                     decode_partitions=1, decode_part_o=po, decode_part_ml=pml,
-                                     decode_part_cnt=cnt)
-    o_ref = attention.decode_rope_attention(qkv, md, k2, v2, rc, Hq, Hkv, D, D ** -0.5, b, qn, kn,
-                                            1e-6)
-    md.decode_sk = (dtab[4:], dtab[0:1], nwg)
-    for _ in range(2):
-        k1c, v1c = k1.clone(), v1.clone()
-        o_sk = attention.decode_rope_attention(qkv, md, k1c, v1c, rc, Hq, Hkv, D, D ** -0.5, b, qn,
-                                               kn, 1e-6)
-        torch.cuda.synchronize()
-        assert int(cnt.abs().sum()) == 0, "arrival counters not reset"
-    if not (torch.equal(k1c, k2) and torch.equal(v1c, v2)):
-        dk = (k1c != k2).nonzero().tolist()[:8]
-        dv = (v1c != v2).nonzero().tolist()[:8]
-        owners = {int(s_) // bs: i for i, s_ in enumerate(slots.tolist()) if s_ >= 0}
-        raise AssertionError(f"K/V cache writes differ: k {dk} v {dv} TU {TU} "
-                             f"rows {[(owners.get(x[0]), lens[owners[x[0]]] if x[0] in owners else None) for x in dk + dv]}")
-    live = sl > 0
-    _close(o_sk[live], o_ref[live], 2e-2, 2e-2, f"stream-K B={B} nwg={nwg}")
