@@ -8,5 +8,5 @@ mkdir -p gpurun_out
 export PYTHONUNBUFFERED=1
 TAG=$1; shift
 timeout -k 10 1150 python scripts/sizing_sweep.py --model 70b --cases "$@" --timeout 540 \
-  --out gpurun_out/sizing_70b_$TAG.md > gpurun_out/sizing_70b_$TAG.log 2>&1
+  --out gpurun_out/sizing_70b_$TAG.md 2>&1 | tee gpurun_out/sizing_70b_$TAG.log
 rc=$?; cat gpurun_out/sizing_70b_$TAG.md; exit $rc

@@ -84,12 +84,32 @@ def main() -> int:
                    "--master-port", "29533"] + cmd[1:] + ["--tp", str(args.tp),
                                                            "--gpus", str(args.tp)]
         print(f"== {name}: {' '.join(cmd)}", flush=True)
-        p = subprocess.run(cmd, capture_output=True, text=True, timeout=args.timeout)
-        if p.returncode != 0:
-            print(p.stdout[-2000:], p.stderr[-4000:], flush=True)
-            print(f"{name} rc={p.returncode}", flush=True)
-            return p.returncode
-        js = [json.loads(ln) for ln in p.stdout.splitlines() if ln.startswith("{")]
+        # the child's output goes to files; a heartbeat line a minute keeps a long row (a 4096-
+        # token generation at 70B takes minutes) visibly alive to whatever watches this process
+        import tempfile
+        import time
+        with tempfile.TemporaryFile("w+") as out, tempfile.TemporaryFile("w+") as err:
+            p = subprocess.Popen(cmd, stdout=out, stderr=err, text=True)
+            t0 = time.time()
+            while True:
+                try:
+                    rc = p.wait(timeout=60)
+                    break
+                except subprocess.TimeoutExpired:
+                    if time.time() - t0 > args.timeout:
+                        p.kill()
+                        p.wait()
+                        rc = -9
+                        break
+                    print(f"   {name}: {time.time() - t0:.0f} s", flush=True)
+            out.seek(0)
+            err.seek(0)
+            stdout, stderr = out.read(), err.read()
+        if rc != 0:
+            print(stdout[-2000:], stderr[-4000:], flush=True)
+            print(f"{name} rc={rc}", flush=True)
+            return rc if rc > 0 else 1
+        js = [json.loads(ln) for ln in stdout.splitlines() if ln.startswith("{")]
         r = js[-1]
         results.append({"case": name, **r})
         ratio = r["value"] / ref_tps
