@@ -33,7 +33,9 @@
 // (65x128: 135 -> 174 TFLOP/s); fetching K/V two tiles ahead (+24 VGPRs) was slower at 1x8192
 // (800 vs 757 us) -- the one-tile-ahead fetch is not the bound there -- and a software
 // pipeline computing S of tile i+1 beside the exponentials of tile i (three LDS buffers, two S
-// register sets, 256 VGPRs) ran at 0.81x.
+// register sets, 256 VGPRs) ran at 0.81x, and running the two wave halves half a tile apart
+// (two raw barriers per tile, the younger half one slot behind, so one wave of each SIMD is in
+// its softmax while the other is in P.V) at 0.92-0.94x (profiles/prefill_attn_fa_r4.md).
 #include "eia_common.h"
 
 namespace {
