@@ -226,6 +226,7 @@ def core_main(fd: int) -> int:
                 if arr:
                     now = time.time()
                     lt["bursts"] = lt.get("bursts", 0) + 1
+                    lt["burst_reqs"] = lt.get("burst_reqs", 0) + len(arr)
                     lt["burst_spread"] = lt.get("burst_spread", 0.0) + (max(arr) - min(arr))
                     lt["burst_wait"] = lt.get("burst_wait", 0.0) + (now - min(arr))
             for msg in msgs:
