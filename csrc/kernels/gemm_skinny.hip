@@ -829,6 +829,21 @@ EIA_API int eia_moe_gemm(const void* X, long ldx, const void* W, long ldw, const
                            out, ldo, 0, N, K, 1, mode, experts, offs, row_idx, (long)N * ldw, st);
 }
 
+// Grouped GEMM with the K range split over grid.y (decode-sized MoE down projections, K = I):
+// fp32 slabs part[sk][rows][N] in expert-sorted row order, summed by eia_moe_combine_sk (the
+// combine reads every token's k rows anyway).  rows = total sorted rows (slab stride).
+EIA_API int eia_moe_gemm_sk(const void* X, long ldx, const void* W, long ldw, float* part,
+                            int rows, int N, int K, int experts, const int* offs,
+                            const int* row_idx, int mt_hint, int sk, int cfg, hipStream_t st) {
+  if (experts < 1 || sk < 1 || rows < 1 || (cfg & 240)) return EIA_BAD_SHAPE;
+  if (int rc = check_shape(N, K, sk, MODE_F32_SPLIT, cfg)) return rc;
+  if ((ldx % 8) || (ldw % 8)) return EIA_BAD_SHAPE;
+  const int mt = mt_hint < 1 ? 1 : (mt_hint > 8 ? 8 : mt_hint);
+  return dispatch_mt<true>(mt, cfg, static_cast<const bf16_t*>(X), ldx,
+                           static_cast<const bf16_t*>(W), ldw, nullptr, part, N, rows, N, K, sk,
+                           MODE_F32_SPLIT, experts, offs, row_idx, (long)N * ldw, st);
+}
+
 EIA_API int eia_splitk_reduce(const float* part, int sk, int M, int N, const void* bias, void* out,
                               long ldo, hipStream_t st) {
   if (N % 4 != 0) return EIA_BAD_SHAPE;

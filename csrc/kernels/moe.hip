@@ -191,6 +191,32 @@ combine_kernel(const bf16_t* __restrict__ y, long ldy, const float* __restrict__
   }
 }
 
+// combine over the fp32 split-K slabs of the down projection: out[t] = sum_s w[t,s] *
+// sum_j part[j][inv[t,s]] (slabs summed in order, then weighted like combine_kernel)
+__global__ void __launch_bounds__(256)
+combine_sk_kernel(const float* __restrict__ part, int sk, long slab, const float* __restrict__ w,
+                  const int* __restrict__ inv, int k, int H, bf16_t* __restrict__ out, long ldo) {
+  const int t = blockIdx.x;
+  for (int c = threadIdx.x * 4; c < H; c += blockDim.x * 4) {
+    f32x4 acc = (f32x4){0.f, 0.f, 0.f, 0.f};
+    for (int s = 0; s < k; ++s) {
+      const int pos = inv[(long)t * k + s];
+      if (pos < 0) continue;
+      const float ws = w[(long)t * k + s];
+      const float* p = part + (long)pos * H + c;
+      f32x4 v = *reinterpret_cast<const f32x4*>(p);
+      for (int j = 1; j < sk; ++j) v += *reinterpret_cast<const f32x4*>(p + j * slab);
+      // the unsplit GEMM rounds its output row to bf16 before the combine: same here
+#pragma unroll
+      for (int e = 0; e < 4; ++e) acc[e] += ws * bf2f(f2bf(v[e]));
+    }
+    bf16x4 o;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) o[e] = f2bf(acc[e]);
+    *reinterpret_cast<bf16x4*>(out + (long)t * ldo + c) = o;
+  }
+}
+
 }  // namespace
 
 EIA_API int eia_moe_topk(const void* logits, int is_bf16, int T, int E, int k, int renorm,
@@ -235,5 +261,14 @@ EIA_API int eia_moe_combine(const void* y, long ldy, const float* w, const int* 
   if (T == 0) return EIA_OK;
   hipLaunchKernelGGL(combine_kernel, dim3(T), dim3(256), 0, st, static_cast<const bf16_t*>(y), ldy,
                      w, inv, k, H, static_cast<bf16_t*>(out), ldo);
+  EIA_LAUNCH_CHECK();
+}
+
+EIA_API int eia_moe_combine_sk(const float* part, int sk, int rows, const float* w, const int* inv,
+                               int T, int k, int H, void* out, long ldo, hipStream_t st) {
+  if (H % 4 != 0 || (ldo % 4) || sk < 1 || rows < 1) return EIA_BAD_SHAPE;
+  if (T == 0) return EIA_OK;
+  hipLaunchKernelGGL(combine_sk_kernel, dim3(T), dim3(256), 0, st, part, sk, (long)rows * H, w,
+                     inv, k, H, static_cast<bf16_t*>(out), ldo);
   EIA_LAUNCH_CHECK();
 }

@@ -57,6 +57,8 @@ _SIGNATURES = {
     "eia_moe_route": [P, L, P, I, I, I, I, I, I, P, P, S],
     "eia_moe_gemm": [P, L, P, L, P, P, L, I, I, I, P, P, I, I, I, S],
     "eia_moe_combine": [P, L, P, P, I, I, I, P, L, S],
+    "eia_moe_gemm_sk": [P, L, P, L, P, I, I, I, I, P, P, I, I, I, S],
+    "eia_moe_combine_sk": [P, I, I, P, P, I, I, I, P, L, S],
     "eia_moe_grouped_gemm": [P, L, IP, P, I, I, I, IP, I, I, P, L, S],
     "eia_gemm_skinny": [P, L, P, L, P, P, L, I, I, I, I, I, I, S],
     "eia_splitk_reduce": [P, I, I, I, P, P, L, S],

@@ -37,6 +37,8 @@ SCORING = {"softmax": 0, "sigmoid": 1}
 # -1 = the shape rule below.  Overrides for tuning runs.
 UP_CFG = int(os.environ.get("EIA_MOE_UP_CFG", "-1"))
 DOWN_CFG = int(os.environ.get("EIA_MOE_DOWN_CFG", "-1"))
+# K split of the decode-sized down projection (K = I): fp32 slabs summed by the combine
+DOWN_SK = int(os.environ.get("EIA_MOE_DOWN_SK", "1"))
 
 def topk_route(logits: torch.Tensor, k: int, renormalize: bool = True,
                scoring: str = "softmax") -> Tuple[torch.Tensor, torch.Tensor]:
@@ -136,6 +138,15 @@ def _fused_moe_grouped(x, w13, w2, topk_w, topk_ids, e_lo, e_hi, mfma: bool = Fa
         check(lib().eia_moe_gemm(ptr(x), x.stride(0), ptr(w13), w13.stride(1), None, ptr(h1),
                                  h1.stride(0), I2, H, El, ptr(offs), ptr(row_idx), mt, 2,
                                  up_cfg, st), "moe_gemm_gate_up")
+        if DOWN_SK > 1 and I % (DOWN_SK * 256) == 0:
+            part = torch.empty(DOWN_SK, max(1, n), H, dtype=torch.float32, device=dev)
+            check(lib().eia_moe_gemm_sk(ptr(h1), h1.stride(0), ptr(w2), w2.stride(1), ptr(part),
+                                        max(1, n), H, I, El, ptr(offs), None, mt, DOWN_SK,
+                                        down_cfg, st), "moe_gemm_down_sk")
+            out = torch.empty(T, H, dtype=x.dtype, device=dev)
+            check(lib().eia_moe_combine_sk(ptr(part), DOWN_SK, max(1, n), ptr(topk_w), ptr(inv),
+                                           T, k, H, ptr(out), out.stride(0), st), "moe_combine_sk")
+            return out
         check(lib().eia_moe_gemm(ptr(h1), h1.stride(0), ptr(w2), w2.stride(1), None, ptr(h2),
                                  h2.stride(0), H, I, El, ptr(offs), None, mt, 0,
                                  down_cfg, st), "moe_gemm_down")

@@ -43,6 +43,29 @@ def test_fused_moe_grouped(T, E, k, H, I):
     assert err.max() < 3e-2 + 3e-2 * r.float().abs().max(), err.max()
 
 
+@pytest.mark.parametrize("sk", [2, 4])
+@pytest.mark.parametrize("T,E,k,H,I", [(1, 8, 2, 512, 1024), (65, 8, 2, 4096, 2048),
+                                       (33, 16, 1, 1024, 1024)])
+def test_fused_moe_down_splitk(monkeypatch, sk, T, E, k, H, I):
+    """Decode MoE with the down projection split over K (eia_moe_gemm_sk, fp32 slabs summed by
+    eia_moe_combine_sk) == the unsplit path up to bf16 rounding, and vs the fp32 reference."""
+    from enterprise_inference_amd.ops import moe
+    torch.manual_seed(T + sk)
+    x = torch.randn(T, H, device=DEV, dtype=BF)
+    w13 = (torch.randn(E, 2 * I, H, device=DEV) * H ** -0.5).to(BF)
+    w2 = (torch.randn(E, H, I, device=DEV) * I ** -0.5).to(BF)
+    w, ids = moe.topk_route(torch.randn(T, E, device=DEV), k, True)
+    monkeypatch.setattr(moe, "DOWN_SK", 1)
+    base = moe.fused_moe(x, w13, w2, w, ids)
+    monkeypatch.setattr(moe, "DOWN_SK", sk)
+    out = moe.fused_moe(x, w13, w2, w, ids)
+    r = ref.fused_moe(x.cpu(), w13.cpu(), w2.cpu(), w.cpu(), ids.cpu())
+    err = (out.float().cpu() - r.float()).abs()
+    assert err.max() < 3e-2 + 3e-2 * r.float().abs().max(), err.max()
+    d = (out.float() - base.float()).abs().max().item()
+    assert d <= 2e-2 * base.float().abs().max().item() + 1e-2, d
+
+
 @pytest.mark.parametrize("T", [40, 600])
 def test_fused_moe_expert_parallel_slices_sum(T):
     from enterprise_inference_amd.ops import moe
