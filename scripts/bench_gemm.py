@@ -7,7 +7,9 @@ Cache, so each call streams its weights from HBM.  Variants are timed in
 interleaved rounds in one process (guide §5.4 rule 24).
 
   --tune  sweeps (cfg, split-K) per (M-tile bucket, N, K) and writes the winners to
-          enterprise_inference_amd/ops/gemm_tuning.json (read by ops/gemm.py).
+          enterprise_inference_amd/ops/gemm_tuning.json (read by ops/gemm.py).  Several --m
+          values in one 16-row bucket are scored together: the bucket's pick is the variant with
+          the least summed time over those rows (e.g. --m 1 8 16 17 24 32 ...).
 """
 import argparse
 import json
@@ -113,6 +115,7 @@ def main():
         pool = max(2, int(600e6 // wbytes) + 1)
         ws = [(torch.randn(N, K, device="cuda") * 0.02).to(torch.bfloat16) for _ in range(pool)]
         wps = [gemm.pack_weight(w) for w in ws] if a.packed else ws
+        buckets = {}   # --tune: m-tile bucket -> summed times over its --m rows
         for M in a.m:
             x = torch.randn(M, K, device="cuda", dtype=torch.bfloat16)
             if swiglu:
@@ -164,11 +167,23 @@ def main():
                 r["regret_pct"] = round(100.0 * (tp / min(to, tb) - 1.0), 1)
             print(json.dumps(r), flush=True)
             if a.tune:
-                results = [r_ for r_ in results if r_[1] != "balanced"] or results
-                to, cfg, sk = results[0]
-                key = f"{gemm.m_bucket(M)},{N},{K},{int(swiglu)}"
-                # cfg -1 = "use hipBLASLt" (the skinny kernel lost on this shape)
-                tuned[key] = [cfg, sk] if to < tb * 1.02 else [-1, 1]
+                b = buckets.setdefault(gemm.m_bucket(M), {"rows": [], "hip": 0.0, "var": {}})
+                b["rows"].append(M)
+                b["hip"] += tb
+                for t, c, s_ in results:
+                    e = b["var"].setdefault((c, s_), [0.0, 0])
+                    e[0] += t
+                    e[1] += 1
+        for mt, b in sorted(buckets.items()):
+            # only variants valid (spill-free) at every row of the bucket compete
+            full = sorted((v[0], c) for c, v in b["var"].items() if v[1] == len(b["rows"]))
+            to, (cfg, sk) = full[0]
+            key = f"{mt},{N},{K},{int(swiglu)}"
+            # cfg -1 = "use hipBLASLt" (the skinny kernel lost on this shape)
+            tuned[key] = [cfg, sk] if to < b["hip"] * 1.02 else [-1, 1]
+            print(json.dumps({"shape": name, "bucket": mt, "rows": b["rows"], "pick": tuned[key],
+                              "sum_us": round(to, 2), "hipblaslt_sum_us": round(b["hip"], 2),
+                              "runner_up": [(round(t, 1), c) for t, c in full[1:3]]}), flush=True)
         del ws, wps
         torch.cuda.empty_cache()
     if a.tune:
