@@ -5,7 +5,10 @@ A decode step ends at the sampler's merge kernel; the last N complete steps are 
 launches per step, kernel time per step, step span (first start -> last end) and the busy
 fraction (kernel time / span), then the per-kernel time per step.
 
-Usage: analyze_steps.py <kernel_trace.csv> [title] [steps] [end_kernel_substring]
+Usage: analyze_steps.py <kernel_trace.csv> [title] [steps] [end_kernel_substring] [last|longest]
+
+``longest`` averages the N steps with the most kernel time instead of the last N (the prefill
+steps of a burst round).
 """
 import collections
 import csv
@@ -26,6 +29,7 @@ def main() -> int:
     title = sys.argv[2] if len(sys.argv) > 2 else path
     nsteps = int(sys.argv[3]) if len(sys.argv) > 3 else 30
     marker = sys.argv[4] if len(sys.argv) > 4 else "sample_merge"
+    pick = sys.argv[5] if len(sys.argv) > 5 else "last"
     rows = sorted(csv.DictReader(open(path)), key=lambda r: int(r["Start_Timestamp"]))
     ends = [i for i, r in enumerate(rows) if marker in r["Kernel_Name"]]
     if len(ends) < 2:
@@ -33,6 +37,11 @@ def main() -> int:
         return 1
     nsteps = min(nsteps, len(ends) - 1)
     pairs = list(zip(ends[-nsteps - 1:-1], ends[-nsteps:]))
+    if pick == "longest":
+        def ktime(ab):
+            return sum(int(r["End_Timestamp"]) - int(r["Start_Timestamp"])
+                       for r in rows[ab[0] + 1:ab[1] + 1])
+        pairs = sorted(zip(ends[:-1], ends[1:]), key=ktime)[-nsteps:]
     agg = collections.defaultdict(list)
     spans, busy, launches = [], [], []
     for a, b in pairs:
@@ -48,7 +57,7 @@ def main() -> int:
     n = len(pairs)
     span, kern = sum(spans) / n, sum(busy) / n
     print(f"### {title}\n")
-    print(f"Last {n} decode steps: {sum(launches) / n:.0f} launches/step, kernel time "
+    print(f"{'Last' if pick != 'longest' else 'Longest'} {n} steps: {sum(launches) / n:.0f} launches/step, kernel time "
           f"{kern / 1e3:.3f} ms/step, span {span / 1e3:.3f} ms/step, busy {100 * kern / span:.1f} %\n")
     print("| kernel | launches/step | µs/step | % of kernel time | avg µs |")
     print("|---|---:|---:|---:|---:|")
