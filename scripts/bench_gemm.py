@@ -72,6 +72,18 @@ def graph_time(fn, iters, rounds=3):
     return best   # us per call
 
 
+def bucket_pick(b, margin=1.02):
+    """A bucket's table entry from its summed timings: ``b`` = {"rows": [M...], "hip": summed
+    hipBLASLt us, "var": {(cfg, sk): [summed us, rows timed]}}.  Only variants timed (valid,
+    spill-free) at every row compete; [-1, 1] (hipBLASLt) unless the best skinny variant is
+    within ``margin`` of it.  Returns (entry, best summed us, sorted [(us, (cfg, sk))])."""
+    full = sorted((v[0], c) for c, v in b["var"].items() if v[1] == len(b["rows"]))
+    if not full:
+        return [-1, 1], b["hip"], full
+    to, (cfg, sk) = full[0]
+    return ([cfg, sk] if to < b["hip"] * margin else [-1, 1]), to, full
+
+
 def candidates(M, N, K, swiglu):
     out = []
     for cfg in gemm.CFGS:
@@ -175,12 +187,8 @@ def main():
                     e[0] += t
                     e[1] += 1
         for mt, b in sorted(buckets.items()):
-            # only variants valid (spill-free) at every row of the bucket compete
-            full = sorted((v[0], c) for c, v in b["var"].items() if v[1] == len(b["rows"]))
-            to, (cfg, sk) = full[0]
             key = f"{mt},{N},{K},{int(swiglu)}"
-            # cfg -1 = "use hipBLASLt" (the skinny kernel lost on this shape)
-            tuned[key] = [cfg, sk] if to < b["hip"] * 1.02 else [-1, 1]
+            tuned[key], to, full = bucket_pick(b)
             print(json.dumps({"shape": name, "bucket": mt, "rows": b["rows"], "pick": tuned[key],
                               "sum_us": round(to, 2), "hipblaslt_sum_us": round(b["hip"], 2),
                               "runner_up": [(round(t, 1), c) for t, c in full[1:3]]}), flush=True)

@@ -1,0 +1,35 @@
+"""scripts/bench_gemm.py bucket scoring (round 4): a 16-row bucket's table entry is the variant
+with the least summed time over the bucket's timed rows, among variants timed at all of them;
+hipBLASLt ([-1, 1]) wins unless the best skinny variant is within 2 %."""
+import importlib.util
+import os
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _mod():
+    spec = importlib.util.spec_from_file_location("bench_gemm",
+                                                  os.path.join(ROOT, "scripts", "bench_gemm.py"))
+    m = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(m)
+    return m
+
+
+def test_bucket_pick_sums_rows_and_skips_partial_variants():
+    bp = _mod().bucket_pick
+    b = {"rows": [49, 56, 64], "hip": 150.0,
+         "var": {(3, 8): [140.0, 3],        # best over all three rows
+                 (2, 2): [90.0, 2],         # fastest sum but spills at one row: not eligible
+                 (22, 8): [141.0, 3]}}
+    entry, to, full = bp(b)
+    assert entry == [3, 8] and to == 140.0
+    assert [c for _, c in full] == [(3, 8), (22, 8)]
+
+
+def test_bucket_pick_routes_to_hipblaslt():
+    bp = _mod().bucket_pick
+    b = {"rows": [17, 24, 32], "hip": 100.0, "var": {(24, 1): [103.0, 3]}}
+    assert bp(b)[0] == [-1, 1]
+    b["var"][(24, 1)][0] = 101.0                  # within the 2 % margin: keep the skinny kernel
+    assert bp(b)[0] == [24, 1]
+    assert bp({"rows": [1], "hip": 5.0, "var": {}})[0] == [-1, 1]
