@@ -96,3 +96,15 @@ def test_rope_cache_accepts_splitk_on_cpu():
         outs.append((q, kc, vc))
     for a, b in zip(*outs):
         assert torch.equal(a, b)
+
+
+def test_grouped_moe_cfg_spill_fallback():
+    """ops/moe.py moe_cfgs: the 3-stage grouped forms only where eia_moe_gemm accepts them
+    (spill-free: <= 2 row tiles, cfg 5 only at 1), else their 2-stage twins; defaults by shape."""
+    from enterprise_inference_amd.ops.moe import moe_cfgs
+    assert moe_cfgs(2, 14336, 4096) == (3, 2)
+    assert moe_cfgs(2, 14336, 4096, 7, 6) == (7, 6)
+    assert moe_cfgs(3, 14336, 4096, 7, 6) == (3, 2)
+    assert moe_cfgs(1, 14336, 4096, 5, 4) == (5, 4)
+    assert moe_cfgs(2, 14336, 4096, 5, 4) == (1, 4)
+    assert moe_cfgs(1, 100, 100) == (1, 0)
