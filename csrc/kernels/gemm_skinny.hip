@@ -624,17 +624,14 @@ int launch_mt(int cfg, const bf16_t* X, long ldx, const bf16_t* W, long ldw, con
   return launch_cfg<MT, NT_, W_, S_, GROUPED, KC_>(X, ldx, W, ldw, bias, out, ldo, M, N, K, sk, \
                                                    mode, experts, offs, row_idx, w_estride, st)
   // cfg = (NT - 1) | ((WAVES / 2 - 1) << 1) | ((S - 2) << 2) | (KC == 128 ? 16 : 0);
-  // grouped (MoE) uses KC = 256, S = 2 (cfg 0-3) or 3 (cfg 4-7, spill-free at MT <= 2)
+  // grouped (MoE) uses S = 2, KC = 256 (3-stage forms measured neutral at Mixtral decode,
+  // profiles/moe_s3_ab_r4.log)
   if constexpr (GROUPED) {
-    switch (cfg & 7) {
+    switch (cfg & 3) {
       case 0: EIA_CFG(1, 2, 2, 256);
       case 1: EIA_CFG(2, 2, 2, 256);
       case 2: EIA_CFG(1, 4, 2, 256);
-      case 3: EIA_CFG(2, 4, 2, 256);
-      case 4: EIA_CFG(1, 2, 3, 256);
-      case 5: EIA_CFG(2, 2, 3, 256);
-      case 6: EIA_CFG(1, 4, 3, 256);
-      default: EIA_CFG(2, 4, 3, 256);
+      default: EIA_CFG(2, 4, 2, 256);
     }
   } else {
     if (cfg & 128) {   // LDS-DMA ring: cfg = 128|16|2 | (NT-1) | (D-2)<<2 | packed<<6
@@ -830,12 +827,10 @@ EIA_API int eia_gemm_skinny(const void* X, long ldx, const void* W, long ldw, co
 EIA_API int eia_moe_gemm(const void* X, long ldx, const void* W, long ldw, const void* bias,
                          void* out, long ldo, int N, int K, int experts, const int* offs,
                          const int* row_idx, int mt_hint, int mode, int cfg, hipStream_t st) {
-  if (experts < 1 || mode == MODE_F32_SPLIT || (cfg & 248)) return EIA_BAD_SHAPE;
+  if (experts < 1 || mode == MODE_F32_SPLIT || (cfg & 252)) return EIA_BAD_SHAPE;
   if (int rc = check_shape(N, K, 1, mode, cfg)) return rc;
   if ((ldx % 8) || (ldw % 8) || (ldo % 4)) return EIA_BAD_SHAPE;
   const int mt = mt_hint < 1 ? 1 : (mt_hint > 8 ? 8 : mt_hint);
-  // 3-stage forms: spill-free at MT <= 2 except (NT 2, 2 waves) at MT 2
-  if ((cfg & 4) && (mt > 2 || (cfg == 5 && mt == 2))) return EIA_BAD_SHAPE;
   return dispatch_mt<true>(mt, cfg, static_cast<const bf16_t*>(X), ldx,
                            static_cast<const bf16_t*>(W), ldw, static_cast<const bf16_t*>(bias),
                            out, ldo, 0, N, K, 1, mode, experts, offs, row_idx, (long)N * ldw, st);
@@ -847,11 +842,10 @@ EIA_API int eia_moe_gemm(const void* X, long ldx, const void* W, long ldw, const
 EIA_API int eia_moe_gemm_sk(const void* X, long ldx, const void* W, long ldw, float* part,
                             int rows, int N, int K, int experts, const int* offs,
                             const int* row_idx, int mt_hint, int sk, int cfg, hipStream_t st) {
-  if (experts < 1 || sk < 1 || rows < 1 || (cfg & 248)) return EIA_BAD_SHAPE;
+  if (experts < 1 || sk < 1 || rows < 1 || (cfg & 252)) return EIA_BAD_SHAPE;
   if (int rc = check_shape(N, K, sk, MODE_F32_SPLIT, cfg)) return rc;
   if ((ldx % 8) || (ldw % 8)) return EIA_BAD_SHAPE;
   const int mt = mt_hint < 1 ? 1 : (mt_hint > 8 ? 8 : mt_hint);
-  if ((cfg & 4) && (mt > 2 || (cfg == 5 && mt == 2))) return EIA_BAD_SHAPE;
   return dispatch_mt<true>(mt, cfg, static_cast<const bf16_t*>(X), ldx,
                            static_cast<const bf16_t*>(W), ldw, nullptr, part, N, rows, N, K, sk,
                            MODE_F32_SPLIT, experts, offs, row_idx, (long)N * ldw, st);

@@ -33,23 +33,21 @@ from ._dispatch import check, lib, ptr, stream, use_hip
 SCORING = {"softmax": 0, "sigmoid": 1}
 
 
-# grouped skinny GEMM configurations (csrc/kernels/gemm_skinny.hip cfg bits: NT-1 |
-# (WAVES/2-1)<<1 | (S-2)<<2, S = weight pipeline stages); -1 = the shape rule in moe_cfgs.
-# Overrides for tuning runs.
+# grouped skinny GEMM configurations (csrc/kernels/gemm_skinny.hip cfg bits: NT-1 | (WAVES/2-1)<<1);
+# -1 = the shape rule in moe_cfgs.  Overrides for tuning runs.  (3-stage weight pipelines were
+# measured neutral at Mixtral decode and are not built for the grouped kernel:
+# profiles/moe_s3_ab_r4.log.)
 UP_CFG = int(os.environ.get("EIA_MOE_UP_CFG", "-1"))
 DOWN_CFG = int(os.environ.get("EIA_MOE_DOWN_CFG", "-1"))
 
 
-def moe_cfgs(mt: int, I: int, H: int, up: int = -1, down: int = -1) -> Tuple[int, int]:
-    """(gate_up cfg, down cfg) of the grouped expert GEMMs at ``mt`` 16-row tiles per pass.
-    The 3-stage forms (cfg bit 2) are spill-free only up to 2 tiles (cfg 5 only at 1), as
-    eia_moe_gemm enforces: above that a requested 3-stage form falls back to its 2-stage twin."""
-    u = up if up >= 0 else (3 if I % 64 == 0 else 1)
-    d = down if down >= 0 else (2 if H % 128 == 0 else 0)
-
-    def ok(c):
-        return not (c & 4) or (mt <= 2 and not (c == 5 and mt == 2))
-    return (u if ok(u) else u & 3), (d if ok(d) else d & 3)
+def moe_cfgs(I: int, H: int, up: int = -1, down: int = -1) -> Tuple[int, int]:
+    """(gate_up cfg, down cfg) of the grouped expert GEMMs: 4-wave workgroups where the shape
+    divides (two 16-row tiles per wave for the SwiGLU pairs), else 2-wave; overrides kept to
+    the four grouped forms (cfg 0-3)."""
+    u = up & 3 if up >= 0 else (3 if I % 64 == 0 else 1)
+    d = down & 3 if down >= 0 else (2 if H % 128 == 0 else 0)
+    return u, d
 # K split of the decode-sized down projection (K = I): fp32 slabs summed by the combine.
 # Mixtral-8x7B at 65 users: TPOT 20.33 -> 19.52 ms at 2 (19.60 at 4), engine 2991 -> 3105 tok/s
 # (profiles/moe_down_sk_r4.log): twice the workgroups keep twice the weight bytes in flight.
@@ -148,7 +146,7 @@ def _fused_moe_grouped(x, w13, w2, topk_w, topk_ids, e_lo, e_hi, mfma: bool = Fa
               "moe_grouped_gemm_down")
     else:
         mt = max(1, min(8, -(-int(1.5 * n / El + 1) // 16)))
-        up_cfg, down_cfg = moe_cfgs(mt, I, H, UP_CFG, DOWN_CFG)
+        up_cfg, down_cfg = moe_cfgs(I, H, UP_CFG, DOWN_CFG)
         check(lib().eia_moe_gemm(ptr(x), x.stride(0), ptr(w13), w13.stride(1), None, ptr(h1),
                                  h1.stride(0), I2, H, El, ptr(offs), ptr(row_idx), mt, 2,
                                  up_cfg, st), "moe_gemm_gate_up")

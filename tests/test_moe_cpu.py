@@ -98,13 +98,11 @@ def test_rope_cache_accepts_splitk_on_cpu():
         assert torch.equal(a, b)
 
 
-def test_grouped_moe_cfg_spill_fallback():
-    """ops/moe.py moe_cfgs: the 3-stage grouped forms only where eia_moe_gemm accepts them
-    (spill-free: <= 2 row tiles, cfg 5 only at 1), else their 2-stage twins; defaults by shape."""
+def test_grouped_moe_cfgs():
+    """ops/moe.py moe_cfgs: 4-wave forms where the shape divides, overrides masked to the four
+    grouped forms the kernel builds (cfg 0-3)."""
     from enterprise_inference_amd.ops.moe import moe_cfgs
-    assert moe_cfgs(2, 14336, 4096) == (3, 2)
-    assert moe_cfgs(2, 14336, 4096, 7, 6) == (7, 6)
-    assert moe_cfgs(3, 14336, 4096, 7, 6) == (3, 2)
-    assert moe_cfgs(1, 14336, 4096, 5, 4) == (5, 4)
-    assert moe_cfgs(2, 14336, 4096, 5, 4) == (1, 4)
-    assert moe_cfgs(1, 100, 100) == (1, 0)
+    assert moe_cfgs(14336, 4096) == (3, 2)
+    assert moe_cfgs(100, 100) == (1, 0)
+    assert moe_cfgs(14336, 4096, 7, 6) == (3, 2)
+    assert moe_cfgs(14336, 4096, 1, 0) == (1, 0)
