@@ -583,7 +583,8 @@ int launch_cfg(const bf16_t* X, long ldx, const bf16_t* W, long ldw, const bf16_
     return e != nullptr ? atoi(e) : -1;
   }();
   const int rot_mul = rot_env >= 0 ? rot_env : (sk == 1 ? 3 : 0);
-  // grouped (MoE) expert GEMMs: the same stagger, split or not -- Mixtral decode MoE layer
+  // grouped (MoE) expert GEMMs: the same stagger, split or not, on walks of >= 8 chunks (the
+  // long streams it is for; short walks keep the plain order) -- Mixtral decode MoE layer
   // 528 -> 512 us, engine TPOT 19.59 -> 19.27 ms (profiles/moe_rot_ab_r4.log); EIA_MOE_ROT=0 off
   static const int moe_rot = [] {
     const char* e = getenv("EIA_MOE_ROT");
@@ -592,7 +593,7 @@ int launch_cfg(const bf16_t* X, long ldx, const bf16_t* W, long ldw, const bf16_
   dim3 grid(mode == MODE_SWIGLU ? (N / 2) / (WAVES * 16) : N / (WAVES * NT * 16), sk, experts);
   hipLaunchKernelGGL((gemm_skinny_kernel<MT, NT, WAVES, S, GROUPED, KC, LOADER, PACKED>), grid, dim3(WAVES * 64 + (LOADER ? 64 : 0)), lds, st,
                      X, ldx, W, ldw, bias, out, ldo, M, N, K / sk, mode, N / 2, offs, row_idx,
-                     w_estride, GROUPED ? moe_rot : rot_mul);
+                     w_estride, GROUPED ? ((K / sk) / KC >= 8 ? moe_rot : 0) : rot_mul);
   return (int)hipGetLastError();
 }
 
