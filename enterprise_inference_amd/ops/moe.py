@@ -50,8 +50,9 @@ def moe_cfgs(I: int, H: int, up: int = -1, down: int = -1) -> Tuple[int, int]:
     return u, d
 # K split of the decode-sized down projection (K = I): fp32 slabs summed by the combine.
 # Mixtral-8x7B at 65 users: TPOT 20.33 -> 19.52 ms at 2 (19.60 at 4), engine 2991 -> 3105 tok/s
-# (profiles/moe_down_sk_r4.log): twice the workgroups keep twice the weight bytes in flight.
-DOWN_SK = int(os.environ.get("EIA_MOE_DOWN_SK", "2"))
+# (profiles/moe_down_sk_r4.log): more workgroups keep more weight bytes in flight.  With the
+# staggered K walk on, 4 edges out 2: TPOT 19.26 vs 19.32 ms in two pairs (moe_sk_ab2_r4.log).
+DOWN_SK = int(os.environ.get("EIA_MOE_DOWN_SK", "4"))
 
 def topk_route(logits: torch.Tensor, k: int, renormalize: bool = True,
                scoring: str = "softmax") -> Tuple[torch.Tensor, torch.Tensor]:
