@@ -129,12 +129,29 @@ def _pinned_request(url: str, ip):
     return urlunparse(u._replace(netloc=netloc)), {"Host": hdr_host}, ext
 
 
+def _proxy_for(url: str) -> Optional[str]:
+    """The egress proxy the environment configures for ``url`` (HTTP(S)_PROXY / ALL_PROXY,
+    honouring NO_PROXY against the host NAME), or None for a direct connection."""
+    import urllib.request
+    from urllib.parse import urlparse
+
+    u = urlparse(url)
+    proxies = urllib.request.getproxies()
+    proxy = proxies.get(u.scheme) or proxies.get("all")
+    if not proxy or urllib.request.proxy_bypass(u.hostname or ""):
+        return None
+    return proxy
+
+
 @contextlib.contextmanager
-def _open_stream(url: str, headers: dict, extensions: dict, timeout: float):
-    """One streamed GET (no redirect following) with per-request transport extensions."""
+def _open_stream(url: str, headers: dict, extensions: dict, timeout: float,
+                 trust_env: bool = False):
+    """One streamed GET (no redirect following) with per-request transport extensions.
+    ``trust_env`` False (the pinned, direct form) ignores HTTP(S)_PROXY: the connection must go
+    to the address the policy check validated, not to a proxy."""
     import httpx
 
-    with httpx.Client(timeout=timeout, follow_redirects=False) as client:
+    with httpx.Client(timeout=timeout, follow_redirects=False, trust_env=trust_env) as client:
         req = client.build_request("GET", url, headers=headers, extensions=extensions)
         r = client.send(req, stream=True)
         try:
@@ -154,9 +171,17 @@ def fetch_image_bytes(url: str, max_bytes: Optional[int] = None, timeout: float 
     cap = MAX_IMAGE_BYTES if max_bytes is None else max_bytes
     for _ in range(5):
         ip = _check_url(url)
-        target, headers, ext = (url, {}, {}) if ip is None else _pinned_request(url, ip)
-        with _open_stream(target, headers, ext, timeout) as r:
-            if ip is not None:      # defence in depth: the peer really is the checked address
+        # Behind an egress proxy (enterprise clusters) the proxy dials the origin: the request
+        # carries the NAME (our own resolution above still applied the policy) and the peer
+        # is the proxy, so neither the pin nor the peer check applies.  Direct fetches dial
+        # the validated address with the environment's proxy settings ignored.
+        proxied = ip is not None and _proxy_for(url) is not None
+        if ip is None or proxied:
+            target, headers, ext = url, {}, {}
+        else:
+            target, headers, ext = _pinned_request(url, ip)
+        with _open_stream(target, headers, ext, timeout, trust_env=ip is None or proxied) as r:
+            if ip is not None and not proxied:   # defence in depth: peer is the checked address
                 stream = r.extensions.get("network_stream")
                 peer = stream.get_extra_info("server_addr") if stream is not None else None
                 if peer and ipaddress.ip_address(str(peer[0]).split("%")[0]) != ip:

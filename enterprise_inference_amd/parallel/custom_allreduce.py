@@ -30,6 +30,7 @@ from __future__ import annotations
 import ctypes
 import logging
 import os
+import time
 from typing import List, Optional
 
 import torch
@@ -332,23 +333,36 @@ def run_self_test(ar, reference, device, cases=None, eps: float = 1e-5) -> Optio
     bad = []
     for case in cases if cases is not None else selftest_cases(ar.max_bytes, ar.oneshot_max):
         op, shape, kind = case
-        t = selftest_inputs(case, ar.rank, device)
-        if op == "ar":
-            want = reference(t[0].clone())
-            got = ar.all_reduce(t[0].clone(), kind=kind)
-            ok = torch.equal(got, want)
-            err = 0.0 if ok else float((got.float() - want.float()).abs().max())
-        else:
-            x, res, w = t
-            s = reference(x.clone())
-            r_want = res.clone()
-            want, r_want = norm_ops.fused_add_rms_norm(s, r_want, w, eps)
-            r_got = res.clone()
-            got = ar.add_rmsnorm(x.clone(), r_got, w, eps, twoshot=bool(kind))
-            ok = torch.equal(r_got, r_want) and bool(
-                torch.allclose(got.float(), want.float(), rtol=1e-2, atol=1e-2))
-            err = 0.0 if ok else max(float((r_got.float() - r_want.float()).abs().max()),
-                                     float((got.float() - want.float()).abs().max()))
+        # Every rank runs the SAME collectives in the same order whatever fails locally: a
+        # rank that left the loop early would strand its peers in the next case's RCCL
+        # reference.  A local failure skips only this rank's custom call (its
+        # peers' custom kernel then spins out and sets their error flag, which is checked below).
+        try:
+            t = selftest_inputs(case, ar.rank, device)
+        except Exception as e:   # noqa: BLE001
+            bad.append(f"{op} {tuple(shape)} inputs raised {e!r}")
+            t = (torch.zeros(shape, dtype=torch.bfloat16, device=device),)
+        want = reference(t[0].clone())
+        if len(t) == 1 and op != "ar":
+            continue
+        try:
+            if op == "ar":
+                got = ar.all_reduce(t[0].clone(), kind=kind)
+                ok = torch.equal(got, want)
+                err = 0.0 if ok else float((got.float() - want.float()).abs().max())
+            else:
+                x, res, w = t
+                r_want = res.clone()
+                want, r_want = norm_ops.fused_add_rms_norm(want, r_want, w, eps)
+                r_got = res.clone()
+                got = ar.add_rmsnorm(x.clone(), r_got, w, eps, twoshot=bool(kind))
+                ok = torch.equal(r_got, r_want) and bool(
+                    torch.allclose(got.float(), want.float(), rtol=1e-2, atol=1e-2))
+                err = 0.0 if ok else max(float((r_got.float() - r_want.float()).abs().max()),
+                                         float((got.float() - want.float()).abs().max()))
+        except Exception as e:   # noqa: BLE001 - recorded; the loop goes on in step
+            bad.append(f"{op}/{'2shot' if kind else '1shot'} {tuple(shape)} raised {e!r}")
+            continue
         if not ok:
             bad.append(f"{op}{'/2shot' if kind else '/1shot'} {tuple(shape)} max|err| {err:.3g}")
     if torch.cuda.is_available():
@@ -360,6 +374,11 @@ def run_self_test(ar, reference, device, cases=None, eps: float = 1e-5) -> Optio
 
 def _time_us(fn, iters: int = 20) -> float:
     fn()
+    if not torch.cuda.is_available():          # CPU stand-ins in the tests: wall clock
+        t0 = time.perf_counter()
+        for _ in range(iters):
+            fn()
+        return (time.perf_counter() - t0) * 1e6 / iters
     torch.cuda.synchronize()
     a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     a.record()
@@ -395,10 +414,18 @@ def run_tuning(ar, rccl_all_reduce, agree_max) -> dict:
     sizes = [s for s in (32 << 10, 128 << 10, 512 << 10, 1 << 20, 2 << 20, 4 << 20, 8 << 20,
                          16 << 20, 32 << 20) if s <= ar.max_bytes]
     rows = []
+    inf = float("inf")
+
+    def timed(fn):
+        try:
+            return _time_us(fn)
+        except Exception:   # noqa: BLE001 - a failing form never wins; RCCL still runs below
+            return inf
+
     for sz in sizes:
-        x = torch.ones(sz // 2, dtype=torch.bfloat16, device="cuda")
-        rows.append([_time_us(lambda: ar.all_reduce(x, kind=0)),
-                     _time_us(lambda: ar.all_reduce(x, kind=1)),
+        x = torch.ones(sz // 2, dtype=torch.bfloat16, device=getattr(ar, "device", "cuda"))
+        rows.append([timed(lambda: ar.all_reduce(x, kind=0)),
+                     timed(lambda: ar.all_reduce(x, kind=1)),
                      _time_us(lambda: rccl_all_reduce(x))])
     t = agree_max(torch.tensor(rows, dtype=torch.float64)).tolist()
     one, two, rc = [r[0] for r in t], [r[1] for r in t], [r[2] for r in t]
@@ -450,8 +477,22 @@ def init_custom_allreduce(max_bytes: int, factory=None, reference=None, agree=No
         return None
     info = {}
     tune = (os.environ.get("EIA_AR_TUNE", "1") != "0") if tune is None else tune
-    if tune and torch.cuda.is_available():
+    if tune and (torch.cuda.is_available() or factory is not CustomAllReduce):
         info = run_tuning(ar, reference, lambda t: agree(t, dist.ReduceOp.MAX))
+        # The timing pass runs the custom kernels again after the self-test's last spin check:
+        # a barrier spin that hits its bound here leaves the sticky flag set, and the engine's
+        # ErrorPoller would then fail at start-up.  Every rank reads its flag and the ranks
+        # agree (MIN of "clean"), so all of them keep the kernel or all go back to RCCL.
+        if torch.cuda.is_available():
+            torch.cuda.synchronize()
+        clean = agree(torch.tensor([0 if ar.error_flag() else 1], dtype=torch.int32),
+                      dist.ReduceOp.MIN)
+        if int(clean.item()) == 0:
+            logger.error("custom all-reduce barrier spin limit hit while tuning; every TP "
+                         "rank uses RCCL")
+            ar.close()
+            STATUS = {"active": False, "reason": "tuning spin timeout", "tuning": info}
+            return None
         ar.oneshot_max, ar.use_max = info["oneshot_max"], info["use_max"]
         logger.info("custom all-reduce tuned: one-shot <= %d B, custom <= %d B (RCCL above)",
                     ar.oneshot_max, ar.use_max)

@@ -179,6 +179,13 @@ def test_logs_stack_values(overlay):
     if overlay:
         aws = cfg["storage_config"]["aws"]
         assert {"region", "bucketnames", "access_key_id", "secret_access_key"} <= set(aws)
+        # credentials are expanded from the Secret at start-up, never rendered into the config
+        assert aws["access_key_id"] == "${AWS_ACCESS_KEY_ID}"
+        assert aws["secret_access_key"] == "${AWS_SECRET_ACCESS_KEY}"
+        for target in ("write", "read", "backend"):
+            t = loki[target]
+            assert "-config.expand-env=true" in t["extraArgs"]
+            assert t["extraEnvFrom"][0]["secretRef"]["name"] == "loki-s3-credentials"
     otel = v["otelcol-logs"]
     assert otel["mode"] == "daemonset" and otel["podMonitor"]["enabled"]
     assert otel["podMonitor"]["extraLabels"]["release"] == "observability"
@@ -207,8 +214,24 @@ def test_observability_plays_apply_s3_overlay():
         assert "aws-s3-values.yaml" in vs["logs_values_files"] and "if logs_s3" in \
             vs["logs_values_files"]
         aws = vs["logs_s3_values"]["loki"]["loki"]["storage_config"]["aws"]
-        assert "aws_secret_key" in aws["secret_access_key"] and "aws_bucket" in aws["bucketnames"]
+        assert "aws_bucket" in aws["bucketnames"]
+        # the keys go to a Secret (no_log), never into helm values / the Loki ConfigMap
+        assert "secret_access_key" not in aws and "access_key_id" not in aws
+        assert "aws_secret_key" not in str(vs)
+        sec = [t for t in doc["tasks"] if t.get("name", "").startswith("Loki S3 credentials")][0]
+        assert sec["no_log"] is True and "logs_s3" in sec["when"]
+        body = sec["kubernetes.core.k8s"]["definition"]
+        assert body["metadata"]["name"] == "loki-s3-credentials"
+        assert "aws_secret_key" in body["stringData"]["AWS_SECRET_ACCESS_KEY"]
         task = [t for t in doc["tasks"] if t.get("name") == "Logs stack (Loki + OTEL collector)"][0]
+        assert task["no_log"] is True
         h = task["kubernetes.core.helm"]
         assert h["values_files"] == "{{ logs_values_files }}"
-        assert "logs_s3_values" in str(h["values"])
+        assert "logs_s3_values" in str(h["values"]) and "logs_common_values" in str(h["values"])
+        # tenant and write endpoint from one variable each (collector header == datasource)
+        cv = vs["logs_common_values"]
+        assert cv["tenant"] == "{{ logs_tenant }}"
+        hdr = cv["otelcol-logs"]["config"]["extensions"]["headers_setter/tenant"]["headers"][0]
+        assert hdr["value"] == "{{ logs_tenant }}"
+        ep = cv["otelcol-logs"]["config"]["exporters"]["otlphttp/loki"]["endpoint"]
+        assert "{{ obs_ns }}" in ep

@@ -28,16 +28,33 @@ class _GlooAR:
 
     device = "cpu"
 
-    def __init__(self, rank, world, wrong=False, max_bytes=8 << 20):
+    def __init__(self, rank, world, wrong=False, max_bytes=8 << 20, raise_case=-1,
+                 spin_in_tuning=False):
         self.rank, self.world, self.wrong = rank, world, wrong
         self.max_bytes = self.use_max = max_bytes
         self.oneshot_max = 512 * 1024
         self.closed = False
+        self.calls = 0
+        self.raise_case = raise_case          # this rank's custom call #n raises
+        self.spin_in_tuning = spin_in_tuning  # a timing call sets the sticky error flag
+        self.err = 0
 
     def all_reduce(self, x, out=None, kind=None):
+        self.calls += 1
+        if self.calls == self.raise_case:
+            # a local failure: the peers' custom call has no partner (their kernel would spin
+            # out); the stand-in does not join their gloo sum, the protocol must not hang
+            raise RuntimeError("injected custom kernel failure")
+        if self.raise_case > 0:
+            # peers of a raising rank: the custom form is local-only here (no cross-rank
+            # traffic), so a missing partner cannot deadlock the stand-in
+            return x * self.world
         dist.all_reduce(x)
         if self.wrong:
             x.view(-1)[-1] += 1.0
+        if self.spin_in_tuning and x.numel() >= (32 << 10) // 2 and x.dtype == torch.bfloat16 \
+                and bool((x == self.world).all()):
+            self.err = 1                      # torch.ones input: the tuning pass
         return x
 
     def add_rmsnorm(self, x, residual, weight, eps, twoshot=None):
@@ -47,17 +64,24 @@ class _GlooAR:
         return out
 
     def error_flag(self):
-        return 0
+        return self.err
 
     def close(self):
         self.closed = True
 
 
-def _worker(rank, world, port, bad_rank, q):
+def _worker(rank, world, port, bad_rank, q, mode="wrong"):
     try:
         dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank,
                                 world_size=world)
-        ar = _GlooAR(rank, world, wrong=(rank == bad_rank))
+        if mode == "raise":
+            # every rank takes the local-only custom form; rank bad_rank's second custom call
+            # raises mid self-test
+            ar = _GlooAR(rank, world, raise_case=2 if rank == bad_rank else 10 ** 9)
+        elif mode == "spin":
+            ar = _GlooAR(rank, world, spin_in_tuning=(rank == bad_rank))
+        else:
+            ar = _GlooAR(rank, world, wrong=(rank == bad_rank))
 
         def reference(x):
             dist.all_reduce(x)
@@ -68,7 +92,7 @@ def _worker(rank, world, port, bad_rank, q):
             return t
 
         got = cam.init_custom_allreduce(8 << 20, factory=lambda mb: ar, reference=reference,
-                                        agree=agree, tune=False)
+                                        agree=agree, tune=(mode == "spin"))
         from enterprise_inference_amd.parallel import comm
         q.put((rank, got is not None, ar.closed, cam.STATUS["reason"],
                comm.get_custom_allreduce() is not None))
@@ -80,11 +104,12 @@ def _worker(rank, world, port, bad_rank, q):
             dist.destroy_process_group()
 
 
-def _run(world, bad_rank):
+def _run(world, bad_rank, mode="wrong"):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _port()
-    ps = [ctx.Process(target=_worker, args=(r, world, port, bad_rank, q)) for r in range(world)]
+    ps = [ctx.Process(target=_worker, args=(r, world, port, bad_rank, q, mode))
+          for r in range(world)]
     for p in ps:
         p.start()
     res = sorted(q.get(timeout=120) for _ in ps)
@@ -139,3 +164,26 @@ def test_status_gauge_rendered():
     m.set_custom_allreduce({"active": False, "reason": "self-test mismatch"})
     text = m.render().decode()
     assert 'eia:custom_allreduce_active{model_name="tiny",reason="self-test mismatch"} 0.0' in text
+
+
+@pytest.mark.parametrize("world,bad", [(2, 0), (4, 2)])
+def test_self_test_local_raise_does_not_hang(world, bad):
+    """One rank's custom call raises mid self-test: it keeps running the remaining cases'
+    reference collectives with its peers, and every rank falls back together (no hang)."""
+    res = _run(world, bad, mode="raise")
+    assert len(res) == world
+    for rank, active, closed, reason, registered in res:
+        assert not isinstance(active, str), active
+        assert not active and not registered and closed, res
+        assert reason == "self-test mismatch", res
+
+
+def test_tuning_spin_timeout_falls_back_everywhere():
+    """A barrier spin limit hit during the timing pass (sticky error flag on ONE rank): every
+    rank closes the custom kernel with reason 'tuning spin timeout' instead of starting the
+    engine with a set flag."""
+    res = _run(2, 1, mode="spin")
+    for rank, active, closed, reason, registered in res:
+        assert not isinstance(active, str), active
+        assert not active and not registered and closed, res
+        assert reason == "tuning spin timeout", res

@@ -253,10 +253,13 @@ def test_remote_image_dns_rebinding_pinned(monkeypatch):
             yield b"abc"
 
     @contextlib.contextmanager
-    def fake_stream(url, headers, extensions, timeout):
-        seen.update(url=url, headers=headers, ext=extensions)
+    def fake_stream(url, headers, extensions, timeout, trust_env=False):
+        seen.update(url=url, headers=headers, ext=extensions, trust_env=trust_env)
         yield _Resp()
 
+    for k in ("HTTPS_PROXY", "https_proxy", "HTTP_PROXY", "http_proxy", "ALL_PROXY",
+              "all_proxy"):
+        monkeypatch.delenv(k, raising=False)
     monkeypatch.setattr(socket, "getaddrinfo", fake_getaddrinfo)
     monkeypatch.setattr(lv, "_open_stream", fake_stream)
     assert lv.fetch_image_bytes("https://img.example.com:8443/a.png") == b"abc"
@@ -264,6 +267,7 @@ def test_remote_image_dns_rebinding_pinned(monkeypatch):
     assert seen["url"] == "https://93.184.216.34:8443/a.png"
     assert seen["headers"] == {"Host": "img.example.com:8443"}
     assert seen["ext"] == {"sni_hostname": "img.example.com"}
+    assert seen["trust_env"] is False         # the pinned dial ignores proxy settings
 
     # a peer address other than the validated one is refused before the body is read
     class _Stream:
@@ -274,6 +278,53 @@ def test_remote_image_dns_rebinding_pinned(monkeypatch):
     answers = iter(["93.184.216.34"])
     with pytest.raises(ValueError, match="unexpected address"):
         lv.fetch_image_bytes("https://img.example.com/a.png")
+
+
+def test_remote_image_through_egress_proxy(monkeypatch):
+    """With HTTPS_PROXY set (enterprise egress), the policy check still resolves and vets the
+    name, but the request goes to the proxy by NAME with the environment trusted, and the
+    peer check (which would see the proxy's address) is skipped; NO_PROXY matches the name."""
+    import contextlib
+    import socket
+
+    from enterprise_inference_amd.models import llama4_vision as lv
+    seen = {}
+
+    class _Stream:
+        def get_extra_info(self, k):
+            return ("10.1.2.3", 3128) if k == "server_addr" else None   # the proxy
+
+    class _Resp:
+        is_redirect = False
+        headers = {"content-length": "3"}
+        extensions = {"network_stream": _Stream()}
+
+        def raise_for_status(self):
+            pass
+
+        def iter_bytes(self):
+            yield b"abc"
+
+    @contextlib.contextmanager
+    def fake_stream(url, headers, extensions, timeout, trust_env=False):
+        seen.update(url=url, headers=headers, ext=extensions, trust_env=trust_env)
+        yield _Resp()
+
+    def fake_getaddrinfo(host, port, *a, **k):
+        return [(socket.AF_INET, socket.SOCK_STREAM, 6, "", ("93.184.216.34", port))]
+
+    monkeypatch.setattr(socket, "getaddrinfo", fake_getaddrinfo)
+    monkeypatch.setattr(lv, "_open_stream", fake_stream)
+    monkeypatch.setenv("HTTPS_PROXY", "http://proxy.corp:3128")
+    monkeypatch.delenv("NO_PROXY", raising=False)
+    monkeypatch.delenv("no_proxy", raising=False)
+    assert lv.fetch_image_bytes("https://img.example.com/a.png") == b"abc"
+    assert seen["url"] == "https://img.example.com/a.png" and seen["trust_env"] is True
+    # the host is exempted by NO_PROXY: back to the pinned direct dial
+    monkeypatch.setenv("NO_PROXY", "img.example.com")
+    _Resp.extensions = {}
+    assert lv.fetch_image_bytes("https://img.example.com/a.png") == b"abc"
+    assert seen["url"] == "https://93.184.216.34/a.png" and seen["trust_env"] is False
 
 
 def test_slow_image_url_does_not_block_event_loop(monkeypatch):
