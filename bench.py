@@ -384,7 +384,7 @@ class Replica:
                 - stats0["num_generation_tokens"],
                 "engine_steps": stats1["num_steps"] - stats0["num_steps"],
                 "engine_busy_s": stats1["step_time_s"] - stats0["step_time_s"],
-                "num_blocks": stats1["num_blocks"]}
+                "num_blocks": stats1["num_blocks"], "dist": stats1.get("dist")}
 
     def closed_loop(self, dur: float, warm: float) -> dict:
         """Steady-state arrival: every user resubmits on completion.  Throughput = engine
@@ -599,7 +599,7 @@ def _extra(a, slots, n_gpus: int, deadline: float, logdir: str) -> dict:
         d = _summary(a, summ, n_gpus, "endpoint")
         keep = ("value", "vs_baseline", "ms_per_step", "ttft_p50_ms", "ttft_p90_ms",
                 "tpot_p50_ms", "tpot_p90_ms", "failed_requests", "init_s",
-                "baseline_tok_s_per_replica", "per_model", "engine_tok_s")
+                "baseline_tok_s_per_replica", "per_model", "engine_tok_s", "dist")
         r = {k: d[k] for k in keep if k in d}
         r.update(model=d["config"]["model"], users_per_replica=a.users,
                  parallelism=d["config"]["parallelism"], steps=a.steps,
@@ -745,12 +745,33 @@ def run_engine(args) -> int:
         ex.shutdown()
     local_stats = {"tokens": tot_tokens, "elapsed": elapsed, "ttft": all_ttft, "tpot": all_tpot,
                    "e2e": [], "failed": [], "init_s": init_s, "num_blocks": engine.num_blocks,
-                   "model": model_id}
+                   "model": model_id, "dist": ex.dist_info()}
     _gather_report(args, dist, local_stats, rank, world, via="engine")
     return 0
 
 
 # --------------------------------------------------------------------------- report
+
+def dist_summary(ranks) -> dict:
+    """Compact self-description of one replica from its ranks' ``describe_distributed``
+    records (engine/executor.py): the world size each rank's process group formed, the
+    collective backend, and the custom all-reduce decision (active / reason / thresholds /
+    per-size timings) -- identical on every rank by construction, checked here."""
+    ranks = [r for r in (ranks or []) if isinstance(r, dict) and "error" not in r]
+    if not ranks:
+        return {"ranks": 0}
+    ar = [r.get("custom_allreduce") or {} for r in ranks]
+    out = {"ranks": len(ranks), "tp": ranks[0].get("tp_size", 1),
+           "pp": ranks[0].get("pp_size", 1),
+           "world_sizes": [r.get("world_size") for r in ranks],
+           "backend": ranks[0].get("backend")}
+    if out["tp"] > 1 or out["pp"] > 1:
+        out["custom_allreduce"] = ar[0]
+        out["custom_allreduce_agreed"] = all(
+            (a.get("active"), a.get("oneshot_max"), a.get("use_max")) ==
+            (ar[0].get("active"), ar[0].get("oneshot_max"), ar[0].get("use_max")) for a in ar)
+    return out
+
 
 def _gather_report(args, dist, local_stats, rank, world, via: str):
     if dist is not None and dist.is_initialized():
@@ -840,6 +861,18 @@ def _summary(args, reps, n_gpus: int, via: str) -> dict:
         out["per_model"] = {m: {"tok_s": round(sum(g["tokens"] for g, mm in zip(reps, models)
                                                   if mm == m) / elapsed, 2),
                                 "replicas": models.count(m)} for m in uniq}
+    ds = [dist_summary(g.get("dist")) for g in reps if g.get("dist") is not None]
+    if ds:
+        # one entry per replica; replicas that look the same collapse into one with a count
+        uniq_d = []
+        for d in ds:
+            for u in uniq_d:
+                if u["desc"] == d:
+                    u["replicas"] += 1
+                    break
+            else:
+                uniq_d.append({"desc": d, "replicas": 1})
+        out["dist"] = [dict(u["desc"], replicas=u["replicas"]) for u in uniq_d]
     if via == "endpoint":
         busy = max(g["engine_busy_s"] for g in reps)
         # engine-level throughput over each engine core's busy time (no HTTP / client), and

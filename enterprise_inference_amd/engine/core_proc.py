@@ -126,14 +126,26 @@ def _run_op(engine, op: str):
         if torch.cuda.is_available() and torch.cuda.is_initialized():
             torch.cuda.synchronize()
         return True
+    if op == "dist":
+        return _dist_info(engine)
     if op == "stats":
         st = engine.stats
         return {"num_steps": st.num_steps, "num_generation_tokens": st.num_generation_tokens,
                 "num_prompt_tokens": st.num_prompt_tokens, "num_blocks": engine.num_blocks,
                 "step_time_s": st.step_time_s,
                 "phase_times": dict(engine.phase_times),
-                "loop_times": dict(getattr(engine, "loop_times", {}))}
+                "loop_times": dict(getattr(engine, "loop_times", {})),
+                "dist": _dist_info(engine)}
     raise ValueError(f"unknown engine op {op!r}")
+
+
+def _dist_info(engine) -> list:
+    """Per-rank process-group / custom all-reduce description of this replica (executor)."""
+    fn = getattr(getattr(engine, "executor", None), "dist_info", None)
+    try:
+        return fn() if fn is not None else []
+    except Exception as e:   # noqa: BLE001 - a description must never fail the stats op
+        return [{"error": repr(e)}]
 
 
 # Intake coalescing: an idle engine that receives a request keeps reading for as long as more

@@ -17,7 +17,7 @@ import multiprocessing as mp
 import os
 import socket
 import time
-from typing import Optional
+from typing import List, Optional
 
 import torch
 import torch.distributed as dist
@@ -44,6 +44,41 @@ def _agree_num_blocks(nb: int) -> int:
     return int(t.item())
 
 
+def describe_distributed(runner: Optional[ModelRunner] = None) -> dict:
+    """What THIS rank's process group looks like (the world size RCCL formed, its TP / PP
+    coordinates, the collective backend) and the custom all-reduce decision -- gathered over
+    the replica at start-up (``gather_dist_info``) so a multi-GPU run describes itself: a
+    silent fallback to RCCL then shows up as a reason, not as a slow kernel."""
+    from ..parallel import custom_allreduce as car
+    info = {"rank": dist.get_rank() if dist.is_initialized() else 0,
+            "world_size": dist.get_world_size() if dist.is_initialized() else 1,
+            "backend": pstate.backend(), "tp_rank": pstate.tp_rank(),
+            "tp_size": pstate.tp_size(), "pp_rank": pstate.pp_rank(),
+            "pp_size": pstate.pp_size(), "pid": os.getpid()}
+    if runner is not None and runner.is_gpu:
+        info["device"] = str(runner.device)
+    st = dict(car.STATUS)
+    tuning = st.pop("tuning", None)
+    info["custom_allreduce"] = st
+    if tuning:
+        info["custom_allreduce"]["tuning"] = {k: tuning[k] for k in
+                                              ("sizes", "oneshot_us", "twoshot_us", "rccl_us")
+                                              if k in tuning}
+    return info
+
+
+def gather_dist_info(runner: ModelRunner) -> List[dict]:
+    """Every replica rank's ``describe_distributed`` (a gloo all-gather over the replica's
+    CPU group; a one-process engine reports itself)."""
+    mine = describe_distributed(runner)
+    grp = pstate.replica_cpu_group()
+    if len(pstate.replica_ranks()) == 1 or grp is None:
+        return [mine]
+    out = [None] * len(pstate.replica_ranks())
+    dist.all_gather_object(out, mine, group=grp)
+    return out
+
+
 def setup_runner(cfg: EngineConfig) -> ModelRunner:
     runner = ModelRunner(cfg)
     ar = None
@@ -51,6 +86,11 @@ def setup_runner(cfg: EngineConfig) -> ModelRunner:
             not cfg.parallel.disable_custom_all_reduce:
         from ..parallel.custom_allreduce import init_custom_allreduce
         ar = init_custom_allreduce(cfg.parallel.custom_allreduce_max_bytes)
+    elif cfg.parallel.tensor_parallel_size > 1:
+        from ..parallel import custom_allreduce as car
+        car.STATUS = {"active": False, "reason": "disabled" if runner.is_gpu and
+                      cfg.parallel.disable_custom_all_reduce else "no GPU"}
+    runner.dist_info = gather_dist_info(runner)
     nb = runner.determine_num_blocks()
     nb = _agree_num_blocks(nb)
     runner.allocate_kv_cache(nb)
@@ -89,6 +129,9 @@ class UniprocExecutor:
     def __init__(self, cfg: EngineConfig, runner: Optional[ModelRunner] = None):
         self.runner = runner or setup_runner(cfg)
         self.num_blocks = self.runner.num_blocks
+
+    def dist_info(self) -> List[dict]:
+        return getattr(self.runner, "dist_info", None) or [describe_distributed(self.runner)]
 
     def execute(self, bm, sched) -> StepOutput:
         return self.runner.execute(bm, sched)
@@ -229,6 +272,9 @@ class TPExecutor:
         self.num_blocks = self.runner.num_blocks
         self._swaps = []             # (kind, gpu block, cpu block) until the next plan
 
+    def dist_info(self) -> List[dict]:
+        return getattr(self.runner, "dist_info", None) or [describe_distributed(self.runner)]
+
     # ------------------------------------------------------------------ liveness
     def dead_workers(self):
         return [p for p in self.procs if not p.is_alive()]
@@ -316,6 +362,15 @@ class FakeExecutor:
         self.num_blocks = cfg.cache.num_gpu_blocks or 16384
         self.vocab = cfg.model.vocab_size
         self._rng = _random.Random(cfg.seed)
+        self._tp = cfg.parallel.tensor_parallel_size
+
+    def dist_info(self) -> List[dict]:
+        """The description a real TP replica gives (one record per rank), so the report
+        plumbing is testable on the CPU; the fake forms no process group."""
+        return [{"rank": r, "world_size": self._tp, "backend": "fake", "tp_rank": r,
+                 "tp_size": self._tp, "pp_rank": 0, "pp_size": 1, "pid": os.getpid(),
+                 "custom_allreduce": {"active": False, "reason": "fake executor"}}
+                for r in range(self._tp)]
 
     def execute(self, bm, sched) -> StepOutput:
         import time as _time

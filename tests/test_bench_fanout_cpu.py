@@ -64,6 +64,13 @@ def test_fanout_tensor_parallel_replicas(tmp_path):
     assert out["config"]["parallelism"] == "dp2xtp2"
     logs = sorted(p.name for p in tmp_path.iterdir() if p.name.startswith("bench_server"))
     assert logs == ["bench_server_rank0.log", "bench_server_rank2.log"]
+    # the line describes every TP replica: ranks, the world size each saw, the custom
+    # all-reduce decision (identical twin replicas collapse into one entry with a count)
+    (d,) = out["dist"]
+    assert d["replicas"] == 2 and d["tp"] == 2 and d["ranks"] == 2
+    assert d["world_sizes"] == [2, 2]
+    assert d["custom_allreduce"] == {"active": False, "reason": "fake executor"}
+    assert d["custom_allreduce_agreed"] is True
 
 
 def test_co_deploy(tmp_path):
@@ -101,6 +108,8 @@ def test_extra_configs_and_closed_loop(tmp_path):
     assert c3["parallelism"] == "dp1xtp2" and c3["users_per_replica"] == 35
     assert c3["value"] > 0 and c3["failed_requests"] == 0
     assert "baseline_tok_s_per_replica" in c3     # 1120 (4x Gaudi 3) at 128/128
+    (d3,) = c3["dist"]                            # config #3 describes its TP=N replica
+    assert d3["tp"] == 2 and d3["world_sizes"] == [2, 2] and "custom_allreduce" in d3
     assert "config5_codeploy_8b_mistral7b" not in ex          # only at N = 8
     cl = out["closed_loop"]
     assert cl["tok_s"] > 0 and cl["requests"] > 0 and cl["failed_requests"] == 0
@@ -128,3 +137,32 @@ def test_extra_config_errors_are_recorded(tmp_path, monkeypatch):
     assert not bench.want_extras(argparse.Namespace(extras="auto", mode="endpoint"), 1)
     assert bench.want_extras(argparse.Namespace(extras="auto", mode="endpoint"), 8)
     assert not bench.want_extras(argparse.Namespace(extras="auto", mode="engine"), 8)
+
+
+def test_dist_summary_keys_and_disagreement():
+    """The per-replica summary of describe_distributed records: world sizes, backend, the
+    custom all-reduce status with thresholds / timings, and a flag when ranks disagree."""
+    sys.path.insert(0, ROOT)
+    import bench
+    ok = {"active": True, "reason": "ok", "oneshot_max": 524288, "use_max": 8 << 20,
+          "tuning": {"sizes": [32768], "oneshot_us": [9.0], "twoshot_us": [12.0],
+                     "rccl_us": [30.0]}}
+    ranks = [{"rank": r, "world_size": 8, "backend": "nccl", "tp_rank": r, "tp_size": 8,
+              "pp_rank": 0, "pp_size": 1, "custom_allreduce": dict(ok)} for r in range(8)]
+    d = bench.dist_summary(ranks)
+    assert d["ranks"] == 8 and d["world_sizes"] == [8] * 8 and d["backend"] == "nccl"
+    assert d["custom_allreduce"]["oneshot_max"] == 524288
+    assert d["custom_allreduce"]["tuning"]["rccl_us"] == [30.0]
+    assert d["custom_allreduce_agreed"] is True
+    ranks[3]["custom_allreduce"] = {"active": False, "reason": "self-test mismatch"}
+    assert bench.dist_summary(ranks)["custom_allreduce_agreed"] is False
+    # a TP=1 replica carries no custom all-reduce entry
+    one = bench.dist_summary([dict(ranks[0], tp_size=1, world_size=1)])
+    assert one["tp"] == 1 and "custom_allreduce" not in one
+    assert bench.dist_summary([]) == {"ranks": 0}
+
+
+def test_describe_distributed_single_process():
+    from enterprise_inference_amd.engine.executor import describe_distributed
+    d = describe_distributed(None)
+    assert d["world_size"] == 1 and d["tp_size"] == 1 and "custom_allreduce" in d

@@ -40,6 +40,11 @@ def _run(path, d, tp, ep=False, pp=1, temperature=0.0, delayed=True, **sp):
                        device="cpu", dtype=torch.float32)
     eng = LLMEngine(cfg)
     try:
+        # every rank of the replica described itself at start-up (bench.py / /eia/stats)
+        info = eng.executor.dist_info()
+        assert len(info) == tp * pp, info
+        assert [r["tp_rank"] for r in info] == [i % tp for i in range(tp * pp)]
+        assert all(r["world_size"] == tp * pp and "custom_allreduce" in r for r in info)
         prompts = [[5, 6, 7, 8, 9, 10] * 8, [11, 12, 13], list(range(40, 90))]
         params = SamplingParams(max_tokens=6, temperature=temperature, ignore_eos=True, seed=11,
                                 **sp)
