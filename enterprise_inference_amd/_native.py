@@ -62,6 +62,9 @@ _SIGNATURES = {
     "eia_moe_grouped_gemm": [P, L, IP, P, I, I, I, IP, I, I, P, L, S],
     "eia_gemm_skinny": [P, L, P, L, P, P, L, I, I, I, I, I, I, S],
     "eia_splitk_reduce": [P, I, I, I, P, P, L, S],
+    "eia_mlp_fused": [P, L, P, P, P, P, IP, I, I, I, I, S],
+    "eia_mlp_fused_plan": [I, I, I, I, P],
+    "eia_mlp_fused_error": [IP, I, P],
     "eia_splitk_add_rmsnorm": [P, I, I, I, P, P, F, P, L, S],
     "eia_ar_alloc": [P, L],
     "eia_ar_free": [P],

@@ -284,12 +284,6 @@ class EngineConfig:
         if self.device == "cuda" and self.parallel.world_size > 1 and (
                 self.parallel.share_device or self.parallel.dist_backend == "gloo"):
             self.enforce_eager = True        # host-staged gloo collectives cannot be captured
-        if self.device == "cuda" and self.parallel.tensor_parallel_size > 1 and \
-                self.parallel.enable_expert_parallel and \
-                os.environ.get("EIA_EP_DISPATCH", "allreduce") == "all_to_all":
-            # the all-to-all dispatch reads its split sizes back to the host every layer: not
-            # capturable in a HIP graph, so decode runs eagerly (docs/runtime-flags.md)
-            self.enforce_eager = True
         if self.cache.cache_dtype is None:
             self.cache.cache_dtype = self.dtype
         if self.scheduler.max_model_len > self.model.max_position_embeddings and \

@@ -302,6 +302,83 @@ def linear(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = None
     return F.linear(x, w, bias)
 
 
+# --------------------------------------------------------------------------- fused decode MLP
+# gate_up + SwiGLU and the split-K down projection in ONE launch (csrc/kernels/mlp_fused.hip):
+# 256 balanced producers (every CU streams the same gate/up bytes) hand h to the down
+# consumers split by split through arrival counters -- no second launch, no boundary, and the
+# 32 CUs the 4-pair SwiGLU grid left idle now stream.  EIA_FUSED_MLP=0 restores two launches.
+FUSED_MLP = os.environ.get("EIA_FUSED_MLP", "1") != "0"
+_MLP_SYNC: dict = {}
+_MLP_SYNC_WORDS = 64
+
+
+def mlp_sync_buffer(device: torch.device) -> Optional[torch.Tensor]:
+    """Per-device arrival / departure counters of the fused MLP (zero between launches: every
+    launch leaves them as it found them).  Created outside graph capture (the eager profiling
+    run comes first); a capture that would have to create it takes the two-launch form."""
+    key = (device.type, device.index)
+    t = _MLP_SYNC.get(key)
+    if t is None:
+        if torch.cuda.is_current_stream_capturing():
+            return None
+        t = torch.zeros(_MLP_SYNC_WORDS, dtype=torch.int32, device=device)
+        _MLP_SYNC[key] = t
+    return t
+
+
+@functools.lru_cache(maxsize=4096)
+def mlp_fused_split(M: int, H: int, I: int) -> int:
+    """Down-projection K split of the fused MLP (128-column tiles x split ~ 256 consumers), or
+    0 when the shape has no fused form (eia_mlp_fused_plan)."""
+    if not FUSED_MLP or H % 128:
+        return 0
+    sk = max(1, 256 // (H // 128))
+    while sk > 1 and I % sk:
+        sk //= 2
+    if 2 * sk + 1 > _MLP_SYNC_WORDS:
+        return 0
+    return sk if lib().eia_mlp_fused_plan(M, H, I, sk, None) == 0 else 0
+
+
+def mlp_fused_ok(x: torch.Tensor, w_gate_up: torch.Tensor, w_down: torch.Tensor) -> bool:
+    if not FUSED_MLP or DISABLE or x.dim() != 2 or not use_hip(x, w_gate_up, w_down):
+        return False
+    if x.dtype != torch.bfloat16 or w_gate_up.dtype != torch.bfloat16 or \
+            w_down.dtype != torch.bfloat16:
+        return False
+    M, H = x.shape
+    I = w_down.shape[1]
+    if w_gate_up.shape != (2 * I, H) or w_down.shape != (H, I):
+        return False
+    if not (w_gate_up.is_contiguous() and w_down.is_contiguous()) or x.stride(1) != 1 or \
+            x.stride(0) % 8:
+        return False
+    return mlp_fused_split(M, H, I) > 0 and mlp_sync_buffer(x.device) is not None
+
+
+def mlp_fused(x: torch.Tensor, w_gate_up: torch.Tensor, w_down: torch.Tensor) -> SplitK:
+    """down(silu(x Wg^T) * (x Wu^T)) as fp32 split-K partials (the consumer's add + RMSNorm
+    sums them, ``splitk_add_rmsnorm``)."""
+    M, H = x.shape
+    I = w_down.shape[1]
+    sk = mlp_fused_split(M, H, I)
+    h = torch.empty(M, I, dtype=torch.bfloat16, device=x.device)
+    part = torch.empty(sk, M, H, dtype=torch.float32, device=x.device)
+    check(lib().eia_mlp_fused(ptr(x), x.stride(0), ptr(w_gate_up), ptr(w_down), ptr(h),
+                              ptr(part), ptr(mlp_sync_buffer(x.device)), M, H, I, sk,
+                              stream(x)), "mlp_fused")
+    return SplitK(part, sk, M, H)
+
+
+def mlp_fused_error(device: torch.device, sk: int) -> int:
+    """1 when a fused-MLP consumer gave up waiting (bounded spin) since the buffer was made."""
+    import ctypes
+    buf = mlp_sync_buffer(device)
+    v = ctypes.c_int(0)
+    check(lib().eia_mlp_fused_error(ptr(buf), sk, ctypes.byref(v)), "mlp_fused_error")
+    return v.value
+
+
 def splitk_add_rmsnorm(s: SplitK, residual: torch.Tensor, weight: torch.Tensor, eps: float):
     """residual += reduce(s) (+bias); returns (rmsnorm(residual) * weight, residual)."""
     if s.bias is not None:

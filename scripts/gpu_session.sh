@@ -19,6 +19,7 @@ run() {  # name timeout cmd...
 for s in $STEPS; do
   case $s in
     tests) run pytest_gpu 900 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread ;;
+    ktests) run pytest_k 600 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread -k "$KEXPR" ;;
     smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench) run bench 900 python bench.py --steps ${BENCH_STEPS:-3} --warmup 1 --verbose ;;
     prof)

@@ -43,6 +43,20 @@ def _worker(rank, world, port, q):
         got = moe_all_to_all(x, w, ids, w13[lo:lo + e_per], w2[lo:lo + e_per], lo, e_per)
         want = ref.fused_moe(x, w13, w2, w, ids)
         err1 = (got - want).abs().max().item()
+        # padded, host-sync-free exchange (capacity = the largest rank's T * k, equal on every
+        # rank): same result; no split sizes are read back (tolist / item would raise)
+        cap = (5 + 3 * (world - 1)) * k
+        real_tolist, real_item = torch.Tensor.tolist, torch.Tensor.item
+
+        def no_sync(*a, **kw):
+            raise AssertionError("host read-back in the padded all-to-all")
+        torch.Tensor.tolist, torch.Tensor.item = no_sync, no_sync
+        try:
+            gotp = moe_all_to_all(x, w, ids, w13[lo:lo + e_per], w2[lo:lo + e_per], lo, e_per,
+                                  capacity=cap)
+        finally:
+            torch.Tensor.tolist, torch.Tensor.item = real_tolist, real_item
+        err1 = max(err1, (gotp - want).abs().max().item())
         # replicated tokens (TP engine form) vs the all-reduce EP form
         gr = torch.Generator().manual_seed(7)
         Tr = 11
@@ -54,6 +68,16 @@ def _worker(rank, world, port, q):
                              (lo, lo + e_per))
         dist.all_reduce(part)
         err2 = (a2a - part).abs().max().item()
+        # the same batch through the exact-split exchange (prefill-sized form)
+        from enterprise_inference_amd.parallel import expert_parallel as ep
+        saved = ep.PADDED_MAX_TOKENS
+        ep.PADDED_MAX_TOKENS = 0
+        try:
+            exact = moe_all_to_all_replicated(xr, wr, idr, w13[lo:lo + e_per],
+                                              w2[lo:lo + e_per], lo, e_per)
+        finally:
+            ep.PADDED_MAX_TOKENS = saved
+        err2 = max(err2, (exact - part).abs().max().item())
         q.put((rank, err1, err2))
     except Exception as e:   # noqa: BLE001
         q.put((rank, repr(e), None))
@@ -87,3 +111,14 @@ def test_tp2_all_to_all_ep_engine_matches_tp1(tmp_path, monkeypatch):
     monkeypatch.setenv("EIA_EP_DISPATCH", "all_to_all")
     got = _run(path, d, 2, ep=True)
     assert got == ref_toks
+
+
+def test_dispatch_layout_slots():
+    """Each (token, slot) pair lands in its owner's block, in order, without collisions."""
+    from enterprise_inference_amd.parallel.expert_parallel import dispatch_layout
+    ids = torch.tensor([[5, 0], [1, 7], [4, 2], [6, 3]], dtype=torch.int32)   # 8 experts
+    gids, dest = dispatch_layout(ids, e_per=2, world=4, capacity=8)
+    assert gids.tolist() == [5, 0, 1, 7, 4, 2, 6, 3]
+    # owners 2,0,0,3,2,1,3,1 -> block * 8 + running position within the block
+    assert dest.tolist() == [16, 0, 1, 24, 17, 8, 25, 9]
+    assert len(set(dest.tolist())) == len(dest)

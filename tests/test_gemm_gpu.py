@@ -127,3 +127,76 @@ def test_splitk_add_rmsnorm(M, H, sk):
     # slab summation order may differ from torch's: one bf16 ulp
     assert ((res.float() - new_res.float()).abs() <= 1e-2 * new_res.float().abs() + 1e-3).all()
     _check(out, ref, f"M={M} H={H} sk={sk}")
+
+
+def _mlp_ref(x, wgu, wd):
+    I = wd.shape[1]
+    g = x.float() @ wgu[:I].float().t()
+    u = x.float() @ wgu[I:].float().t()
+    h = (F.silu(g) * u).to(BF).float()       # the kernel hands h over in bf16
+    return h @ wd.float().t()
+
+
+@pytest.mark.parametrize("M", [1, 16, 33, 65, 80])
+@pytest.mark.parametrize("H,I", [(4096, 14336), (8192, 28672)])
+def test_mlp_fused(M, H, I):
+    """Fused decode MLP (gate_up + SwiGLU producers -> split-K down consumers in one launch)
+    vs the fp32 reference; repeated launches (the counters re-arm themselves) and no consumer
+    may have hit its spin bound."""
+    from enterprise_inference_amd.ops import gemm
+    torch.manual_seed(M + I)
+    x = torch.randn(M, H, device=DEV, dtype=BF)
+    wgu = (torch.randn(2 * I, H, device=DEV) * H ** -0.5).to(BF)
+    wd = (torch.randn(H, I, device=DEV) * I ** -0.5).to(BF)
+    sk = gemm.mlp_fused_split(M, H, I)
+    assert sk > 0 and gemm.mlp_fused_ok(x, wgu, wd)
+    ref = _mlp_ref(x, wgu, wd)
+    for it in range(3):
+        out = gemm.mlp_fused(x, wgu, wd).materialize()
+        _check(out, ref, f"M={M} H={H} I={I} launch {it}")
+    torch.cuda.synchronize()
+    assert gemm.mlp_fused_split(M, H, I) == sk
+    assert gemm.mlp_fused_error(x.device, sk) == 0
+    assert int(gemm.mlp_sync_buffer(x.device)[:2 * sk].abs().sum()) == 0   # re-armed
+
+
+def test_mlp_fused_graph_replay():
+    """Captured once, replayed many times with new inputs: every replay matches."""
+    from enterprise_inference_amd.ops import gemm
+    M, H, I = 65, 4096, 14336
+    torch.manual_seed(5)
+    x = torch.randn(M, H, device=DEV, dtype=BF)
+    wgu = (torch.randn(2 * I, H, device=DEV) * H ** -0.5).to(BF)
+    wd = (torch.randn(H, I, device=DEV) * I ** -0.5).to(BF)
+    gemm.mlp_fused(x, wgu, wd)                       # eager first: creates the sync buffer
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        with torch.cuda.graph(g):
+            out = gemm.mlp_fused(x, wgu, wd).materialize()
+    torch.cuda.current_stream().wait_stream(s)
+    for it in range(4):
+        x.copy_(torch.randn(M, H, device=DEV, dtype=BF))
+        g.replay()
+        torch.cuda.synchronize()
+        _check(out, _mlp_ref(x, wgu, wd), f"replay {it}")
+    assert gemm.mlp_fused_error(x.device, gemm.mlp_fused_split(M, H, I)) == 0
+
+
+def test_llama_mlp_takes_fused_path():
+    """The Llama MLP module routes a decode batch through the fused kernel at TP = 1 and the
+    result (split-K partials) matches the two-launch form."""
+    from enterprise_inference_amd.models.llama import LlamaMLP
+    from enterprise_inference_amd.ops import gemm
+    torch.manual_seed(9)
+    mlp = LlamaMLP(4096, 14336, "silu", BF, DEV)
+    mlp.gate_up_proj.weight.data.normal_(0, 4096 ** -0.5)
+    mlp.down_proj.weight.data.normal_(0, 14336 ** -0.5)
+    x = torch.randn(65, 4096, device=DEV, dtype=BF)
+    y = mlp(x)
+    assert isinstance(y, gemm.SplitK) and y.sk == gemm.mlp_fused_split(65, 4096, 14336)
+    two = mlp.down_proj(mlp.gate_up_proj.forward_act_and_mul(x), defer_reduce=True)
+    two = two.materialize() if isinstance(two, gemm.SplitK) else two
+    _check(y.materialize(), two.float(), "fused vs two launches")
