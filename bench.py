@@ -384,6 +384,7 @@ class Replica:
                 - stats0["num_generation_tokens"],
                 "engine_steps": stats1["num_steps"] - stats0["num_steps"],
                 "engine_busy_s": stats1["step_time_s"] - stats0["step_time_s"],
+                "sync_steps": stats1.get("num_sync_steps", 0) - stats0.get("num_sync_steps", 0),
                 "num_blocks": stats1["num_blocks"], "dist": stats1.get("dist")}
 
     def closed_loop(self, dur: float, warm: float) -> dict:
@@ -881,6 +882,8 @@ def _summary(args, reps, n_gpus: int, via: str) -> dict:
                                         for g in reps), 2)
         out["engine_busy_frac"] = round(busy / elapsed, 3)
         out["engine_steps"] = sum(g["engine_steps"] for g in reps)
+        # steps that could not be launched ahead of the previous step's token read-back
+        out["engine_sync_steps"] = sum(g.get("sync_steps", 0) for g in reps)
     return out
 
 

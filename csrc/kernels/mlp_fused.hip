@@ -31,12 +31,15 @@
 // Hand-off recipe: cdna_hip_programming.md Guideline 16 (R1 publish: sc1 payload stores, every
 // storing wave drains vmcnt, barrier, one relaxed agent-scope atomic; consume: relaxed poll,
 // one fence(acquire, agent), barrier, plain loads).
+#include <cstdlib>
+
 #include "eia_common.h"
 
 namespace {
 
 typedef __attribute__((address_space(1))) unsigned long long gu64;
 typedef __attribute__((address_space(1))) int gi32;
+typedef __attribute__((address_space(1))) unsigned short gu16;
 
 constexpr int XPAD = 8;
 constexpr int KLANE = 8, KSTEP = 32;     // same k permutation as gemm_skinny.hip
@@ -159,8 +162,19 @@ template <int MT, int KCP, int KCC>
 __global__ void __launch_bounds__(256, 1)
 mlp_fused_kernel(const bf16_t* __restrict__ X, long ldx, const bf16_t* __restrict__ Wgu,
                  const bf16_t* __restrict__ Wd, bf16_t* __restrict__ h, float* __restrict__ part,
-                 int* __restrict__ sync, int M, int H, int I, int R, int P, int SK, int spin_max) {
+                 int* __restrict__ sync, int M, int H, int I, int R, int P, int SK, int spin_max,
+                 int flags, long long* __restrict__ trace) {
+  // flags (diagnostics, scripts/bench_mlp.py): 1 = producers only (consumers exit), 2 =
+  // consumers do not wait (h as left by an earlier launch).  trace: per workgroup 4 wall-clock
+  // stamps (100 MHz): entry, first chunk staged, stream done, exit.
   extern __shared__ __align__(16) bf16_t xs[];
+  long long t_entry = trace != nullptr ? wall_clock64() : 0, t_staged = 0, t_done = 0;
+  auto stamp_out = [&] {
+    if (trace != nullptr && threadIdx.x == 0) {
+      long long* tp = trace + 4 * blockIdx.x;
+      tp[0] = t_entry; tp[1] = t_staged; tp[2] = t_done; tp[3] = wall_clock64();
+    }
+  };
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
   const int r = lane & 15, g = lane >> 4;
@@ -173,16 +187,21 @@ mlp_fused_kernel(const bf16_t* __restrict__ X, long ldx, const bf16_t* __restric
   if ((int)blockIdx.x < P) {
     // ---------------------------------------------------------------- producer: gate_up
     const int i = blockIdx.x;
-    const int row0 = i * R + 16 * wave;               // this wave's pair rows [row0, +rows)
-    const int rows = min(16, R - 16 * wave);          // 16, or 8 for the half pair
-    const int rr = rows == 16 ? r : (r & 7);
+    const int rw = R >> 2;                            // rows of this wave's (gate, up) pair
+    const int row0 = i * R + rw * wave;
+    const int rr = r < rw ? r : r % rw;               // lanes past rw re-read a live row
     const bf16_t* wp[2] = {Wgu + (long)(row0 + rr) * H + KLANE * g,
                            Wgu + (long)(I + row0 + rr) * H + KLANE * g};
     f32x4 acc[2][MT];
-    stream_gemm<MT, 2, KCP>(X, ldx, wp, 0, H, Mc, xs, acc, [] {});
-    // epilogue: lane (r, g) holds rows row0 + 4g + j of column m*16 + r; write-through stores
-    if (4 * g < rows) {
+    stream_gemm<MT, 2, KCP>(X, ldx, wp, 0, H, Mc, xs, acc, [&] {
+      if (trace != nullptr) t_staged = wall_clock64();
+    });
+    if (trace != nullptr) t_done = wall_clock64();
+    // epilogue: lane (r, g) holds rows row0 + 4g + j of column m*16 + r; write-through (sc1)
+    // stores, 8 B where the group is whole and aligned, else one bf16 per element
+    if (4 * g < rw) {
       const int n = row0 + 4 * g;
+      const bool whole = (rw & 3) == 0;
 #pragma unroll
       for (int m = 0; m < MT; ++m) {
         const int row = m * 16 + r;
@@ -190,9 +209,17 @@ mlp_fused_kernel(const bf16_t* __restrict__ X, long ldx, const bf16_t* __restric
           bf16x4 v;
 #pragma unroll
           for (int j = 0; j < 4; ++j) v[j] = f2bf(silu(acc[0][m][j]) * acc[1][m][j]);
-          __hip_atomic_store((gu64*)(h + (long)row * I + n),
-                             __builtin_bit_cast(unsigned long long, v), __ATOMIC_RELAXED,
-                             __HIP_MEMORY_SCOPE_AGENT);
+          bf16_t* dst = h + (long)row * I + n;
+          if (whole) {
+            __hip_atomic_store((gu64*)dst, __builtin_bit_cast(unsigned long long, v),
+                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          } else {
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+              if (4 * g + j < rw)
+                __hip_atomic_store((gu16*)(dst + j), __builtin_bit_cast(unsigned short, v[j]),
+                                   __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          }
         }
       }
     }
@@ -201,8 +228,10 @@ mlp_fused_kernel(const bf16_t* __restrict__ X, long ldx, const bf16_t* __restric
     if (threadIdx.x == 0)
       __hip_atomic_fetch_add(cnt + (i * R) / (I / SK), 1, __ATOMIC_RELAXED,
                              __HIP_MEMORY_SCOPE_AGENT);
+    stamp_out();
     return;
   }
+  if (flags & 1) return;
   // ------------------------------------------------------------------ consumer: down, split-K
   const int c = blockIdx.x - P;
   const int ntiles = H / (WAVES * 2 * 16);
@@ -213,7 +242,8 @@ mlp_fused_kernel(const bf16_t* __restrict__ X, long ldx, const bf16_t* __restric
   const bf16_t* wp[2] = {Wd + (long)(nbase + r) * I + k0 + KLANE * g,
                          Wd + (long)(nbase + 16 + r) * I + k0 + KLANE * g};
   auto wait = [&] {
-    if (threadIdx.x == 0) {
+    if (trace != nullptr) t_staged = wall_clock64();      // consumer: weights issued
+    if (threadIdx.x == 0 && !(flags & 2)) {
       for (int it = 0;; ++it) {
         if (__hip_atomic_load(cnt + s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= per_split)
           break;
@@ -229,7 +259,10 @@ mlp_fused_kernel(const bf16_t* __restrict__ X, long ldx, const bf16_t* __restric
     __syncthreads();
   };
   f32x4 acc[2][MT];
-  stream_gemm<MT, 2, KCC>(h, I, wp, k0, krange, Mc, xs, acc, wait);
+  stream_gemm<MT, 2, KCC>(h, I, wp, k0, krange, Mc, xs, acc, [&] {
+    wait();
+    if (trace != nullptr) t_done = wall_clock64();        // consumer: wait passed
+  });
   // the split's last departing consumer re-arms both counters for the next launch (every
   // consumer of this split has passed its wait, and every producer of it has arrived)
   if (threadIdx.x == 0) {
@@ -249,11 +282,13 @@ mlp_fused_kernel(const bf16_t* __restrict__ X, long ldx, const bf16_t* __restric
       if (row < Mc) *reinterpret_cast<f32x4*>(o + (long)row * H + n) = acc[t][m];
     }
   }
+  stamp_out();
 }
 
 template <int MT>
 int launch_mt(const bf16_t* X, long ldx, const bf16_t* Wgu, const bf16_t* Wd, bf16_t* h,
-              float* part, int* sync, int M, int H, int I, int R, int SK, hipStream_t st) {
+              float* part, int* sync, int M, int H, int I, int R, int SK, int flags,
+              long long* trace, hipStream_t st) {
   constexpr int KCP = 256, KCC = 128;
   const size_t lds = 2ull * MT * 16 * (KCP + XPAD) * sizeof(bf16_t);
   static bool attr = false;
@@ -269,23 +304,61 @@ int launch_mt(const bf16_t* X, long ldx, const bf16_t* Wgu, const bf16_t* Wd, bf
     return e != nullptr ? atoi(e) : (1 << 20);
   }();
   hipLaunchKernelGGL((mlp_fused_kernel<MT, KCP, KCC>), dim3(P + C), dim3(256), lds, st, X, ldx,
-                     Wgu, Wd, h, part, sync, M, H, I, R, P, SK, spin_max);
+                     Wgu, Wd, h, part, sync, M, H, I, R, P, SK, spin_max, flags, trace);
   return (int)hipGetLastError();
 }
 
 }  // namespace
 
-// Shape gate shared by the launcher and the Python side: R (rows of gate / up per producer) is
-// 56 or 64, the producers cover the chip (>= 192), every down K-split is fed by whole
-// producers and is a whole number of 128-deep chunks, H a whole number of 128-column tiles.
-EIA_API int eia_mlp_fused_plan(int M, int H, int I, int sk, int* R_out) {
-  if (M < 1 || M > 80 || H % 256 || sk < 1 || I % sk) return EIA_BAD_SHAPE;
-  for (int R : {56, 64}) {
-    if (I % R || I / R < 192 || (I / sk) % R || (I / sk) % 128) continue;
-    if (R_out) *R_out = R;
-    return EIA_OK;
+// Shape gate shared by the launcher and the Python side.  R = rows of gate (and of up) per
+// producer, R / 4 per wave (<= 16).  Preferred: producers in whole rounds of 256 (one per CU)
+// and at least two rounds, so the consumers of the first round's splits find their h ready
+// when they are dispatched; *R_io in = a forced R (0 = choose), out = the R used.
+EIA_API int eia_mlp_fused_plan(int M, int H, int I, int sk, int* R_io) {
+  if (M < 1 || M > 80 || H % 256 || sk < 1 || I % sk || (I / sk) % 128) return EIA_BAD_SHAPE;
+  auto ok = [&](int R) {
+    return R >= 4 && R <= 64 && R % 4 == 0 && I % R == 0 && (I / sk) % R == 0;
+  };
+  const int want = R_io != nullptr ? *R_io : 0;
+  int best = 0;
+  if (want > 0) {
+    best = ok(want) ? want : 0;
+  } else {
+    for (int R = 64; R >= 4; R -= 4)      // largest R with >= 2 whole rounds of 256 producers
+      if (ok(R) && (I / R) % 256 == 0 && I / R >= 512) { best = R; break; }
+    if (best == 0)
+      for (int R = 64; R >= 4; R -= 4)    // else the largest R that still covers the chip
+        if (ok(R) && I / R >= 256) { best = R; break; }
   }
-  return EIA_BAD_SHAPE;
+  if (best == 0) return EIA_BAD_SHAPE;
+  if (R_io) *R_io = best;
+  return EIA_OK;
+}
+
+// Diagnostic entry point: flags / trace as in mlp_fused_kernel (scripts/bench_mlp.py).
+EIA_API int eia_mlp_fused_dbg(const void* X, long ldx, const void* Wgu, const void* Wd, void* h,
+                              float* part, int* sync, int M, int H, int I, int sk, int flags,
+                              void* trace, hipStream_t st) {
+  static const int r_env = [] {
+    const char* e = getenv("EIA_MLP_ROWS");
+    return e != nullptr ? atoi(e) : 0;
+  }();
+  int R = (flags >> 8) > 0 ? (flags >> 8) : r_env;   // flags bits 8+: forced R (bench)
+  flags &= 0xff;
+  if (int rc = eia_mlp_fused_plan(M, H, I, sk, &R)) return rc;
+  if (ldx % 8) return EIA_BAD_SHAPE;
+  auto x = static_cast<const bf16_t*>(X);
+  auto wgu = static_cast<const bf16_t*>(Wgu);
+  auto wd = static_cast<const bf16_t*>(Wd);
+  auto hh = static_cast<bf16_t*>(h);
+  auto tr = static_cast<long long*>(trace);
+  switch ((M + 15) / 16) {
+    case 1: return launch_mt<1>(x, ldx, wgu, wd, hh, part, sync, M, H, I, R, sk, flags, tr, st);
+    case 2: return launch_mt<2>(x, ldx, wgu, wd, hh, part, sync, M, H, I, R, sk, flags, tr, st);
+    case 3: return launch_mt<3>(x, ldx, wgu, wd, hh, part, sync, M, H, I, R, sk, flags, tr, st);
+    case 4: return launch_mt<4>(x, ldx, wgu, wd, hh, part, sync, M, H, I, R, sk, flags, tr, st);
+    default: return launch_mt<5>(x, ldx, wgu, wd, hh, part, sync, M, H, I, R, sk, flags, tr, st);
+  }
 }
 
 // X [M][ldx] (normalised hidden), Wgu [2I][H] = [gate; up] (contiguous), Wd [H][I] (contiguous);
@@ -293,20 +366,7 @@ EIA_API int eia_mlp_fused_plan(int M, int H, int I, int sk, int* R_out) {
 // sync: 2 sk + 1 ints, zero before the first launch (the kernel leaves them zero).
 EIA_API int eia_mlp_fused(const void* X, long ldx, const void* Wgu, const void* Wd, void* h,
                           float* part, int* sync, int M, int H, int I, int sk, hipStream_t st) {
-  int R = 0;
-  if (int rc = eia_mlp_fused_plan(M, H, I, sk, &R)) return rc;
-  if (ldx % 8) return EIA_BAD_SHAPE;
-  auto x = static_cast<const bf16_t*>(X);
-  auto wgu = static_cast<const bf16_t*>(Wgu);
-  auto wd = static_cast<const bf16_t*>(Wd);
-  auto hh = static_cast<bf16_t*>(h);
-  switch ((M + 15) / 16) {
-    case 1: return launch_mt<1>(x, ldx, wgu, wd, hh, part, sync, M, H, I, R, sk, st);
-    case 2: return launch_mt<2>(x, ldx, wgu, wd, hh, part, sync, M, H, I, R, sk, st);
-    case 3: return launch_mt<3>(x, ldx, wgu, wd, hh, part, sync, M, H, I, R, sk, st);
-    case 4: return launch_mt<4>(x, ldx, wgu, wd, hh, part, sync, M, H, I, R, sk, st);
-    default: return launch_mt<5>(x, ldx, wgu, wd, hh, part, sync, M, H, I, R, sk, st);
-  }
+  return eia_mlp_fused_dbg(X, ldx, Wgu, Wd, h, part, sync, M, H, I, sk, 0, nullptr, st);
 }
 
 // Host read of the bounded-spin flag (tests; a set flag means a consumer gave up waiting).

@@ -64,6 +64,7 @@ _SIGNATURES = {
     "eia_splitk_reduce": [P, I, I, I, P, P, L, S],
     "eia_mlp_fused": [P, L, P, P, P, P, IP, I, I, I, I, S],
     "eia_mlp_fused_plan": [I, I, I, I, P],
+    "eia_mlp_fused_dbg": [P, L, P, P, P, P, IP, I, I, I, I, I, P, S],
     "eia_mlp_fused_error": [IP, I, P],
     "eia_splitk_add_rmsnorm": [P, I, I, I, P, P, F, P, L, S],
     "eia_ar_alloc": [P, L],

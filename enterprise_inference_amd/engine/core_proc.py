@@ -133,6 +133,8 @@ def _run_op(engine, op: str):
         return {"num_steps": st.num_steps, "num_generation_tokens": st.num_generation_tokens,
                 "num_prompt_tokens": st.num_prompt_tokens, "num_blocks": engine.num_blocks,
                 "step_time_s": st.step_time_s,
+                "num_overlapped_steps": st.num_overlapped_steps,
+                "num_sync_steps": st.num_sync_steps,
                 "phase_times": dict(engine.phase_times),
                 "loop_times": dict(getattr(engine, "loop_times", {})),
                 "dist": _dist_info(engine)}

@@ -89,6 +89,10 @@ class EngineStats:
     num_steps: int = 0
     num_preemptions: int = 0
     step_time_s: float = 0.0
+    # overlapped-scheduling decisions (LLMEngine.step): launched ahead of the previous step's
+    # token read-back vs run synchronously because a row needed host-side token processing
+    num_overlapped_steps: int = 0
+    num_sync_steps: int = 0
 
 
 class LLMEngine:
@@ -313,6 +317,10 @@ class LLMEngine:
         t1 = time.time()
         sample_items = sched.decodes + [p for p in sched.prefills if p.samples]
         overlap = not any(self._needs_host_tokens(it.seq) for it in sample_items)
+        if overlap:
+            self.stats.num_overlapped_steps += 1
+        else:
+            self.stats.num_sync_steps += 1
         handle = self.profiler.step(
             lambda: self.executor.launch(self.scheduler.bm, sched, overlap))
         t2 = time.time()

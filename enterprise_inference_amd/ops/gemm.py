@@ -306,8 +306,10 @@ def linear(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = None
 # gate_up + SwiGLU and the split-K down projection in ONE launch (csrc/kernels/mlp_fused.hip):
 # 256 balanced producers (every CU streams the same gate/up bytes) hand h to the down
 # consumers split by split through arrival counters -- no second launch, no boundary, and the
-# 32 CUs the 4-pair SwiGLU grid left idle now stream.  EIA_FUSED_MLP=0 restores two launches.
-FUSED_MLP = os.environ.get("EIA_FUSED_MLP", "1") != "0"
+# 32 CUs the 4-pair SwiGLU grid left idle now stream.  Opt-in (EIA_FUSED_MLP=1): measured
+# level with the two launches in isolation and slower in the engine (docs/performance.md,
+# "Round 5: the decode MLP in one launch").
+FUSED_MLP = os.environ.get("EIA_FUSED_MLP", "0") == "1"
 _MLP_SYNC: dict = {}
 _MLP_SYNC_WORDS = 64
 
@@ -330,14 +332,16 @@ def mlp_sync_buffer(device: torch.device) -> Optional[torch.Tensor]:
 def mlp_fused_split(M: int, H: int, I: int) -> int:
     """Down-projection K split of the fused MLP (128-column tiles x split ~ 256 consumers), or
     0 when the shape has no fused form (eia_mlp_fused_plan)."""
-    if not FUSED_MLP or H % 128:
+    if H % 128:
         return 0
     sk = max(1, 256 // (H // 128))
     while sk > 1 and I % sk:
         sk //= 2
     if 2 * sk + 1 > _MLP_SYNC_WORDS:
         return 0
-    return sk if lib().eia_mlp_fused_plan(M, H, I, sk, None) == 0 else 0
+    import ctypes
+    r = ctypes.c_int(int(os.environ.get("EIA_MLP_ROWS", "0")))
+    return sk if lib().eia_mlp_fused_plan(M, H, I, sk, ctypes.byref(r)) == 0 else 0
 
 
 def mlp_fused_ok(x: torch.Tensor, w_gate_up: torch.Tensor, w_down: torch.Tensor) -> bool:

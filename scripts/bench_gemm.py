@@ -42,6 +42,21 @@ SHAPES = {  # name: (N, K, swiglu)
     "lm_head_405b_tp8": (16032, 16384, False),
     # Mistral-7B / Mixtral-8x7B LM heads (their attention projections are the 8B shapes)
     "lm_head_mistral": (32768, 4096, False), "lm_head_mixtral": (32000, 4096, False),
+    # rest of the deployed catalog (reference core/playbooks/deploy-inference-models.yml):
+    # Qwen2.5-32B (TP1, :909-977), DeepSeek-R1-Distill-Qwen-32B per TP2 rank (:1682-1768),
+    # CodeLlama-34B (TP1, :1258-1340), Falcon3-7B (head_dim 256, :1342-1425)
+    "qkv_qwen32b": (7168, 5120, False), "o_qwen32b": (5120, 5120, False),
+    "gate_up_qwen32b": (55296, 5120, True), "down_qwen32b": (5120, 27648, False),
+    "lm_head_qwen32b": (152064, 5120, False),
+    "qkv_qwen32b_tp2": (3584, 5120, False), "o_qwen32b_tp2": (5120, 2560, False),
+    "gate_up_qwen32b_tp2": (27648, 5120, True), "down_qwen32b_tp2": (5120, 13824, False),
+    "lm_head_qwen32b_tp2": (76032, 5120, False),
+    "qkv_codellama34b": (10240, 8192, False), "o_codellama34b": (8192, 8192, False),
+    "gate_up_codellama34b": (44032, 8192, True), "down_codellama34b": (8192, 22016, False),
+    "lm_head_codellama34b": (32000, 8192, False),
+    "qkv_falcon3_7b": (5120, 3072, False), "o_falcon3_7b": (3072, 3072, False),
+    "gate_up_falcon3_7b": (46080, 3072, True), "down_falcon3_7b": (3072, 23040, False),
+    "lm_head_falcon3_7b": (131072, 3072, False),
     # gate_up grid-size probes (8B K): 196 / 224 (the real shape) / 256 four-pair workgroups
     "gu_probe_196": (25088, 4096, True), "gu_probe_256": (32768, 4096, True),
 }

@@ -176,3 +176,23 @@ def test_overlapped_scheduling_stops_and_streams():
     assert final.outputs[0].finish_reason == "stop"
     assert final.outputs[0].token_ids == ref.outputs[0].token_ids[:4]
     assert streamed == final.outputs[0].token_ids       # no token lost or duplicated
+
+
+def test_overlap_decision_pinned():
+    """The headline workload (temperature sampling, ignore_eos, no logprobs / penalties / stop
+    strings) launches EVERY step ahead of the previous step's token read-back; a row that needs
+    host-side processing (logprobs) makes exactly its steps synchronous."""
+    d = tiny_config()
+    eng = _engine(d)
+    assert eng._overlap
+    prompts = [list(range(10 + i, 30 + i)) for i in range(4)]
+    eng.generate(prompt_token_ids=prompts,
+                 params=SamplingParams(max_tokens=12, temperature=1.0, ignore_eos=True, seed=3))
+    st = eng.stats
+    assert st.num_sync_steps == 0 and st.num_overlapped_steps == st.num_steps > 0
+    # a row with logprobs: its steps read the tokens back before the next launch
+    eng.generate(prompt_token_ids=prompts[:1],
+                 params=SamplingParams(max_tokens=5, temperature=1.0, ignore_eos=True, seed=3,
+                                       logprobs=1))
+    assert st.num_sync_steps >= 5
+    assert st.num_overlapped_steps + st.num_sync_steps == st.num_steps

@@ -139,7 +139,7 @@ def _mlp_ref(x, wgu, wd):
 
 @pytest.mark.parametrize("M", [1, 16, 33, 65, 80])
 @pytest.mark.parametrize("H,I", [(4096, 14336), (8192, 28672)])
-def test_mlp_fused(M, H, I):
+def test_mlp_fused(M, H, I, monkeypatch):
     """Fused decode MLP (gate_up + SwiGLU producers -> split-K down consumers in one launch)
     vs the fp32 reference; repeated launches (the counters re-arm themselves) and no consumer
     may have hit its spin bound."""
@@ -148,6 +148,7 @@ def test_mlp_fused(M, H, I):
     x = torch.randn(M, H, device=DEV, dtype=BF)
     wgu = (torch.randn(2 * I, H, device=DEV) * H ** -0.5).to(BF)
     wd = (torch.randn(H, I, device=DEV) * I ** -0.5).to(BF)
+    monkeypatch.setattr(gemm, "FUSED_MLP", True)
     sk = gemm.mlp_fused_split(M, H, I)
     assert sk > 0 and gemm.mlp_fused_ok(x, wgu, wd)
     ref = _mlp_ref(x, wgu, wd)
@@ -185,11 +186,12 @@ def test_mlp_fused_graph_replay():
     assert gemm.mlp_fused_error(x.device, gemm.mlp_fused_split(M, H, I)) == 0
 
 
-def test_llama_mlp_takes_fused_path():
+def test_llama_mlp_takes_fused_path(monkeypatch):
     """The Llama MLP module routes a decode batch through the fused kernel at TP = 1 and the
     result (split-K partials) matches the two-launch form."""
     from enterprise_inference_amd.models.llama import LlamaMLP
     from enterprise_inference_amd.ops import gemm
+    monkeypatch.setattr(gemm, "FUSED_MLP", True)
     torch.manual_seed(9)
     mlp = LlamaMLP(4096, 14336, "silu", BF, DEV)
     mlp.gate_up_proj.weight.data.normal_(0, 4096 ** -0.5)

@@ -93,13 +93,19 @@ def _make_cache(nb, Hkv, bs, D, fill=False):
 @pytest.mark.parametrize("D,Hq,Hkv,bias,qkn", [(128, 32, 8, False, False), (128, 40, 8, True, False),
                                                 (64, 12, 12, False, False), (128, 16, 8, False, True),
                                                 (256, 12, 4, False, False)])
-def test_rope_qkv_cache(D, Hq, Hkv, bias, qkn):
+@pytest.mark.parametrize("T,bs,nb,contig", [(37, 16, 8, False), (200, 16, 16, False),
+                                            (300, 128, 4, True)])
+def test_rope_qkv_cache(D, Hq, Hkv, bias, qkn, T, bs, nb, contig):
+    """T >= 64 runs the tiled prefill kernel (lane = token V^T stores), T < 64 the per-token
+    one; both against the fp32 reference, random and prefill-like consecutive slots."""
     from enterprise_inference_amd.ops import rotary
     torch.manual_seed(0)
-    T, bs, nb = 37, 16, 8
     qkv = torch.randn(T, (Hq + 2 * Hkv) * D, device=DEV, dtype=BF)
     pos = torch.randint(0, 4000, (T,), device=DEV, dtype=torch.int32)
-    slots = torch.randperm(nb * bs, device=DEV)[:T].to(torch.int32)
+    if contig:      # a prompt's tokens fill consecutive slots from a block start (+ an offset)
+        slots = (torch.arange(T, device=DEV) + 40).to(torch.int32)
+    else:
+        slots = torch.randperm(nb * bs, device=DEV)[:T].to(torch.int32)
     slots[3] = -1
     rc = rotary.RotaryCache(D, 4096, 500000.0, {"rope_type": "llama3", "factor": 8.0,
                                                 "low_freq_factor": 1.0, "high_freq_factor": 4.0,
