@@ -122,11 +122,16 @@ EIA_DEV void store_tile(const f32x4 (&acc)[NT][MT], int mode, void* __restrict__
 // LOADER: one extra wave stages the X chunks into LDS (one chunk ahead) while the WAVES
 // compute waves only stream W: their in-order vmcnt queue then holds nothing but weight
 // loads, so the weight pipeline stays S-1 chunks deep without X lookahead registers.
-// PACKED: W is stored tile-major (pack_weight): for each 16-row tile and 128-deep K block,
+// PK: 0 = plain rows; 1 = W stored tile-major (pack_weight): for each 16-row tile and 128-deep K block,
 // the four 64-lane fragment loads are consecutive 1 KiB runs, so a wave streams its tile's
 // whole K range as one contiguous region (8 full cache lines per load instruction instead of
 // 64-B pieces of 16 rows 8 KiB apart).
-template <int MT, int NT, int WAVES, int S, bool GROUPED, int KC, bool LOADER, bool PACKED>
+// 2 = workgroup-packed (pack_weight_wg): a workgroup's WAVES x NT tiles are interleaved per
+// 128-deep K block ([group][kb][wave][tile][step][lane][8]), so the workgroup reads ONE
+// sequential stream (a 16-32 KiB run per chunk) instead of 16-row x 64-B pieces of 2 x WAVES
+// rows 8 KiB apart: a read-only probe streams 5.7 TB/s with one stream per workgroup against
+// 4.1-5.3 for the row pattern (profiles/probe_stream_r5.log).
+template <int MT, int NT, int WAVES, int S, bool GROUPED, int KC, bool LOADER, int PK>
 __global__ void __launch_bounds__(WAVES * 64 + (LOADER ? 64 : 0),
                                   ((KC == 128 && WAVES == 4) || LOADER) ? 2 : 1)
 gemm_skinny_kernel(const bf16_t* __restrict__ X, long ldx, const bf16_t* __restrict__ W, long ldw,
@@ -162,20 +167,26 @@ gemm_skinny_kernel(const bf16_t* __restrict__ X, long ldx, const bf16_t* __restr
   int nbase;
   // element offset of row `row0 + r` (row0 a multiple of 16) at k0 for this lane
   auto wrow = [&](int row0) -> long {
-    if constexpr (PACKED) return (long)row0 * ldw + (long)(k0 / 128) * 2048 + lane * 8;
+    if constexpr (PK == 1) return (long)row0 * ldw + (long)(k0 / 128) * 2048 + lane * 8;
     return (long)(row0 + r) * ldw + k0 + KLANE * g;
   };
+  // PK 2: this wave's tile t at K block kb = group base + kb * (WAVES NT 2048) + (wave NT + t) 2048
+  auto wgp = [&](int t) -> long {
+    constexpr int ROWS = WAVES * NT * 16;     // SwiGLU: WAVES*16 gate + WAVES*16 up rows
+    return (long)blockIdx.x * ROWS * ldw + (long)(k0 / 128) * (WAVES * NT * 2048) +
+           (long)(wave * NT + t) * 2048 + lane * 8;
+  };
   // strides (elements) between a lane's fragments: MFMA step s, 128-deep super-step
-  constexpr int WS_STEP = PACKED ? 512 : KSTEP;
-  constexpr int WS_SUPER = PACKED ? 2048 : 128;
+  constexpr int WS_STEP = PK ? 512 : KSTEP;
+  constexpr int WS_SUPER = PK == 2 ? WAVES * NT * 2048 : (PK ? 2048 : 128);
   if (NT == 2 && mode == MODE_SWIGLU) {
     nbase = blockIdx.x * (WAVES * 16) + wave * 16;      // output column block
-    wp[0] = W + wrow(nbase);
-    wp[NT - 1] = W + wrow(inter + nbase);
+    wp[0] = W + (PK == 2 ? wgp(0) : wrow(nbase));
+    wp[NT - 1] = W + (PK == 2 ? wgp(1) : wrow(inter + nbase));
   } else {
     nbase = blockIdx.x * (WAVES * NT * 16) + wave * (NT * 16);
 #pragma unroll
-    for (int t = 0; t < NT; ++t) wp[t] = W + wrow(nbase + 16 * t);
+    for (int t = 0; t < NT; ++t) wp[t] = W + (PK == 2 ? wgp(t) : wrow(nbase + 16 * t));
   }
 
   constexpr int XV = MT * 16 * (KC / 8);                // 16-B vectors per X chunk
@@ -565,7 +576,7 @@ splitk_add_rmsnorm_kernel(const float* __restrict__ part, int sk_rt, int M, int 
 }
 
 template <int MT, int NT, int WAVES, int S, bool GROUPED, int KC, bool LOADER = false,
-          bool PACKED = false>
+          int PACKED = 0>
 int launch_cfg(const bf16_t* X, long ldx, const bf16_t* W, long ldw, const bf16_t* bias, void* out,
                long ldo, int M, int N, int K, int sk, int mode, int experts, const int* offs,
                const int* row_idx, long w_estride, hipStream_t st) {
@@ -660,6 +671,24 @@ int launch_mt(int cfg, const bf16_t* X, long ldx, const bf16_t* W, long ldw, con
       }
 #undef EIA_GL
     }
+    if (cfg & 1024) {  // workgroup-packed weights (pack_weight_wg), register-staged, 2 stages
+#define EIA_CFGW(NT_, W_, S_, KC_)                                                            \
+  return launch_cfg<MT, NT_, W_, S_, GROUPED, KC_, false, 2>(X, ldx, W, ldw, bias, out, ldo, M, N, \
+                                                             K, sk, mode, experts, offs, row_idx,   \
+                                                             w_estride, st)
+      if constexpr (!GROUPED) {
+        switch (cfg & ~1024) {
+          case 1: EIA_CFGW(2, 2, 2, 256);
+          case 3: EIA_CFGW(2, 4, 2, 256);
+          case 17: EIA_CFGW(2, 2, 2, 128);
+          case 19: EIA_CFGW(2, 4, 2, 128);
+          case 512 + 17: EIA_CFGW(2, 3, 2, 128);
+          default: break;
+        }
+      }
+#undef EIA_CFGW
+      return EIA_BAD_SHAPE;
+    }
     if (cfg & 512) {   // 3 waves: Llama-8B QKV (6144 rows = 64 x 96, x split-K 4 = 256 workgroups)
       switch (cfg & 31) {
         case 0: EIA_CFG(1, 3, 2, 256);
@@ -706,7 +735,7 @@ int launch_mt(int cfg, const bf16_t* X, long ldx, const bf16_t* W, long ldw, con
       default: break;
     }
 #define EIA_CFGP(NT_, W_, S_, KC_, L_)                                                      \
-  return launch_cfg<MT, NT_, W_, S_, GROUPED, KC_, L_, true>(X, ldx, W, ldw, bias, out, ldo, M, \
+  return launch_cfg<MT, NT_, W_, S_, GROUPED, KC_, L_, 1>(X, ldx, W, ldw, bias, out, ldo, M, \
                                                             N, K, sk, mode, experts, offs,     \
                                                             row_idx, w_estride, st)
     // bit 6: tile-packed weights, for the configurations the decode tables use
@@ -768,7 +797,12 @@ int check_shape(int N, int K, int sk, int mode, int cfg) {
   const int nt = (cfg & 1) ? 2 : 1;
   const int waves = (cfg & 512) ? 3 : (cfg & 256) ? 7 : (cfg & 2) ? 4 : 2;
   const int kc = (cfg & 16) ? 128 : 256;
-  if (sk < 1 || cfg < 0 || (cfg & ~(16 | 32 | 64 | 128 | 256 | 512)) > 11 || K % (sk * kc) != 0)
+  if (sk < 1 || cfg < 0 || (cfg & ~(16 | 32 | 64 | 128 | 256 | 512 | 1024)) > 11 ||
+      K % (sk * kc) != 0)
+    return EIA_BAD_SHAPE;
+  // workgroup-packed: the forms built above (two 16-row tiles per wave, 2 stages)
+  if ((cfg & 1024) && (cfg & ~1024) != 1 && (cfg & ~1024) != 3 && (cfg & ~1024) != 17 &&
+      (cfg & ~1024) != 19 && (cfg & ~1024) != 512 + 17)
     return EIA_BAD_SHAPE;
   // 3-wave form: register-staged, plain layout, no SwiGLU pairing, 2-3 stages
   if ((cfg & 512) && ((cfg & (2 | 8 | 32 | 64 | 128 | 256)) || mode == MODE_SWIGLU))
@@ -799,6 +833,8 @@ int check_shape(int N, int K, int sk, int mode, int cfg) {
 // bit 7 -> LDS-DMA ring kernel (with bits 1 and 4; bits 2-3 = ring depth - 2)
 // bit 8 -> 7 waves of (gate, up) pairs per workgroup (SwiGLU only; cfg 273 = + bits 0 and 4):
 //          70B's 1792 pairs are exactly 256 workgroups, where 4-wave workgroups leave 448
+// bit 10 -> workgroup-packed W (pack_weight_wg; ldw must be K) with cfg 1, 3, 17, 19 or 529:
+//          each workgroup streams its rows as one sequential run
 // bit 9 -> 3 waves per workgroup (+ bits 0, 2, 4): Llama-8B's QKV (6144 rows) as 64 x 96-row
 //          tiles x split-K 4 = 256 workgroups, where 4-wave (128-row) tiles leave 192 -- a
 //          decode GEMM streams at a per-CU rate (~20 GB/s), so idle CUs are lost bandwidth
@@ -808,6 +844,7 @@ EIA_API int eia_gemm_skinny(const void* X, long ldx, const void* W, long ldw, co
   if (M < 1 || M > 128) return EIA_BAD_SHAPE;
   if (int rc = check_shape(N, K, sk, mode, cfg)) return rc;
   if (!(cfg & 896) && ((kSpillCfg[(M + 15) / 16] >> (cfg & 63)) & 1ull)) return EIA_BAD_SHAPE;
+  if ((cfg & 1024) && ldw != K) return EIA_BAD_SHAPE;           // packed over the full K
   // 7-wave form: cfg 273 only (KC 128, 2 stages), spill-free up to 4 row tiles (M <= 64); at
   // 7 waves two share a SIMD, so the register budget is 256
   if ((cfg & 256) && (cfg != 256 + 17 || M > 64)) return EIA_BAD_SHAPE;

@@ -45,6 +45,8 @@ CFGS = tuple(range(12)) + tuple(range(16, 28)) + (50, 51, 54, 55, 58, 59) + \
 PACKED_CFGS = tuple(64 + c for c in (1, 2, 3, 7, 17, 18, 19, 22, 23, 51, 55, 146, 147, 150, 151, 154, 155))
 # bit7: LDS-DMA ring kernel, 4 waves, KC 128: 146 | (NT-1) | (depth-2) << 2 (+64 packed)
 GLDS_CFGS = (146, 147, 150, 151, 154, 155)
+# bit10: workgroup-packed weights (pack_weight_wg) for the forms the decode tables use
+WGPACK_CFGS = tuple(1024 + c for c in (1, 3, 17, 19, 529))
 GLDS_PACKED_CFGS = tuple(c + 64 for c in GLDS_CFGS)
 
 
@@ -68,21 +70,24 @@ def m_bucket(M: int) -> int:
     return (M + 15) // 16
 
 
-def _load_tuning() -> dict:
-    """(m_tiles, N, K, swiglu) -> (cfg, sk), measured by scripts/bench_gemm.py --tune."""
+def _load_tuning(section: str = "entries") -> dict:
+    """(m_tiles, N, K, swiglu) -> (cfg, sk), measured by scripts/bench_gemm.py --tune.
+    ``wg_entries``: the workgroup-packed picks (cfg bit 10), used for weights that carry a
+    packed copy (``attach_wg_packed``) where they beat the plain pick."""
     try:
         with open(TUNING_FILE) as f:
             raw = json.load(f)
     except (OSError, ValueError):
         return {}
     out = {}
-    for k, v in raw.get("entries", {}).items():
+    for k, v in raw.get(section, {}).items():
         mt, n, kk, sw = (int(x) for x in k.split(","))
         out[(mt, n, kk, bool(sw))] = (int(v[0]), int(v[1]))
     return out
 
 
 _TUNED = _load_tuning()
+_TUNED_WG = _load_tuning("wg_entries")
 
 
 # (M-tile bucket -> cfgs whose kernel spills registers; mirrors kSpillCfg in gemm_skinny.hip)
@@ -117,6 +122,30 @@ def pack_weight(w: torch.Tensor) -> torch.Tensor:
     assert N % 16 == 0 and K % 128 == 0, (N, K)
     return w.reshape(N // 16, 16, K // 128, 4, 4, 8).permute(0, 2, 3, 4, 1, 5).contiguous() \
         .view(N, K)
+
+
+def pack_weight_wg(w: torch.Tensor, cfg: int, swiglu: bool = False) -> torch.Tensor:
+    """[N, K] row-major -> the workgroup-packed layout of cfg bit 10 (same shape and dtype): for
+    each workgroup's row group and 128-deep K block, its waves' tiles are adjacent 2 KiB runs
+    ([group][kb][wave][tile][step s][lane g][lane r][8]; lane (r, g) of MFMA step s holds
+    k = 8 g + 32 s + j, the kernel's k permutation), so one workgroup reads one sequential run.
+    SwiGLU (w = [gate; up], 2I rows): a wave's tile 0 is its 16 gate rows, tile 1 the matching
+    up rows."""
+    N, K = w.shape
+    waves = cfg_waves(cfg)
+    nt = 2 if cfg & 1 else 1
+    assert K % 128 == 0, (N, K)
+    if swiglu:
+        I = N // 2
+        assert nt == 2 and I % (waves * 16) == 0, (N, cfg)
+        g = w[:I].reshape(I // (waves * 16), waves, 1, 16, K // 128, 4, 4, 8)
+        u = w[I:].reshape(I // (waves * 16), waves, 1, 16, K // 128, 4, 4, 8)
+        t = torch.cat([g, u], 2)                         # [grp, wave, tile, r, kb, s, g, j]
+    else:
+        rows = waves * nt * 16
+        assert N % rows == 0, (N, cfg)
+        t = w.reshape(N // rows, waves, nt, 16, K // 128, 4, 4, 8)
+    return t.permute(0, 4, 1, 2, 5, 6, 3, 7).contiguous().view(N, K)
 
 
 def unpack_weight(p: torch.Tensor) -> torch.Tensor:
@@ -154,6 +183,68 @@ def choose(M: int, N: int, K: int, swiglu: bool = False):
     return cfg, heuristic_splitk(N, K, cfg, swiglu)
 
 
+def choose_packed(M: int, N: int, K: int, swiglu: bool, w: torch.Tensor):
+    """(cfg, sk, packed weight) when ``w`` carries the workgroup-packed layout the table's
+    packed pick for this shape and batch needs (attach_wg_packed), else None."""
+    d = getattr(w, "_eia_wg", None)
+    if not d:
+        return None
+    e = _TUNED_WG.get((m_bucket(M), N, K, swiglu))
+    if e is None:
+        return None
+    wp = d.get((cfg_waves(e[0]), swiglu))
+    if wp is None or not valid(N, K, swiglu, e[0], e[1], M=M):
+        return None
+    return e[0], e[1], wp
+
+
+def wg_layouts(N: int, K: int, swiglu: bool, max_m: int = MAX_M):
+    """Workgroup-packed layouts (waves) the table's packed picks for this shape use, over the
+    batch buckets up to ``max_m``."""
+    return sorted({cfg_waves(c) for (mt, n, k, sw), (c, _) in _TUNED_WG.items()
+                   if n == N and k == K and sw == swiglu and mt <= m_bucket(max_m) and c & 1024})
+
+
+def attach_wg_packed(model: torch.nn.Module, budget_bytes: int, max_m: int = MAX_M) -> int:
+    """Give every decode GEMM weight whose shape has workgroup-packed table picks a packed copy
+    (``w._eia_wg[(waves, swiglu)]``) -- the decode kernels then read each workgroup's rows as
+    one sequential stream; prefill keeps the row-major weight for hipBLASLt.  All or nothing:
+    when the copies would exceed ``budget_bytes`` (e.g. a 70B on one GPU) nothing is packed.
+    Returns the bytes added."""
+    from ..models import layers as L
+    plan = []
+    for mod in model.modules():
+        w = getattr(mod, "weight", None)
+        if not isinstance(w, torch.Tensor) or w.dim() != 2 or w.dtype != torch.bfloat16 or \
+                not w.is_cuda or not w.is_contiguous():
+            continue
+        if not isinstance(mod, (L.ColumnParallelLinear, L.RowParallelLinear, L.ParallelLMHead,
+                                L.ReplicatedLinear)):
+            continue
+        N, K = w.shape
+        forms = [False]
+        if isinstance(mod, L.MergedColumnParallelLinear) and len(mod.out_sizes) == 2:
+            forms.append(True)
+        for sw in forms:
+            for waves in wg_layouts(N, K, sw, max_m):
+                plan.append((w, waves, sw))
+    seen = set()
+    total = 0
+    for w, waves, sw in plan:
+        if (id(w), waves, sw) not in seen:
+            seen.add((id(w), waves, sw))
+            total += w.numel() * w.element_size()
+    if total == 0 or total > budget_bytes:
+        return 0
+    for w, waves, sw in plan:
+        d = w.__dict__.setdefault("_eia_wg", {})
+        if (waves, sw) in d:
+            continue
+        cfg = 1024 + {2: 17, 3: 529, 4: 19}[waves]
+        d[(waves, sw)] = pack_weight_wg(w.data, cfg, sw)
+    return total
+
+
 def choose_splitk(N: int, K: int, swiglu: bool = False, M: int = 64) -> int:
     return choose(M, N, K, swiglu)[1]
 
@@ -167,6 +258,8 @@ def skinny_ok(x: torch.Tensor, w: torch.Tensor, swiglu: bool = False) -> bool:
         return False
     if x.stride(1) != 1 or w.stride(1) != 1 or x.stride(0) % 8 or w.stride(0) % 8:
         return False
+    if choose_packed(M, N, K, swiglu, w) is not None:
+        return True
     cfg, sk = choose(M, N, K, swiglu)
     return cfg >= 0 and valid(N, K, swiglu, cfg, sk, M=M)
 
@@ -207,7 +300,11 @@ def skinny(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = None
     M, K = x.shape
     N = w.shape[0]
     if cfg is None:
-        cfg, sk = choose(M, N, K, False)
+        pk = choose_packed(M, N, K, False, w)
+        if pk is not None:
+            cfg, sk, w = pk
+        else:
+            cfg, sk = choose(M, N, K, False)
     if sk == 1:
         out = torch.empty(M, N, dtype=torch.bfloat16, device=x.device)
         check(lib().eia_gemm_skinny(ptr(x), x.stride(0), ptr(w), w.stride(0), ptr(bias), ptr(out),
@@ -229,7 +326,11 @@ def linear_f32(x: torch.Tensor, w: torch.Tensor) -> Optional[torch.Tensor]:
         return None
     M, K = x.shape
     N = w.shape[0]
-    cfg, sk = choose(M, N, K, False)
+    pk = choose_packed(M, N, K, False, w)
+    if pk is not None and pk[1] == 1:
+        cfg, sk, w = pk
+    else:
+        cfg, sk = choose(M, N, K, False)
     if sk != 1:
         return None
     out = torch.empty(M, N, dtype=torch.float32, device=x.device)
@@ -243,7 +344,11 @@ def swiglu_gemm(x: torch.Tensor, w_gate_up: torch.Tensor, cfg: Optional[int] = N
     M, K = x.shape
     N = w_gate_up.shape[0]
     if cfg is None:
-        cfg = choose(M, N, K, True)[0]
+        pk = choose_packed(M, N, K, True, w_gate_up)
+        if pk is not None:
+            cfg, _, w_gate_up = pk
+        else:
+            cfg = choose(M, N, K, True)[0]
     out = torch.empty(M, N // 2, dtype=torch.bfloat16, device=x.device)
     check(lib().eia_gemm_skinny(ptr(x), x.stride(0), ptr(w_gate_up), w_gate_up.stride(0), None,
                                 ptr(out), out.stride(0), M, N, K, 1, MODE_SWIGLU, cfg, stream(x)),

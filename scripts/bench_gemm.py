@@ -132,16 +132,26 @@ def main():
     ap.add_argument("--all", action="store_true", help="print every timed (cfg, sk) variant")
     ap.add_argument("--packed", action="store_true",
                     help="sweep the tile-packed-weight configurations (cfg bit 6)")
+    ap.add_argument("--wgpack", action="store_true",
+                    help="sweep the workgroup-packed forms (cfg bit 10) beside the plain ones")
     a = ap.parse_args()
-    tuned = {}
+    tuned, tuned_wg = {}, {}
     if a.tune and os.path.exists(gemm.TUNING_FILE):
-        tuned = json.load(open(gemm.TUNING_FILE)).get("entries", {})
+        raw = json.load(open(gemm.TUNING_FILE))
+        tuned, tuned_wg = raw.get("entries", {}), raw.get("wg_entries", {})
     for name in a.shapes:
         N, K, swiglu = SHAPES[name]
         wbytes = N * K * 2
         pool = max(2, int(600e6 // wbytes) + 1)
         ws = [(torch.randn(N, K, device="cuda") * 0.02).to(torch.bfloat16) for _ in range(pool)]
         wps = [gemm.pack_weight(w) for w in ws] if a.packed else ws
+        wgp = {}    # waves -> workgroup-packed copies of the pool (cfg bit 10)
+
+        def wg_pool(cfg):
+            key = gemm.cfg_waves(cfg)
+            if key not in wgp:
+                wgp[key] = [gemm.pack_weight_wg(w, cfg, swiglu) for w in ws]
+            return wgp[key]
         buckets = {}   # --tune: m-tile bucket -> summed times over its --m rows
         for M in a.m:
             x = torch.randn(M, K, device="cuda", dtype=torch.bfloat16)
@@ -157,6 +167,15 @@ def main():
                 cands = [(c, sk) for c in gemm.PACKED_CFGS for sk in {s for _, s in cands}
                          if gemm.valid(N, K, swiglu, c, sk, M=M)
                          and (N // gemm.cfg_rows(c)) * sk <= 4096]
+            if a.wgpack:
+                # the table's plain pick against the workgroup-packed forms at every split
+                # (--tune --wgpack: the plain entries stay, the packed picks go to wg_entries)
+                pc, ps = gemm.choose(M, N, K, swiglu)
+                cands = ([(pc, ps)] if pc >= 0 else []) + [
+                    (c, sk) for c in gemm.WGPACK_CFGS for sk in (1, 2, 3, 4, 6, 8, 12, 16)
+                    if gemm.valid(N, K, swiglu, c, sk, M=M)
+                    and K % (sk * gemm.cfg_kc(c)) == 0 and (N // gemm.cfg_rows(c)) * sk <= 4096
+                    and (N // gemm.cfg_rows(c)) * sk >= 64]
             if not cands:
                 print(json.dumps({"shape": name, "M": M, "hipblaslt_us": round(tb, 2),
                                   "hipblaslt_TBps": round(wbytes / tb / 1e6, 2),
@@ -164,12 +183,12 @@ def main():
                 continue
             results = []
             for cfg, sk in cands:
+                src = wg_pool(cfg) if cfg & 1024 else (wps if cfg & 64 else ws)
                 if swiglu:
-                    f = lambda i, cfg=cfg: gemm.swiglu_gemm(
-                        x, (wps if cfg & 64 else ws)[i % pool], cfg=cfg)
+                    f = lambda i, cfg=cfg, src=src: gemm.swiglu_gemm(x, src[i % pool], cfg=cfg)
                 else:
-                    f = lambda i, cfg=cfg, sk=sk: gemm.skinny(
-                        x, (wps if cfg & 64 else ws)[i % pool], cfg=cfg, sk=sk)
+                    f = lambda i, cfg=cfg, sk=sk, src=src: gemm.skinny(x, src[i % pool], cfg=cfg,
+                                                                       sk=sk)
                 results.append((graph_time(f, a.iters), cfg, sk))
             results.sort(key=lambda r_: r_[0])
             to, cfg, sk = results[0]
@@ -203,21 +222,38 @@ def main():
                     e[1] += 1
         for mt, b in sorted(buckets.items()):
             key = f"{mt},{N},{K},{int(swiglu)}"
+            if a.wgpack:
+                # packed pick: the best packed variant timed at every row of the bucket, kept
+                # when it beats the plain entry (timed in the same run) by >= 1 %
+                full = sorted((v[0], c) for c, v in b["var"].items()
+                              if v[1] == len(b["rows"]))
+                plain = [(t, c) for t, c in full if not c[0] & 1024]
+                packed = [(t, c) for t, c in full if c[0] & 1024]
+                ref_t = plain[0][0] if plain else b["hip"]
+                if packed and packed[0][0] < 0.99 * ref_t:
+                    tuned_wg[key] = list(packed[0][1])
+                else:
+                    tuned_wg.pop(key, None)
+                print(json.dumps({"shape": name, "bucket": mt, "rows": b["rows"],
+                                  "wg_pick": tuned_wg.get(key), "plain_sum_us": round(ref_t, 2),
+                                  "wg_sum_us": round(packed[0][0], 2) if packed else None}),
+                      flush=True)
+                continue
             tuned[key], to, full = bucket_pick(b)
             print(json.dumps({"shape": name, "bucket": mt, "rows": b["rows"], "pick": tuned[key],
                               "sum_us": round(to, 2), "hipblaslt_sum_us": round(b["hip"], 2),
                               "runner_up": [(round(t, 1), c) for t, c in full[1:3]]}), flush=True)
-        del ws, wps
+        del ws, wps, wgp
         torch.cuda.empty_cache()
     if a.tune:
+        table = {"device": torch.cuda.get_device_name(0), "entries": tuned,
+                 "wg_entries": tuned_wg}
         with open(gemm.TUNING_FILE, "w") as f:
-            json.dump({"device": torch.cuda.get_device_name(0), "entries": tuned}, f, indent=0,
-                      sort_keys=True)
+            json.dump(table, f, indent=0, sort_keys=True)
         print("wrote", gemm.TUNING_FILE)
         if a.out:
             with open(a.out, "w") as f:
-                json.dump({"device": torch.cuda.get_device_name(0), "entries": tuned}, f, indent=0,
-                          sort_keys=True)
+                json.dump(table, f, indent=0, sort_keys=True)
         if a.persist:
             from enterprise_inference_amd.utils.cache_dir import persist
             print("persisted", persist(gemm.TUNING_FILE, "gemm_tuning.json"))

@@ -202,3 +202,34 @@ def test_llama_mlp_takes_fused_path(monkeypatch):
     two = mlp.down_proj(mlp.gate_up_proj.forward_act_and_mul(x), defer_reduce=True)
     two = two.materialize() if isinstance(two, gemm.SplitK) else two
     _check(y.materialize(), two.float(), "fused vs two launches")
+
+
+@pytest.mark.parametrize("M", [1, 33, 65, 80])
+@pytest.mark.parametrize("N,K,swiglu", [(6144, 4096, False), (4096, 4096, False),
+                                        (4096, 14336, False), (28672, 4096, True)])
+def test_skinny_wg_packed(M, N, K, swiglu):
+    """Workgroup-packed weights (cfg bit 10, pack_weight_wg): same product as the plain rows,
+    for every packed form and split the shape admits."""
+    from enterprise_inference_amd.ops import gemm
+    torch.manual_seed(M + N + K)
+    x = torch.randn(M, K, device=DEV, dtype=BF)
+    w = (torch.randn(N, K, device=DEV) * K ** -0.5).to(BF)
+    if swiglu:
+        I = N // 2
+        ref = F.silu(_ref(x, w[:I])) * _ref(x, w[I:])
+    else:
+        ref = _ref(x, w)
+    n = 0
+    for cfg in gemm.WGPACK_CFGS:
+        wp = None
+        for sk in (1, 2, 4, 8):
+            if not gemm.valid(N, K, swiglu, cfg, sk, M=M) or K % (sk * gemm.cfg_kc(cfg)):
+                continue
+            if swiglu and sk != 1:
+                continue
+            if wp is None:
+                wp = gemm.pack_weight_wg(w, cfg, swiglu)
+            out = gemm.swiglu_gemm(x, wp, cfg=cfg) if swiglu else gemm.skinny(x, wp, cfg=cfg, sk=sk)
+            _check(out, ref, f"M={M} N={N} K={K} cfg={cfg} sk={sk}")
+            n += 1
+    assert n > 0

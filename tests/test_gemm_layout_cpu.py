@@ -1,4 +1,5 @@
 """Tile-packed weight layout of the skinny GEMM (cfg bit 6): pure index math, CPU."""
+import pytest
 import torch
 
 from enterprise_inference_amd.ops import gemm
@@ -39,3 +40,30 @@ def test_seven_wave_swiglu_cfg_rules():
     assert not gemm.valid(2 * 11008, 4096, True, 273, 1, M=35)        # 688 pairs: not 7 | pairs
     assert not gemm.valid(2 * 28672, 8192, True, 257, 1, M=35)        # only the KC-128 form
     assert (28672 // 16) // 7 == 256
+
+
+@pytest.mark.parametrize("cfg,swiglu,N", [(1024 + 3, False, 256), (1024 + 3, True, 256),
+                                          (1024 + 529, False, 192), (1024 + 17, False, 128)])
+def test_pack_weight_wg_matches_kernel_addressing(cfg, swiglu, N):
+    """pack_weight_wg puts element (row, k) where gemm_skinny.hip's PK = 2 path reads it:
+    group * ROWS * K + kb * (WAVES NT 2048) + (wave NT + tile) 2048 + 512 s + 8 lane + j, with
+    lane (r, g) of MFMA step s holding k = 128 kb + 8 g + 32 s + j."""
+    import torch
+    from enterprise_inference_amd.ops import gemm
+    K = 256
+    w = torch.arange(N * K, dtype=torch.float32).view(N, K)
+    p = gemm.pack_weight_wg(w, cfg, swiglu).view(-1)
+    waves, nt = gemm.cfg_waves(cfg), 2
+    rows = waves * nt * 16
+    ngrp = (N // 2) // (waves * 16) if swiglu else N // rows
+    g_, kb, wv, t, s, lane, j = torch.meshgrid(
+        torch.arange(ngrp), torch.arange(K // 128), torch.arange(waves), torch.arange(nt),
+        torch.arange(4), torch.arange(64), torch.arange(8), indexing="ij")
+    r, g = lane % 16, lane // 16
+    off = g_ * rows * K + kb * (waves * nt * 2048) + (wv * nt + t) * 2048 + s * 512 + lane * 8 + j
+    if swiglu:
+        row = g_ * waves * 16 + wv * 16 + r + t * (N // 2)
+    else:
+        row = g_ * rows + wv * nt * 16 + t * 16 + r
+    k = kb * 128 + 8 * g + 32 * s + j
+    assert torch.equal(p[off.reshape(-1)], w[row.reshape(-1), k.reshape(-1)])

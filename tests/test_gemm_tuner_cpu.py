@@ -33,3 +33,23 @@ def test_bucket_pick_routes_to_hipblaslt():
     b["var"][(24, 1)][0] = 101.0                  # within the 2 % margin: keep the skinny kernel
     assert bp(b)[0] == [24, 1]
     assert bp({"rows": [1], "hip": 5.0, "var": {}})[0] == [-1, 1]
+
+
+def test_wg_packed_selection(monkeypatch):
+    """A weight that carries a workgroup-packed copy takes the table's packed pick for its
+    batch bucket; without the copy (or without a packed pick) the plain entry stands."""
+    import torch
+    from enterprise_inference_amd.ops import gemm
+    N, K = 4096, 4096
+    monkeypatch.setattr(gemm, "_TUNED_WG", {(5, N, K, False): (1024 + 17, 4),
+                                            (2, N, K, False): (1024 + 19, 4)})
+    w = torch.nn.Parameter(torch.zeros(N, K, dtype=torch.bfloat16), requires_grad=False)
+    assert gemm.choose_packed(65, N, K, False, w) is None           # no packed copy attached
+    assert gemm.wg_layouts(N, K, False) == [2, 4]
+    assert gemm.wg_layouts(N, K, False, max_m=32) == [4]            # buckets <= 2 only
+    packed = torch.ones(N, K, dtype=torch.bfloat16)
+    w.__dict__["_eia_wg"] = {(2, False): packed}
+    cfg, sk, wp = gemm.choose_packed(65, N, K, False, w)
+    assert (cfg, sk) == (1024 + 17, 4) and wp is packed
+    assert gemm.choose_packed(20, N, K, False, w) is None            # layout 4 not attached
+    assert gemm.choose_packed(5, N, K, False, w) is None             # bucket 1: no packed pick
