@@ -74,9 +74,12 @@ paged_prefill_fa_kernel(const bf16_t* __restrict__ q, long q_stride, bf16_t* __r
   extern __shared__ __align__(16) bf16_t lds[];         // FA_LDS_BYTES
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int r32 = lane & 31, h = lane >> 5;
-  const int s = work[2 * blockIdx.x], q0 = work[2 * blockIdx.x + 1];
+  // grid (head groups, work items): the heads of one query block are dispatched together and
+  // the work list is latest-block-first, so the dispatch order is longest-first over the
+  // whole grid (causal blocks grow with their position), not per head
+  const int s = work[2 * blockIdx.y], q0 = work[2 * blockIdx.y + 1];
   const int G = Hq / Hkv, NHG = G / 4;
-  const int kvh = blockIdx.y / NHG, hg = blockIdx.y % NHG;
+  const int kvh = blockIdx.x / NHG, hg = blockIdx.x % NHG;
   const int hq = kvh * G + hg * 4 + (w & 3);
   const int qsub = w >> 2;
   const int qbeg = cu_q[s], qlen = cu_q[s + 1] - qbeg;
@@ -281,7 +284,7 @@ paged_prefill_fa_kernel(const bf16_t* __restrict__ q, long q_stride, bf16_t* __r
 }  // namespace
 
 // work = [seq, first query] pairs with 64-query blocks (attention.prefill_query_block);
-// grid (n_work, Hkv * G/4).  Requires D = 128, G % 4 == 0, block size % 64 == 0.
+// grid (Hkv * G/4, n_work).  Requires D = 128, G % 4 == 0, block size % 64 == 0.
 EIA_API int eia_paged_prefill_fa(const void* q, long q_stride, void* out, long out_stride,
                                  const void* k_cache, const void* v_cache,
                                  const int* block_tables, int bt_stride, const int* seq_lens,
@@ -298,7 +301,7 @@ EIA_API int eia_paged_prefill_fa(const void* q, long q_stride, void* out, long o
                               hipFuncAttributeMaxDynamicSharedMemorySize, FA_LDS_BYTES);
     attr = true;
   }
-  dim3 grid(n_work, Hkv * ((Hq / Hkv) / 4));
+  dim3 grid(Hkv * ((Hq / Hkv) / 4), n_work);
   hipLaunchKernelGGL(paged_prefill_fa_kernel, grid, dim3(FTHREADS), FA_LDS_BYTES, st, (const bf16_t*)q,
                      q_stride, (bf16_t*)out, out_stride, (const bf16_t*)k_cache,
                      (const bf16_t*)v_cache, block_tables, bt_stride, seq_lens, cu_q, work,

@@ -214,10 +214,13 @@ mlp_fused_kernel(const bf16_t* __restrict__ X, long ldx, const bf16_t* __restric
             __hip_atomic_store((gu64*)dst, __builtin_bit_cast(unsigned long long, v),
                                __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
           } else {
+            // elements from the packed 64-bit word: a bit_cast of v[j] itself was compiled
+            // to element 0 for every j (ROCm 7.2, wrong stores at R = 28 / 56)
+            const unsigned long long u = __builtin_bit_cast(unsigned long long, v);
 #pragma unroll
             for (int j = 0; j < 4; ++j)
               if (4 * g + j < rw)
-                __hip_atomic_store((gu16*)(dst + j), __builtin_bit_cast(unsigned short, v[j]),
+                __hip_atomic_store((gu16*)(dst + j), (unsigned short)(u >> (16 * j)),
                                    __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
           }
         }

@@ -87,6 +87,13 @@ def graph_time(fn, iters, rounds=3):
     return best   # us per call
 
 
+def write_table(tuned, tuned_wg, out=None):
+    table = {"device": torch.cuda.get_device_name(0), "entries": tuned, "wg_entries": tuned_wg}
+    for path in [gemm.TUNING_FILE] + ([out] if out else []):
+        with open(path, "w") as f:
+            json.dump(table, f, indent=0, sort_keys=True)
+
+
 def bucket_pick(b, margin=1.02):
     """A bucket's table entry from its summed timings: ``b`` = {"rows": [M...], "hip": summed
     hipBLASLt us, "var": {(cfg, sk): [summed us, rows timed]}}.  Only variants timed (valid,
@@ -245,15 +252,10 @@ def main():
                               "runner_up": [(round(t, 1), c) for t, c in full[1:3]]}), flush=True)
         del ws, wps, wgp
         torch.cuda.empty_cache()
+        if a.tune:
+            write_table(tuned, tuned_wg, a.out)     # after every shape: a cut-off run keeps them
     if a.tune:
-        table = {"device": torch.cuda.get_device_name(0), "entries": tuned,
-                 "wg_entries": tuned_wg}
-        with open(gemm.TUNING_FILE, "w") as f:
-            json.dump(table, f, indent=0, sort_keys=True)
         print("wrote", gemm.TUNING_FILE)
-        if a.out:
-            with open(a.out, "w") as f:
-                json.dump(table, f, indent=0, sort_keys=True)
         if a.persist:
             from enterprise_inference_amd.utils.cache_dir import persist
             print("persisted", persist(gemm.TUNING_FILE, "gemm_tuning.json"))
