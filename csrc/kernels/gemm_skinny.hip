@@ -639,6 +639,13 @@ int launch_mt(int cfg, const bf16_t* X, long ldx, const bf16_t* W, long ldw, con
   // grouped (MoE) uses S = 2, KC = 256 (3-stage forms measured neutral at Mixtral decode,
   // profiles/moe_s3_ab_r4.log)
   if constexpr (GROUPED) {
+    if (cfg & 1024) {   // workgroup-packed expert weights (pack_weight_wg per expert)
+      switch (cfg & ~1024) {
+        case 1: return launch_cfg<MT, 2, 2, 2, GROUPED, 256, false, 2>(X, ldx, W, ldw, bias, out, ldo, M, N, K, sk, mode, experts, offs, row_idx, w_estride, st);
+        case 3: return launch_cfg<MT, 2, 4, 2, GROUPED, 256, false, 2>(X, ldx, W, ldw, bias, out, ldo, M, N, K, sk, mode, experts, offs, row_idx, w_estride, st);
+        default: return EIA_BAD_SHAPE;
+      }
+    }
     switch (cfg & 3) {
       case 0: EIA_CFG(1, 2, 2, 256);
       case 1: EIA_CFG(2, 2, 2, 256);
@@ -865,7 +872,9 @@ EIA_API int eia_gemm_skinny(const void* X, long ldx, const void* W, long ldw, co
 EIA_API int eia_moe_gemm(const void* X, long ldx, const void* W, long ldw, const void* bias,
                          void* out, long ldo, int N, int K, int experts, const int* offs,
                          const int* row_idx, int mt_hint, int mode, int cfg, hipStream_t st) {
-  if (experts < 1 || mode == MODE_F32_SPLIT || (cfg & 252)) return EIA_BAD_SHAPE;
+  if (experts < 1 || mode == MODE_F32_SPLIT || (cfg & ~(3 | 1024))) return EIA_BAD_SHAPE;
+  if ((cfg & 1024) && (cfg & 3) != 1 && (cfg & 3) != 3) return EIA_BAD_SHAPE;
+  if ((cfg & 1024) && ldw != K) return EIA_BAD_SHAPE;
   if (int rc = check_shape(N, K, 1, mode, cfg)) return rc;
   if ((ldx % 8) || (ldw % 8) || (ldo % 4)) return EIA_BAD_SHAPE;
   const int mt = mt_hint < 1 ? 1 : (mt_hint > 8 ? 8 : mt_hint);

@@ -228,6 +228,17 @@ def attach_wg_packed(model: torch.nn.Module, budget_bytes: int, max_m: int = MAX
         for sw in forms:
             for waves in wg_layouts(N, K, sw, max_m):
                 plan.append((w, waves, sw))
+    if os.environ.get("EIA_MOE_WG_PACK", "1") != "0":
+        # MoE expert gate_up [E, 2I, H] (the grouped skinny kernel's decode form, cfg 1 / 3)
+        from .moe import moe_cfgs
+        for mod in model.modules():
+            w13 = getattr(mod, "w13", None)
+            if (isinstance(w13, torch.Tensor) and w13.dim() == 3 and w13.is_cuda
+                    and w13.dtype == torch.bfloat16 and w13.is_contiguous()):
+                E, I2, H = w13.shape
+                up = moe_cfgs(I2 // 2, H)[0]
+                if up in (1, 3) and H % 128 == 0:
+                    plan.append((w13, 2 if up == 1 else 4, True))
     seen = set()
     total = 0
     for w, waves, sw in plan:
@@ -241,7 +252,11 @@ def attach_wg_packed(model: torch.nn.Module, budget_bytes: int, max_m: int = MAX
         if (waves, sw) in d:
             continue
         cfg = 1024 + {2: 17, 3: 529, 4: 19}[waves]
-        d[(waves, sw)] = pack_weight_wg(w.data, cfg, sw)
+        if w.dim() == 3:           # per expert
+            d[(waves, sw)] = torch.stack([pack_weight_wg(w.data[e], cfg, sw)
+                                          for e in range(w.shape[0])])
+        else:
+            d[(waves, sw)] = pack_weight_wg(w.data, cfg, sw)
     return total
 
 

@@ -148,7 +148,14 @@ def _fused_moe_grouped(x, w13, w2, topk_w, topk_ids, e_lo, e_hi, mfma: bool = Fa
     else:
         mt = max(1, min(8, -(-int(1.5 * n / El + 1) // 16)))
         up_cfg, down_cfg = moe_cfgs(I, H, UP_CFG, DOWN_CFG)
-        check(lib().eia_moe_gemm(ptr(x), x.stride(0), ptr(w13), w13.stride(1), None, ptr(h1),
+        w_up = w13
+        packed = getattr(w13, "_eia_wg", None)
+        if packed and up_cfg in (1, 3) and (2 if up_cfg == 1 else 4, True) in packed:
+            # workgroup-packed expert gate_up (ops/gemm.py attach_wg_packed): one sequential
+            # weight stream per workgroup
+            w_up = packed[(2 if up_cfg == 1 else 4, True)]
+            up_cfg |= 1024
+        check(lib().eia_moe_gemm(ptr(x), x.stride(0), ptr(w_up), w13.stride(1), None, ptr(h1),
                                  h1.stride(0), I2, H, El, ptr(offs), ptr(row_idx), mt, 2,
                                  up_cfg, st), "moe_gemm_gate_up")
         if DOWN_SK > 1 and I % (DOWN_SK * 256) == 0:

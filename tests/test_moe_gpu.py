@@ -180,56 +180,66 @@ def test_sorted_blas_expert_parallel_after_poisoned_allocator():
     assert (full - part).abs().max() < 5e-2
 
 
-A2A_GRAPH = r'''
-import os, sys, socket, torch, torch.distributed as dist
-sys.path.insert(0, os.environ["EIA_ROOT"])
-torch.cuda.set_device(0)
-s = socket.socket(); s.bind(("127.0.0.1", 0)); port = s.getsockname()[1]; s.close()
-dist.init_process_group("nccl", rank=0, world_size=1, init_method=f"tcp://127.0.0.1:{port}",
-                        device_id=torch.device("cuda", 0))
-from enterprise_inference_amd.ops import moe
-from enterprise_inference_amd.parallel.expert_parallel import moe_all_to_all_replicated
-E, k, H, I, T = 8, 2, 1024, 1792, 65
-g = torch.Generator(device="cuda").manual_seed(0)
-w13 = (torch.randn(E, 2 * I, H, device="cuda", generator=g) * H ** -0.5).bfloat16()
-w2 = (torch.randn(E, H, I, device="cuda", generator=g) * I ** -0.5).bfloat16()
-x = torch.randn(T, H, device="cuda").bfloat16()
-lg = torch.randn(T, E, device="cuda")
-def layer():
-    w, ids = moe.topk_route(lg, k, True)
-    return moe_all_to_all_replicated(x, w, ids, w13, w2, 0, E)
-layer(); torch.cuda.synchronize()
-graph = torch.cuda.CUDAGraph()
-st = torch.cuda.Stream(); st.wait_stream(torch.cuda.current_stream())
-with torch.cuda.stream(st):
-    with torch.cuda.graph(graph):          # a host read-back here would fail the capture
-        out = layer()
-torch.cuda.current_stream().wait_stream(st)
-worst = 0.0
-for it in range(3):
-    x.copy_(torch.randn(T, H, device="cuda").bfloat16()); lg.copy_(torch.randn(T, E, device="cuda"))
-    graph.replay(); torch.cuda.synchronize()
-    w, ids = moe.topk_route(lg, k, True)
-    ref = moe.fused_moe(x, w13, w2, w, ids)
-    worst = max(worst, (out.float() - ref.float()).abs().max().item())
-dist.destroy_process_group()
-print("A2A_GRAPH_OK", worst, flush=True)
-'''
+def test_all_to_all_ep_captures_in_hip_graph(monkeypatch):
+    """The padded all-to-all EP layer (device-side slots, no host read-back) captures into a
+    HIP graph and its replays match the single-GPU fused MoE.  One rank: the exchange itself is
+    the identity (a copy stands in for the collective), what is tested is that nothing in the
+    layer syncs the host -- a .tolist() / .item() would fail the capture."""
+    from enterprise_inference_amd.ops import moe
+    from enterprise_inference_amd.parallel import comm
+    from enterprise_inference_amd.parallel import expert_parallel as ep
+
+    def a2a(out, inp, out_splits=None, in_splits=None, group=None):
+        assert out_splits is None and in_splits is None     # equal splits only
+        out.copy_(inp)
+        return out
+    monkeypatch.setattr(comm, "all_to_all_single", a2a)
+    E, k, H, I, T = 8, 2, 1024, 1792, 65
+    g = torch.Generator(device=DEV).manual_seed(0)
+    w13 = (torch.randn(E, 2 * I, H, device=DEV, generator=g) * H ** -0.5).to(BF)
+    w2 = (torch.randn(E, H, I, device=DEV, generator=g) * I ** -0.5).to(BF)
+    x = torch.randn(T, H, device=DEV).to(BF)
+    lg = torch.randn(T, E, device=DEV)
+
+    def layer():
+        w, ids = moe.topk_route(lg, k, True)
+        return ep._moe_all_to_all_padded(x, w, ids, w13, w2, 0, E, None, "silu", 1, T * k)
+    layer()
+    torch.cuda.synchronize()
+    graph = torch.cuda.CUDAGraph()
+    st = torch.cuda.Stream()
+    st.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(st):
+        with torch.cuda.graph(graph):
+            out = layer()
+    torch.cuda.current_stream().wait_stream(st)
+    for it in range(3):
+        x.copy_(torch.randn(T, H, device=DEV).to(BF))
+        lg.copy_(torch.randn(T, E, device=DEV))
+        graph.replay()
+        torch.cuda.synchronize()
+        w, ids = moe.topk_route(lg, k, True)
+        ref = moe.fused_moe(x, w13, w2, w, ids)
+        err = (out.float() - ref.float()).abs().max().item()
+        assert err < 3e-2, (it, err)
 
 
-def test_all_to_all_ep_captures_in_hip_graph(tmp_path):
-    """The padded all-to-all EP layer (no host read-back) captures into a HIP graph over an
-    RCCL group and its replays match the single-GPU fused MoE (a one-rank group: the
-    exchange is the identity, the capture is what is tested)."""
-    import os
-    import subprocess
-    import sys
-    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-    f = tmp_path / "a2a_graph.py"
-    f.write_text(A2A_GRAPH)
-    r = subprocess.run([sys.executable, str(f)], env=dict(os.environ, EIA_ROOT=root),
-                       capture_output=True, text=True, timeout=300)
-    out = r.stdout + r.stderr
-    assert r.returncode == 0, out[-3000:]
-    line = [ln for ln in out.splitlines() if ln.startswith("A2A_GRAPH_OK")][0]
-    assert float(line.split()[1]) < 3e-2, line
+@pytest.mark.parametrize("T,E,k,H,I", [(1, 8, 2, 512, 256), (33, 8, 2, 1024, 512),
+                                       (65, 8, 2, 4096, 1792)])
+def test_fused_moe_wg_packed_gate_up(T, E, k, H, I):
+    """Decode MoE with the expert gate_up read from its workgroup-packed copy (cfg bit 10,
+    attach_wg_packed's per-expert packing) equals the row-major run bit for bit."""
+    from enterprise_inference_amd.ops import gemm, moe
+    torch.manual_seed(T + 1)
+    x = torch.randn(T, H, device=DEV, dtype=BF)
+    w13 = (torch.randn(E, 2 * I, H, device=DEV) * H ** -0.5).to(BF)
+    w2 = (torch.randn(E, H, I, device=DEV) * I ** -0.5).to(BF)
+    w, ids = moe.topk_route(torch.randn(T, E, device=DEV), k, True)
+    plain = moe.fused_moe(x, w13, w2, w, ids)
+    up = moe.moe_cfgs(I, H)[0]
+    waves = 2 if up == 1 else 4
+    cfg = 1024 + (17 if waves == 2 else 19)
+    w13.__dict__["_eia_wg"] = {(waves, True): torch.stack(
+        [gemm.pack_weight_wg(w13[e], cfg, True) for e in range(E)])}
+    packed = moe.fused_moe(x, w13, w2, w, ids)
+    assert torch.equal(plain, packed)
