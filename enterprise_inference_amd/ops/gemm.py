@@ -249,15 +249,40 @@ def attach_wg_packed(model: torch.nn.Module, budget_bytes: int, max_m: int = MAX
         return 0
     for w, waves, sw in plan:
         d = w.__dict__.setdefault("_eia_wg", {})
-        if (waves, sw) in d:
-            continue
-        cfg = 1024 + {2: 17, 3: 529, 4: 19}[waves]
-        if w.dim() == 3:           # per expert
-            d[(waves, sw)] = torch.stack([pack_weight_wg(w.data[e], cfg, sw)
-                                          for e in range(w.shape[0])])
-        else:
-            d[(waves, sw)] = pack_weight_wg(w.data, cfg, sw)
+        if (waves, sw) not in d:
+            d[(waves, sw)] = _pack_wg_any(w, waves, sw)
+    # a later load_weights (weight hot-swap, tests loading HF tensors into a built engine) must
+    # not leave the decode kernels reading stale copies
+    load = getattr(model, "load_weights", None)
+    if load is not None and not getattr(load, "_eia_wg_refresh", False):
+        def load_and_refresh(weights, _load=load):
+            out = _load(weights)
+            refresh_wg_packed(model)
+            return out
+        load_and_refresh._eia_wg_refresh = True
+        model.load_weights = load_and_refresh
     return total
+
+
+def _pack_wg_any(w: torch.Tensor, waves: int, sw: bool) -> torch.Tensor:
+    cfg = 1024 + {2: 17, 3: 529, 4: 19}[waves]
+    if w.dim() == 3:               # per expert
+        return torch.stack([pack_weight_wg(w.data[e], cfg, sw) for e in range(w.shape[0])])
+    return pack_weight_wg(w.data, cfg, sw)
+
+
+def refresh_wg_packed(model: torch.nn.Module) -> int:
+    """Re-pack every workgroup-packed copy from its (re)loaded weight, in place so pointers
+    captured in decode graphs stay valid.  Returns the number of copies refreshed."""
+    n = 0
+    for p in model.parameters():
+        d = p.__dict__.get("_eia_wg")
+        if not d:
+            continue
+        for (waves, sw), wp in d.items():
+            wp.copy_(_pack_wg_any(p, waves, sw))
+            n += 1
+    return n
 
 
 def choose_splitk(N: int, K: int, swiglu: bool = False, M: int = 64) -> int:

@@ -67,3 +67,19 @@ def test_pack_weight_wg_matches_kernel_addressing(cfg, swiglu, N):
         row = g_ * rows + wv * nt * 16 + t * 16 + r
     k = kb * 128 + 8 * g + 32 * s + j
     assert torch.equal(p[off.reshape(-1)], w[row.reshape(-1), k.reshape(-1)])
+
+
+def test_refresh_wg_packed_follows_weight_reload():
+    """A packed copy attached before a weight reload is re-packed in place (same storage, so
+    graph-captured pointers stay valid) by refresh_wg_packed."""
+    lin = torch.nn.Linear(256, 256, bias=False).to(torch.bfloat16)
+    cfg = 1024 + 3
+    wp = gemm.pack_weight_wg(lin.weight.data, cfg, False)
+    lin.weight.__dict__["_eia_wg"] = {(4, False): wp}
+    ptr = wp.data_ptr()
+    with torch.no_grad():
+        lin.weight.copy_(torch.randn(256, 256, dtype=torch.bfloat16))
+    assert not torch.equal(wp, gemm.pack_weight_wg(lin.weight.data, cfg, False))
+    assert gemm.refresh_wg_packed(lin) == 1
+    assert wp.data_ptr() == ptr
+    assert torch.equal(wp, gemm.pack_weight_wg(lin.weight.data, cfg, False))
