@@ -276,16 +276,6 @@ EIA_API int eia_ar_alloc(void** ptr, long bytes) {
   return (int)hipMemset(*ptr, 0, (size_t)bytes);
 }
 
-// Data buffer with the default (coarse-grained, L2-cached) placement: the local staging copy
-// then lands in L2 and is written back by the barrier's system-scope release; peers' reads
-// follow their system-scope acquire.  Opt-in (EIA_AR_CACHED_DATA=1) -- the one-GPU harness
-// (scripts/ar_cached_ab.py) times both; only an 8-GPU run can confirm it across xGMI.
-EIA_API int eia_ar_alloc_cached(void** ptr, long bytes) {
-  hipError_t e = hipMalloc(ptr, (size_t)bytes);
-  if (e != hipSuccess) return (int)e;
-  return (int)hipMemset(*ptr, 0, (size_t)bytes);
-}
-
 EIA_API int eia_ar_free(void* ptr) { return (int)hipFree(ptr); }
 
 EIA_API int eia_ar_signal_bytes() { return (int)sizeof(ArSignal); }

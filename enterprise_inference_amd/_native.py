@@ -68,7 +68,6 @@ _SIGNATURES = {
     "eia_mlp_fused_error": [IP, I, P],
     "eia_splitk_add_rmsnorm": [P, I, I, I, P, P, F, P, L, S],
     "eia_ar_alloc": [P, L],
-    "eia_ar_alloc_cached": [P, L],
     "eia_ar_free": [P],
     "eia_ar_signal_bytes": [],
     "eia_ar_run": [P, P, I, I, P, P, L, L, I, I, S],

@@ -95,11 +95,7 @@ class CustomAllReduce:
         sig_bytes = self.lib.eia_ar_signal_bytes()
         self._own = []
         sig = self._alloc(sig_bytes)
-        # data halves: uncached by default; EIA_AR_CACHED_DATA=1 places them in cached memory
-        # (the staging copy then goes through L2, written back by the barrier's release --
-        # scripts/ar_cached_ab.py times both in the one-GPU harness)
-        self.cached_data = os.environ.get("EIA_AR_CACHED_DATA", "0") == "1"
-        data = self._alloc(2 * max_bytes, cached=self.cached_data)
+        data = self._alloc(2 * max_bytes)
         mine = (ipc_get(sig), ipc_get(data))
         handles: List[Optional[tuple]] = [None] * self.world
         dist.all_gather_object(handles, mine, group=self.cpu_group)
@@ -163,10 +159,9 @@ class CustomAllReduce:
             objs.append(o)
         return objs
 
-    def _alloc(self, nbytes: int, cached: bool = False) -> int:
+    def _alloc(self, nbytes: int) -> int:
         p = ctypes.c_void_p()
-        fn = self.lib.eia_ar_alloc_cached if cached else self.lib.eia_ar_alloc
-        rc = fn(ctypes.byref(p), ctypes.c_long(nbytes))
+        rc = self.lib.eia_ar_alloc(ctypes.byref(p), ctypes.c_long(nbytes))
         if rc != 0:
             raise RuntimeError(f"eia_ar_alloc({nbytes}) failed ({rc})")
         self._own.append(p.value)
