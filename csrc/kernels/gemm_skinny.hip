@@ -641,7 +641,9 @@ int launch_mt(int cfg, const bf16_t* X, long ldx, const bf16_t* W, long ldw, con
   if constexpr (GROUPED) {
     if (cfg & 1024) {   // workgroup-packed expert weights (pack_weight_wg per expert)
       switch (cfg & ~1024) {
+        case 0: return launch_cfg<MT, 1, 2, 2, GROUPED, 256, false, 2>(X, ldx, W, ldw, bias, out, ldo, M, N, K, sk, mode, experts, offs, row_idx, w_estride, st);
         case 1: return launch_cfg<MT, 2, 2, 2, GROUPED, 256, false, 2>(X, ldx, W, ldw, bias, out, ldo, M, N, K, sk, mode, experts, offs, row_idx, w_estride, st);
+        case 2: return launch_cfg<MT, 1, 4, 2, GROUPED, 256, false, 2>(X, ldx, W, ldw, bias, out, ldo, M, N, K, sk, mode, experts, offs, row_idx, w_estride, st);
         case 3: return launch_cfg<MT, 2, 4, 2, GROUPED, 256, false, 2>(X, ldx, W, ldw, bias, out, ldo, M, N, K, sk, mode, experts, offs, row_idx, w_estride, st);
         default: return EIA_BAD_SHAPE;
       }
@@ -807,9 +809,10 @@ int check_shape(int N, int K, int sk, int mode, int cfg) {
   if (sk < 1 || cfg < 0 || (cfg & ~(16 | 32 | 64 | 128 | 256 | 512 | 1024)) > 11 ||
       K % (sk * kc) != 0)
     return EIA_BAD_SHAPE;
-  // workgroup-packed: the forms built above (two 16-row tiles per wave, 2 stages)
-  if ((cfg & 1024) && (cfg & ~1024) != 1 && (cfg & ~1024) != 3 && (cfg & ~1024) != 17 &&
-      (cfg & ~1024) != 19 && (cfg & ~1024) != 512 + 17)
+  // workgroup-packed: the forms built above (2 stages; the one-tile forms 0 / 2 are grouped
+  // only -- the MoE down projection)
+  if ((cfg & 1024) && (cfg & ~1024) > 3 && (cfg & ~1024) != 17 && (cfg & ~1024) != 19 &&
+      (cfg & ~1024) != 512 + 17)
     return EIA_BAD_SHAPE;
   // 3-wave form: register-staged, plain layout, no SwiGLU pairing, 2-3 stages
   if ((cfg & 512) && ((cfg & (2 | 8 | 32 | 64 | 128 | 256)) || mode == MODE_SWIGLU))
@@ -840,8 +843,8 @@ int check_shape(int N, int K, int sk, int mode, int cfg) {
 // bit 7 -> LDS-DMA ring kernel (with bits 1 and 4; bits 2-3 = ring depth - 2)
 // bit 8 -> 7 waves of (gate, up) pairs per workgroup (SwiGLU only; cfg 273 = + bits 0 and 4):
 //          70B's 1792 pairs are exactly 256 workgroups, where 4-wave workgroups leave 448
-// bit 10 -> workgroup-packed W (pack_weight_wg; ldw must be K) with cfg 1, 3, 17, 19 or 529:
-//          each workgroup streams its rows as one sequential run
+// bit 10 -> workgroup-packed W (pack_weight_wg; ldw must be K) with cfg 1, 3, 17, 19 or 529
+//          (grouped: 0-3): each workgroup streams its rows as one sequential run
 // bit 9 -> 3 waves per workgroup (+ bits 0, 2, 4): Llama-8B's QKV (6144 rows) as 64 x 96-row
 //          tiles x split-K 4 = 256 workgroups, where 4-wave (128-row) tiles leave 192 -- a
 //          decode GEMM streams at a per-CU rate (~20 GB/s), so idle CUs are lost bandwidth
@@ -873,7 +876,6 @@ EIA_API int eia_moe_gemm(const void* X, long ldx, const void* W, long ldw, const
                          void* out, long ldo, int N, int K, int experts, const int* offs,
                          const int* row_idx, int mt_hint, int mode, int cfg, hipStream_t st) {
   if (experts < 1 || mode == MODE_F32_SPLIT || (cfg & ~(3 | 1024))) return EIA_BAD_SHAPE;
-  if ((cfg & 1024) && (cfg & 3) != 1 && (cfg & 3) != 3) return EIA_BAD_SHAPE;
   if ((cfg & 1024) && ldw != K) return EIA_BAD_SHAPE;
   if (int rc = check_shape(N, K, 1, mode, cfg)) return rc;
   if ((ldx % 8) || (ldw % 8) || (ldo % 4)) return EIA_BAD_SHAPE;
@@ -889,7 +891,8 @@ EIA_API int eia_moe_gemm(const void* X, long ldx, const void* W, long ldw, const
 EIA_API int eia_moe_gemm_sk(const void* X, long ldx, const void* W, long ldw, float* part,
                             int rows, int N, int K, int experts, const int* offs,
                             const int* row_idx, int mt_hint, int sk, int cfg, hipStream_t st) {
-  if (experts < 1 || sk < 1 || rows < 1 || (cfg & 252)) return EIA_BAD_SHAPE;
+  if (experts < 1 || sk < 1 || rows < 1 || (cfg & ~(3 | 1024))) return EIA_BAD_SHAPE;
+  if ((cfg & 1024) && ldw != K) return EIA_BAD_SHAPE;           // packed over the full K
   if (int rc = check_shape(N, K, sk, MODE_F32_SPLIT, cfg)) return rc;
   if ((ldx % 8) || (ldw % 8)) return EIA_BAD_SHAPE;
   const int mt = mt_hint < 1 ? 1 : (mt_hint > 8 ? 8 : mt_hint);

@@ -217,7 +217,248 @@ combine_sk_kernel(const float* __restrict__ part, int sk, long slab, const float
   }
 }
 
+// ------------------------------------------------------------------------------------------
+// Decode-step norms around the MoE block, one 1024-thread workgroup per token row (H <= 16384
+// as 4-column vectors, VPT per thread).  The unfused step ran the O projection's split-K
+// add + RMSNorm, then route_kernel (10.6 us per layer), and after the experts combine_sk_kernel
+// (14.4 us: 65 one-token workgroups, a serial chain per 1024 columns) plus the next layer's
+// add + RMSNorm (5 us) -- profiles/rocprof_r5_decode_steps_mixtral.md.
+
+// Post-attention: residual += sum of the O projection's fp32 slabs (slab order);
+// out = rmsnorm(residual) * w; then the router logits of the normalised (bf16) row, rounded to
+// bf16 like the Linear they replace, and the top-k (topk_select).  The router rows (E x H bf16,
+// L2-resident) are loaded beside the slabs.
+template <int VPT, int SK, int EM>
+__global__ void __launch_bounds__(1024)
+splitk_norm_route_kernel(const float* __restrict__ part, int sk_rt, int M, int H,
+                         bf16_t* __restrict__ residual, const bf16_t* __restrict__ w, float eps,
+                         bf16_t* __restrict__ out, long ldo, const bf16_t* __restrict__ wr,
+                         int E, int k, int renorm, int scoring, float* __restrict__ w_out,
+                         int* __restrict__ id_out) {
+  __shared__ float scratch[16];
+  __shared__ float red[16][EM];
+  const int row = blockIdx.x;
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const long total = (long)M * H;
+  const int sk = SK > 0 ? SK : sk_rt;
+  float v[VPT][4];
+  bf16x4 rw[VPT][EM];
+  float ss = 0.f;
+#pragma unroll
+  for (int i = 0; i < VPT; ++i) {
+    const int c = (threadIdx.x + i * 1024) * 4;
+    if (c < H) {
+      const long off = (long)row * H + c;
+      f32x4 p[SK > 0 ? SK : 1];
+      if constexpr (SK > 0) {
+#pragma unroll
+        for (int j = 0; j < SK; ++j) p[j] = *reinterpret_cast<const f32x4*>(part + j * total + off);
+      } else {
+        p[0] = *reinterpret_cast<const f32x4*>(part + off);
+      }
+      const bf16x4 rr = *reinterpret_cast<const bf16x4*>(residual + off);
+#pragma unroll
+      for (int e = 0; e < EM; ++e)
+        if (e < E) rw[i][e] = *reinterpret_cast<const bf16x4*>(wr + (long)e * H + c);
+      f32x4 a = p[0];
+      if constexpr (SK > 0) {
+#pragma unroll
+        for (int j = 1; j < SK; ++j) a += p[j];
+      } else {
+        for (int j = 1; j < sk; ++j) a += *reinterpret_cast<const f32x4*>(part + j * total + off);
+      }
+      bf16x4 nr;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        nr[j] = f2bf(a[j] + bf2f(rr[j]));
+        v[i][j] = bf2f(nr[j]);
+        ss += v[i][j] * v[i][j];
+      }
+      *reinterpret_cast<bf16x4*>(residual + off) = nr;
+    }
+  }
+  const float tot = block_sum(ss, scratch);
+  const float inv = rsqrtf(tot / (float)H + eps);
+  float lg[EM];
+#pragma unroll
+  for (int e = 0; e < EM; ++e) lg[e] = 0.f;
+#pragma unroll
+  for (int i = 0; i < VPT; ++i) {
+    const int c = (threadIdx.x + i * 1024) * 4;
+    if (c < H) {
+      const bf16x4 ww = *reinterpret_cast<const bf16x4*>(w + c);
+      bf16x4 o;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) o[j] = f2bf(v[i][j] * inv * bf2f(ww[j]));
+      *reinterpret_cast<bf16x4*>(out + (long)row * ldo + c) = o;
+#pragma unroll
+      for (int e = 0; e < EM; ++e)
+        if (e < E) {
+#pragma unroll
+          for (int j = 0; j < 4; ++j) lg[e] = fmaf(bf2f(o[j]), bf2f(rw[i][e][j]), lg[e]);
+        }
+    }
+  }
+  // reduce-scatter over the wave: halve the expert set at each butterfly step (EM - 1 + the
+  // remaining log2(64 / EM) shuffles instead of 6 EM); lane then holds expert lane / (64 / EM)
+#pragma unroll
+  for (int n = EM, o = 32; n > 1; n >>= 1, o >>= 1) {
+    const bool hi = (lane & o) != 0;
+#pragma unroll
+    for (int i = 0; i < n / 2; ++i) {
+      const float mine = hi ? lg[n / 2 + i] : lg[i];
+      const float other = hi ? lg[i] : lg[n / 2 + i];
+      lg[i] = mine + __shfl_xor(other, o, 64);
+    }
+  }
+#pragma unroll
+  for (int o = 32 / EM; o > 0; o >>= 1) lg[0] += __shfl_xor(lg[0], o, 64);
+  if ((lane & (64 / EM - 1)) == 0 && lane / (64 / EM) < E) red[wid][lane / (64 / EM)] = lg[0];
+  __syncthreads();
+  if (wid != 0) return;
+  float x = -INFINITY;
+  if (lane < E) {
+    float s = 0.f;
+    for (int ww = 0; ww < 16; ++ww) s += red[ww][lane];
+    x = bf2f(f2bf(s));
+  }
+  topk_select(x, row, lane, E, k, renorm, scoring, w_out, id_out);
+}
+
+// After the experts: y[t] = sum_s w[t,s] * bf16(sum_j part[j][inv[t,s]]) (combine_sk_kernel's
+// rounding), residual += y (bf16, like the add + RMSNorm it replaces), out = rmsnorm * w.  All
+// of a thread's slab loads (KM slots x SK slabs x VPT) are issued before the first use.
+template <int VPT, int SK, int KM>
+__global__ void __launch_bounds__(1024)
+moe_combine_norm_kernel(const float* __restrict__ part, long slab, const float* __restrict__ tw,
+                        const int* __restrict__ inv, int k, int H, bf16_t* __restrict__ residual,
+                        const bf16_t* __restrict__ w, float eps, bf16_t* __restrict__ out,
+                        long ldo) {
+  __shared__ float scratch[16];
+  const int t = blockIdx.x;
+  int pos[KM];
+  float ws[KM];
+#pragma unroll
+  for (int s = 0; s < KM; ++s) {
+    pos[s] = s < k ? inv[(long)t * k + s] : -1;
+    ws[s] = s < k ? tw[(long)t * k + s] : 0.f;
+  }
+  float v[VPT][4];
+  float ss = 0.f;
+#pragma unroll
+  for (int i = 0; i < VPT; ++i) {
+    const int c = (threadIdx.x + i * 1024) * 4;
+    if (c < H) {
+      f32x4 p[KM][SK];
+#pragma unroll
+      for (int s = 0; s < KM; ++s)
+#pragma unroll
+        for (int j = 0; j < SK; ++j)
+          p[s][j] = pos[s] >= 0 ? *reinterpret_cast<const f32x4*>(part + j * slab +
+                                                                  (long)pos[s] * H + c)
+                                : (f32x4){0.f, 0.f, 0.f, 0.f};
+      const long off = (long)t * H + c;
+      const bf16x4 rr = *reinterpret_cast<const bf16x4*>(residual + off);
+      f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int s = 0; s < KM; ++s) {
+        if (pos[s] < 0) continue;
+        f32x4 a = p[s][0];
+#pragma unroll
+        for (int j = 1; j < SK; ++j) a += p[s][j];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) acc[e] += ws[s] * bf2f(f2bf(a[e]));
+      }
+      bf16x4 nr;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        nr[j] = f2bf(bf2f(f2bf(acc[j])) + bf2f(rr[j]));
+        v[i][j] = bf2f(nr[j]);
+        ss += v[i][j] * v[i][j];
+      }
+      *reinterpret_cast<bf16x4*>(residual + off) = nr;
+    }
+  }
+  const float tot = block_sum(ss, scratch);
+  const float rinv = rsqrtf(tot / (float)H + eps);
+#pragma unroll
+  for (int i = 0; i < VPT; ++i) {
+    const int c = (threadIdx.x + i * 1024) * 4;
+    if (c < H) {
+      const bf16x4 ww = *reinterpret_cast<const bf16x4*>(w + c);
+      bf16x4 o;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) o[j] = f2bf(v[i][j] * rinv * bf2f(ww[j]));
+      *reinterpret_cast<bf16x4*>(out + (long)t * ldo + c) = o;
+    }
+  }
+}
+
 }  // namespace
+
+// Fused O-projection split-K add + RMSNorm + router + top-k (decode).  part [sk, M, H] fp32,
+// residual [M, H] bf16 (updated), out [M, ldo], router wr [E, H] bf16 (E <= 16).
+EIA_API int eia_moe_splitk_norm_route(const float* part, int sk, int M, int H, void* residual,
+                                      const void* w, float eps, void* out, long ldo,
+                                      const void* wr, int E, int k, int renorm, int scoring,
+                                      float* w_out, int* id_out, hipStream_t st) {
+  if (H % 4 != 0 || H > 4 * 1024 * 2 || ldo % 4 || sk < 1 || E < 1 || E > 16 || k < 1 || k > E)
+    return EIA_BAD_SHAPE;
+  if (M == 0) return EIA_OK;
+  const int vpt = (H / 4 + 1023) / 1024;
+  bf16_t* res = static_cast<bf16_t*>(residual);
+  const bf16_t* ww = static_cast<const bf16_t*>(w);
+  bf16_t* o = static_cast<bf16_t*>(out);
+  const bf16_t* r = static_cast<const bf16_t*>(wr);
+#define EIA_SNR(V, K, EM)                                                                        \
+  hipLaunchKernelGGL((splitk_norm_route_kernel<V, K, EM>), dim3(M), dim3(1024), 0, st, part, sk, \
+                     M, H, res, ww, eps, o, ldo, r, E, k, renorm, scoring, w_out, id_out)
+#define EIA_SNR_K(V, EM)                    \
+  switch (sk) {                             \
+    case 1: EIA_SNR(V, 1, EM); break;       \
+    case 2: EIA_SNR(V, 2, EM); break;       \
+    case 4: EIA_SNR(V, 4, EM); break;       \
+    default: EIA_SNR(V, 0, EM); break;      \
+  }
+  if (E <= 8) {
+    if (vpt <= 1) { EIA_SNR_K(1, 8) } else { EIA_SNR_K(2, 8) }
+  } else {
+    if (vpt <= 1) { EIA_SNR_K(1, 16) } else { EIA_SNR_K(2, 16) }
+  }
+#undef EIA_SNR_K
+#undef EIA_SNR
+  EIA_LAUNCH_CHECK();
+}
+
+// Fused MoE combine (over the down projection's split-K slabs) + residual add + RMSNorm.
+// part [sk, rows, H] fp32; tw / inv [T, k] (k <= 2: every slot's slabs in flight at once);
+// residual [T, H] bf16 (updated); out [T, ldo].
+EIA_API int eia_moe_combine_norm(const float* part, int sk, int rows, const float* tw,
+                                 const int* inv, int T, int k, int H, void* residual,
+                                 const void* w, float eps, void* out, long ldo, hipStream_t st) {
+  if (H % 4 != 0 || H > 4 * 1024 * 2 || ldo % 4 || rows < 1 || k < 1 || k > 2 ||
+      (sk != 1 && sk != 2 && sk != 4))
+    return EIA_BAD_SHAPE;
+  if (T == 0) return EIA_OK;
+  const int vpt = (H / 4 + 1023) / 1024;
+  const long slab = (long)rows * H;
+  bf16_t* res = static_cast<bf16_t*>(residual);
+  const bf16_t* ww = static_cast<const bf16_t*>(w);
+  bf16_t* o = static_cast<bf16_t*>(out);
+#define EIA_MCN(V, K, KM)                                                                       \
+  hipLaunchKernelGGL((moe_combine_norm_kernel<V, K, KM>), dim3(T), dim3(1024), 0, st, part, slab, \
+                     tw, inv, k, H, res, ww, eps, o, ldo)
+#define EIA_MCN_K(V, KM)                    \
+  switch (sk) {                             \
+    case 1: EIA_MCN(V, 1, KM); break;       \
+    case 2: EIA_MCN(V, 2, KM); break;       \
+    default: EIA_MCN(V, 4, KM); break;      \
+  }
+  if (vpt <= 1) { EIA_MCN_K(1, 2) } else { EIA_MCN_K(2, 2) }
+#undef EIA_MCN_K
+#undef EIA_MCN
+  EIA_LAUNCH_CHECK();
+}
 
 EIA_API int eia_moe_topk(const void* logits, int is_bf16, int T, int E, int k, int renorm,
                          int scoring, float* w_out, int* id_out, hipStream_t st) {

@@ -328,6 +328,11 @@ class RMSNorm(nn.Module):
             if residual is not None:
                 return gemm.splitk_add_rmsnorm(x, residual, self.weight, self.eps)
             x = x.materialize()
+        from ..ops import moe as moe_ops
+        if isinstance(x, moe_ops.MoECombine):
+            if residual is not None:
+                return moe_ops.combine_add_rmsnorm(x, residual, self.weight, self.eps)
+            x = x.materialize()
         if residual is None:
             return norm.rms_norm(x, self.weight, self.eps)
         return norm.fused_add_rms_norm(x, residual, self.weight, self.eps)

@@ -112,6 +112,12 @@ class LlamaDecoderLayer(nn.Module):
         else:
             h, residual = self.input_layernorm(h, residual)
         h = self.self_attn(h, md, kv)
+        fuse = getattr(self.mlp, "norm_and_route", None)
+        if fuse is not None:            # MoE: router + top-k inside the add + RMSNorm launch
+            r = fuse(h, residual, self.post_attention_layernorm)
+            if r is not None:
+                h, residual, routing = r
+                return self.mlp(h, routing=routing), residual
         h, residual = self.post_attention_layernorm(h, residual)
         return self.mlp(h), residual
 

@@ -95,8 +95,12 @@ class FusedMoE(nn.Module):
             param.data[e].copy_(self._ishard(loaded, 1))
 
     def forward(self, x: torch.Tensor, router_logits: Optional[torch.Tensor] = None,
-                reduce: bool = True, router_w: Optional[torch.Tensor] = None):
-        if router_logits is None:     # fused router GEMM + top-k
+                reduce: bool = True, router_w: Optional[torch.Tensor] = None,
+                routing: Optional[Tuple[torch.Tensor, torch.Tensor]] = None,
+                defer_combine: bool = False):
+        if routing is not None:       # routed by the preceding norm (MixtralMoE.norm_and_route)
+            w, ids = routing
+        elif router_logits is None:   # fused router GEMM + top-k
             w, ids = moe_ops.route(x, router_w, self.k, self.renormalize, self.scoring)
         else:
             w, ids = moe_ops.topk_route(router_logits, self.k, self.renormalize, self.scoring)
@@ -109,7 +113,9 @@ class FusedMoE(nn.Module):
             return moe_all_to_all_replicated(x, w, ids, self.w13, self.w2, self.e_lo,
                                              self.e_per, state.tp_group())
         out = moe_ops.fused_moe(x, self.w13, self.w2, w, ids,
-                                (self.e_lo, self.e_lo + self.e_per) if self.ep else None)
+                                (self.e_lo, self.e_lo + self.e_per) if self.ep else None,
+                                defer_combine=defer_combine and not (reduce and
+                                                                     state.tp_size() > 1))
         if reduce and state.tp_size() > 1:
             out = comm.all_reduce(out)
         return out
@@ -140,9 +146,24 @@ class MixtralMoE(nn.Module):
             self.shared_expert.down_proj.reduce_results = False   # one all-reduce for the sum
             self.shared_expert_gate = ReplicatedLinear(H, 1, dtype=dtype, device=device)
 
-    def forward(self, x):
-        if self.gate.bias is None and x.dim() == 2:
-            out = self.experts(x, None, reduce=False, router_w=self.gate.weight)
+    def norm_and_route(self, h, residual, norm):
+        """Decode: the O projection's split-K add + RMSNorm (``norm``) with this block's router
+        and top-k in the same launch -> (x, residual, routing), or None when not applicable."""
+        ex = self.experts
+        if (self.gate.bias is not None or ex.scale_input or
+                not moe_ops.splitk_norm_route_ok(h, residual, self.gate.weight, ex.k)):
+            return None
+        return moe_ops.splitk_norm_route(h, residual, norm.weight, norm.eps, self.gate.weight,
+                                         ex.k, ex.renormalize, ex.scoring)
+
+    def forward(self, x, routing=None):
+        # one rank, no shared expert: the combine may be left to the next add + RMSNorm
+        defer = self.shared_expert is None and state.tp_size() == 1
+        if routing is not None:
+            out = self.experts(x, None, reduce=False, routing=routing, defer_combine=defer)
+        elif self.gate.bias is None and x.dim() == 2:
+            out = self.experts(x, None, reduce=False, router_w=self.gate.weight,
+                               defer_combine=defer)
         else:
             out = self.experts(x, self.gate(x), reduce=False)
         a2a = self.experts.a2a          # all-to-all EP: `out` is already complete

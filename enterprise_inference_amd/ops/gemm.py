@@ -208,11 +208,13 @@ def wg_layouts(N: int, K: int, swiglu: bool, max_m: int = MAX_M):
 def attach_wg_packed(model: torch.nn.Module, budget_bytes: int, max_m: int = MAX_M) -> int:
     """Give every decode GEMM weight whose shape has workgroup-packed table picks a packed copy
     (``w._eia_wg[(waves, swiglu)]``) -- the decode kernels then read each workgroup's rows as
-    one sequential stream; prefill keeps the row-major weight for hipBLASLt.  All or nothing:
-    when the copies would exceed ``budget_bytes`` (e.g. a 70B on one GPU) nothing is packed.
-    Returns the bytes added."""
+    one sequential stream; prefill keeps the row-major weight for hipBLASLt.  Weight families
+    are packed whole or not at all, in priority order -- dense linears, then MoE expert
+    gate_up, then MoE expert down (``EIA_MOE_WG_PACK``: 1 both, ``up`` gate_up only, 0 none)
+    -- while the copies fit ``budget_bytes`` (a 70B on one GPU stays row-major; Mixtral at the
+    default budget packs its dense layers and expert gate_up).  Returns the bytes added."""
     from ..models import layers as L
-    plan = []
+    plan = []                    # (priority, weight, key)
     for mod in model.modules():
         w = getattr(mod, "weight", None)
         if not isinstance(w, torch.Tensor) or w.dim() != 2 or w.dtype != torch.bfloat16 or \
@@ -227,8 +229,9 @@ def attach_wg_packed(model: torch.nn.Module, budget_bytes: int, max_m: int = MAX
             forms.append(True)
         for sw in forms:
             for waves in wg_layouts(N, K, sw, max_m):
-                plan.append((w, waves, sw))
-    if os.environ.get("EIA_MOE_WG_PACK", "1") != "0":
+                plan.append((0, w, (waves, sw)))
+    moe_mode = os.environ.get("EIA_MOE_WG_PACK", "1")
+    if moe_mode != "0":
         # MoE expert gate_up [E, 2I, H] (the grouped skinny kernel's decode form, cfg 1 / 3)
         from .moe import moe_cfgs
         for mod in model.modules():
@@ -236,21 +239,37 @@ def attach_wg_packed(model: torch.nn.Module, budget_bytes: int, max_m: int = MAX
             if (isinstance(w13, torch.Tensor) and w13.dim() == 3 and w13.is_cuda
                     and w13.dtype == torch.bfloat16 and w13.is_contiguous()):
                 E, I2, H = w13.shape
-                up = moe_cfgs(I2 // 2, H)[0]
+                up, down = moe_cfgs(I2 // 2, H)
                 if up in (1, 3) and H % 128 == 0:
-                    plan.append((w13, 2 if up == 1 else 4, True))
+                    plan.append((1, w13, (2 if up == 1 else 4, True)))
+                # expert down [E, H, I]: one 16-row tile per wave (grouped cfg 0 / 2), keyed
+                # (waves, False, 1)
+                w2 = getattr(mod, "w2", None)
+                if (moe_mode != "up" and isinstance(w2, torch.Tensor) and w2.dim() == 3
+                        and w2.is_contiguous() and w2.dtype == torch.bfloat16
+                        and down in (0, 2) and w2.shape[2] % 128 == 0):
+                    plan.append((2, w2, (2 if down == 0 else 4, False, 1)))
     seen = set()
+    size = {}
+    for pri, w, key in plan:
+        if (id(w), key) not in seen:
+            seen.add((id(w), key))
+            size[pri] = size.get(pri, 0) + w.numel() * w.element_size()
     total = 0
-    for w, waves, sw in plan:
-        if (id(w), waves, sw) not in seen:
-            seen.add((id(w), waves, sw))
-            total += w.numel() * w.element_size()
-    if total == 0 or total > budget_bytes:
+    take = set()
+    for pri in sorted(size):
+        if total + size[pri] > budget_bytes:
+            break
+        total += size[pri]
+        take.add(pri)
+    if total == 0:
         return 0
-    for w, waves, sw in plan:
+    for pri, w, key in plan:
+        if pri not in take:
+            continue
         d = w.__dict__.setdefault("_eia_wg", {})
-        if (waves, sw) not in d:
-            d[(waves, sw)] = _pack_wg_any(w, waves, sw)
+        if key not in d:
+            d[key] = _pack_wg_any(w, key)
     # a later load_weights (weight hot-swap, tests loading HF tensors into a built engine) must
     # not leave the decode kernels reading stale copies
     load = getattr(model, "load_weights", None)
@@ -264,8 +283,14 @@ def attach_wg_packed(model: torch.nn.Module, budget_bytes: int, max_m: int = MAX
     return total
 
 
-def _pack_wg_any(w: torch.Tensor, waves: int, sw: bool) -> torch.Tensor:
-    cfg = 1024 + {2: 17, 3: 529, 4: 19}[waves]
+def _pack_wg_any(w: torch.Tensor, key) -> torch.Tensor:
+    """key (waves, swiglu): the two-tile forms (cfg 17 / 529 / 19); (waves, False, 1): one
+    16-row tile per wave (the grouped down projection, cfg 0 / 2)."""
+    waves, sw = key[0], key[1]
+    if len(key) > 2 and key[2] == 1:
+        cfg = 1024 + (2 if waves == 4 else 0)
+    else:
+        cfg = 1024 + {2: 17, 3: 529, 4: 19}[waves]
     if w.dim() == 3:               # per expert
         return torch.stack([pack_weight_wg(w.data[e], cfg, sw) for e in range(w.shape[0])])
     return pack_weight_wg(w.data, cfg, sw)
@@ -279,8 +304,8 @@ def refresh_wg_packed(model: torch.nn.Module) -> int:
         d = p.__dict__.get("_eia_wg")
         if not d:
             continue
-        for (waves, sw), wp in d.items():
-            wp.copy_(_pack_wg_any(p, waves, sw))
+        for key, wp in d.items():
+            wp.copy_(_pack_wg_any(p, key))
             n += 1
     return n
 

@@ -95,10 +95,75 @@ def _grouped_ok(x, w13, w2) -> bool:
             and (w13.shape[1] // 2) % 32 == 0 and w2.shape[1] % 64 == 0)
 
 
+# Decode-step fusions of the norms around the MoE block (moe.hip splitk_norm_route_kernel,
+# moe_combine_norm_kernel): the O projection's split-K add + RMSNorm also computes the router
+# logits and top-k, and the experts' combine is left to the next add + RMSNorm.
+FUSED_NORMS = os.environ.get("EIA_MOE_FUSED_NORMS", "1") != "0"
+
+
+class MoECombine:
+    """A decode MoE block's output left as the down projection's fp32 split-K slabs plus the
+    routing: the consumer's add + RMSNorm combines them (``combine_add_rmsnorm``, one launch
+    instead of combine + norm); anything else calls ``materialize``."""
+
+    __slots__ = ("part", "sk", "rows", "topk_w", "inv", "T", "k", "H")
+
+    def __init__(self, part, sk, rows, topk_w, inv, T, k, H):
+        self.part, self.sk, self.rows = part, sk, rows
+        self.topk_w, self.inv, self.T, self.k, self.H = topk_w, inv, T, k, H
+
+    @property
+    def shape(self):
+        return (self.T, self.H)
+
+    def materialize(self) -> torch.Tensor:
+        out = torch.empty(self.T, self.H, dtype=torch.bfloat16, device=self.part.device)
+        check(lib().eia_moe_combine_sk(ptr(self.part), self.sk, self.rows, ptr(self.topk_w),
+                                       ptr(self.inv), self.T, self.k, self.H, ptr(out),
+                                       out.stride(0), stream(out)), "moe_combine_sk")
+        return out
+
+
+def combine_add_rmsnorm(c: MoECombine, residual: torch.Tensor, weight: torch.Tensor,
+                        eps: float):
+    """residual += combine(c); returns (rmsnorm(residual) * weight, residual)."""
+    out = torch.empty(c.T, c.H, dtype=torch.bfloat16, device=residual.device)
+    check(lib().eia_moe_combine_norm(ptr(c.part), c.sk, c.rows, ptr(c.topk_w), ptr(c.inv), c.T,
+                                     c.k, c.H, ptr(residual), ptr(weight), float(eps), ptr(out),
+                                     out.stride(0), stream(out)), "moe_combine_norm")
+    return out, residual
+
+
+def splitk_norm_route_ok(s, residual, router_w: torch.Tensor, k: int) -> bool:
+    from .gemm import SplitK
+    return (FUSED_NORMS and isinstance(s, SplitK) and s.bias is None and s.part.is_cuda
+            and residual is not None and residual.is_contiguous()
+            and residual.dtype == torch.bfloat16 and router_w.dtype == torch.bfloat16
+            and router_w.is_contiguous() and router_w.shape[0] <= 16 and k <= router_w.shape[0]
+            and s.N % 4 == 0 and s.N <= 8192 and router_w.shape[1] == s.N)
+
+
+def splitk_norm_route(s, residual: torch.Tensor, weight: torch.Tensor, eps: float,
+                      router_w: torch.Tensor, k: int, renormalize: bool = True,
+                      scoring: str = "softmax"):
+    """residual += reduce(s); x = rmsnorm(residual) * weight; route(x) -- one launch.
+    Returns (x, residual, (topk weights fp32 [T, k], expert ids int32 [T, k]))."""
+    out = torch.empty(s.M, s.N, dtype=torch.bfloat16, device=residual.device)
+    w = torch.empty(s.M, k, dtype=torch.float32, device=residual.device)
+    ids = torch.empty(s.M, k, dtype=torch.int32, device=residual.device)
+    check(lib().eia_moe_splitk_norm_route(ptr(s.part), s.sk, s.M, s.N, ptr(residual),
+                                          ptr(weight), float(eps), ptr(out), out.stride(0),
+                                          ptr(router_w), router_w.shape[0], k,
+                                          1 if renormalize else 0, SCORING[scoring], ptr(w),
+                                          ptr(ids), stream(out)), "moe_splitk_norm_route")
+    return out, residual, (w, ids)
+
+
 def fused_moe(x: torch.Tensor, w13: torch.Tensor, w2: torch.Tensor, topk_w: torch.Tensor,
               topk_ids: torch.Tensor, expert_range: Optional[Tuple[int, int]] = None,
-              act: str = "silu") -> torch.Tensor:
-    """x [T, H]; w13 [E_local, 2I, H] ([gate; up] rows); w2 [E_local, H, I] -> [T, H]."""
+              act: str = "silu", defer_combine: bool = False):
+    """x [T, H]; w13 [E_local, 2I, H] ([gate; up] rows); w2 [E_local, H, I] -> [T, H].
+    ``defer_combine``: the decode path may return a ``MoECombine`` for the next add + norm."""
     T, H = x.shape
     El = w13.shape[0]
     e_lo, e_hi = expert_range or (0, El)
@@ -110,7 +175,8 @@ def fused_moe(x: torch.Tensor, w13: torch.Tensor, w2: torch.Tensor, topk_w: torc
         return ref.fused_moe(x, w13, w2, tw, ids.clamp(0, El - 1).to(torch.int32), act)
     avg = T * k / max(1, El)
     if act == "silu" and avg <= 96 and _grouped_ok(x, w13, w2):
-        return _fused_moe_grouped(x, w13, w2, topk_w, topk_ids, e_lo, e_hi)
+        return _fused_moe_grouped(x, w13, w2, topk_w, topk_ids, e_lo, e_hi,
+                                  defer_combine=defer_combine)
     if act == "silu" and _mfma_ok(x, w13, w2) and avg <= MFMA_MAX_ROWS:
         return _fused_moe_grouped(x, w13, w2, topk_w, topk_ids, e_lo, e_hi, mfma=True)
     if _grouped_ok(x, w13, w2):
@@ -127,7 +193,8 @@ def _mfma_ok(x, w13, w2) -> bool:
             and w13.is_contiguous() and w2.is_contiguous() and x.stride(1) == 1)
 
 
-def _fused_moe_grouped(x, w13, w2, topk_w, topk_ids, e_lo, e_hi, mfma: bool = False):
+def _fused_moe_grouped(x, w13, w2, topk_w, topk_ids, e_lo, e_hi, mfma: bool = False,
+                       defer_combine: bool = False):
     T, H = x.shape
     El, I2, _ = w13.shape
     I = I2 // 2
@@ -158,16 +225,26 @@ def _fused_moe_grouped(x, w13, w2, topk_w, topk_ids, e_lo, e_hi, mfma: bool = Fa
         check(lib().eia_moe_gemm(ptr(x), x.stride(0), ptr(w_up), w13.stride(1), None, ptr(h1),
                                  h1.stride(0), I2, H, El, ptr(offs), ptr(row_idx), mt, 2,
                                  up_cfg, st), "moe_gemm_gate_up")
+        w_down = w2
+        if packed_down := getattr(w2, "_eia_wg", None):
+            wp = packed_down.get((4 if down_cfg == 2 else 2, False, 1)) if down_cfg in (0, 2) \
+                else None
+            if wp is not None:       # workgroup-packed expert down (one tile per wave)
+                w_down = wp
+                down_cfg |= 1024
         if DOWN_SK > 1 and I % (DOWN_SK * 256) == 0:
             part = torch.empty(DOWN_SK, max(1, n), H, dtype=torch.float32, device=dev)
-            check(lib().eia_moe_gemm_sk(ptr(h1), h1.stride(0), ptr(w2), w2.stride(1), ptr(part),
-                                        max(1, n), H, I, El, ptr(offs), None, mt, DOWN_SK,
-                                        down_cfg, st), "moe_gemm_down_sk")
+            check(lib().eia_moe_gemm_sk(ptr(h1), h1.stride(0), ptr(w_down), w2.stride(1),
+                                        ptr(part), max(1, n), H, I, El, ptr(offs), None, mt,
+                                        DOWN_SK, down_cfg, st), "moe_gemm_down_sk")
+            if (defer_combine and FUSED_NORMS and k <= 2 and H % 4 == 0 and H <= 8192
+                    and DOWN_SK in (1, 2, 4) and x.dtype == torch.bfloat16):
+                return MoECombine(part, DOWN_SK, max(1, n), topk_w, inv, T, k, H)
             out = torch.empty(T, H, dtype=x.dtype, device=dev)
             check(lib().eia_moe_combine_sk(ptr(part), DOWN_SK, max(1, n), ptr(topk_w), ptr(inv),
                                            T, k, H, ptr(out), out.stride(0), st), "moe_combine_sk")
             return out
-        check(lib().eia_moe_gemm(ptr(h1), h1.stride(0), ptr(w2), w2.stride(1), None, ptr(h2),
+        check(lib().eia_moe_gemm(ptr(h1), h1.stride(0), ptr(w_down), w2.stride(1), None, ptr(h2),
                                  h2.stride(0), H, I, El, ptr(offs), None, mt, 0,
                                  down_cfg, st), "moe_gemm_down")
     out = torch.empty(T, H, dtype=x.dtype, device=dev)

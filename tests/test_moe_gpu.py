@@ -226,7 +226,7 @@ def test_all_to_all_ep_captures_in_hip_graph(monkeypatch):
 
 @pytest.mark.parametrize("T,E,k,H,I", [(1, 8, 2, 512, 256), (33, 8, 2, 1024, 512),
                                        (65, 8, 2, 4096, 1792)])
-def test_fused_moe_wg_packed_gate_up(T, E, k, H, I):
+def test_fused_moe_wg_packed_gate_up(monkeypatch, T, E, k, H, I):
     """Decode MoE with the expert gate_up read from its workgroup-packed copy (cfg bit 10,
     attach_wg_packed's per-expert packing) equals the row-major run bit for bit."""
     from enterprise_inference_amd.ops import gemm, moe
@@ -243,3 +243,72 @@ def test_fused_moe_wg_packed_gate_up(T, E, k, H, I):
         [gemm.pack_weight_wg(w13[e], cfg, True) for e in range(E)])}
     packed = moe.fused_moe(x, w13, w2, w, ids)
     assert torch.equal(plain, packed)
+    # + the expert down projection packed one tile per wave (grouped cfg 0 / 2), split-K and not
+    down = moe.moe_cfgs(I, H)[1]
+    w2.__dict__["_eia_wg"] = {(4 if down == 2 else 2, False, 1): torch.stack(
+        [gemm.pack_weight_wg(w2[e], 1024 + down, False) for e in range(E)])}
+    for sk in (1, 4):
+        monkeypatch.setattr(moe, "DOWN_SK", sk)
+        w2d = w2.__dict__.pop("_eia_wg")
+        plain = moe.fused_moe(x, w13, w2, w, ids)
+        w2.__dict__["_eia_wg"] = w2d
+        both = moe.fused_moe(x, w13, w2, w, ids)
+        assert torch.equal(plain, both), sk
+
+
+@pytest.mark.parametrize("M,H,E,k,sk", [(1, 4096, 8, 2, 4), (65, 4096, 8, 2, 4),
+                                        (33, 2048, 16, 1, 2), (17, 6144, 8, 2, 3)])
+def test_splitk_norm_route_matches_unfused(M, H, E, k, sk):
+    """O-projection split-K add + RMSNorm + router + top-k in one launch (moe.hip
+    splitk_norm_route_kernel) == splitk_add_rmsnorm then route: residual and normalised row bit
+    for bit, same experts, same weights; and the normalised row vs an fp32 reference."""
+    from enterprise_inference_amd.ops import gemm, moe
+    torch.manual_seed(M + H)
+    part = torch.randn(sk, M, H, device=DEV) * 0.5
+    res0 = torch.randn(M, H, device=DEV, dtype=BF)
+    nw = (1 + 0.1 * torch.randn(H, device=DEV)).to(BF)
+    rw = (torch.randn(E, H, device=DEV) * H ** -0.5).to(BF)
+    s = gemm.SplitK(part, sk, M, H)
+    r1 = res0.clone()
+    x1, _ = gemm.splitk_add_rmsnorm(s, r1, nw, 1e-5)
+    w1, i1 = moe.route(x1, rw, k, True)
+    r2 = res0.clone()
+    x2, _, (w2, i2) = moe.splitk_norm_route(s, r2, nw, 1e-5, rw, k, True)
+    torch.cuda.synchronize()
+    assert torch.equal(r1, r2)
+    assert torch.equal(x1, x2)
+    assert torch.equal(i1.sort(-1).values, i2.sort(-1).values)
+    o1, o2 = i1.argsort(-1), i2.argsort(-1)
+    assert torch.allclose(w1.gather(1, o1), w2.gather(1, o2), atol=1e-5)
+    hr = (part.sum(0) + res0.float()).to(BF).float()
+    ref_x = hr * torch.rsqrt(hr.pow(2).mean(-1, keepdim=True) + 1e-5) * nw.float()
+    assert (x2.float() - ref_x).abs().max() < 3e-2 * ref_x.abs().max()
+
+
+@pytest.mark.parametrize("T,E,k,H,I", [(1, 8, 2, 4096, 1024), (65, 8, 2, 4096, 2048),
+                                       (33, 16, 1, 2048, 1024)])
+def test_moe_combine_norm_matches_unfused(T, E, k, H, I):
+    """The decode MoE output left as split-K slabs (fused_moe defer_combine -> MoECombine) and
+    combined inside the next add + RMSNorm (moe_combine_norm_kernel) == combine_sk then
+    fused_add_rms_norm: residual bit for bit, normalised row within one bf16 step."""
+    from enterprise_inference_amd.ops import moe, norm
+    torch.manual_seed(T + H)
+    x = torch.randn(T, H, device=DEV, dtype=BF)
+    w13 = (torch.randn(E, 2 * I, H, device=DEV) * H ** -0.5).to(BF)
+    w2 = (torch.randn(E, H, I, device=DEV) * I ** -0.5).to(BF)
+    w, ids = moe.topk_route(torch.randn(T, E, device=DEV), k, True)
+    c = moe.fused_moe(x, w13, w2, w, ids, defer_combine=True)
+    assert isinstance(c, moe.MoECombine)
+    y = c.materialize()
+    ref_y = ref.fused_moe(x.cpu(), w13.cpu(), w2.cpu(), w.cpu(), ids.cpu()).float()
+    assert (y.float().cpu() - ref_y).abs().max() < 3e-2 + 3e-2 * ref_y.abs().max()
+    res0 = torch.randn(T, H, device=DEV, dtype=BF)
+    nw = (1 + 0.1 * torch.randn(H, device=DEV)).to(BF)
+    r1 = res0.clone()
+    o1, _ = norm.fused_add_rms_norm(y, r1, nw, 1e-5)
+    r2 = res0.clone()
+    o2, _ = moe.combine_add_rmsnorm(c, r2, nw, 1e-5)
+    torch.cuda.synchronize()
+    assert torch.equal(r1, r2)
+    d = (o1.float() - o2.float()).abs()
+    assert d.max() <= 1.01 * o1.float().abs().max() * 2 ** -7, d.max()
