@@ -156,11 +156,11 @@ class ModelRunner:
         if self.is_gpu and os.environ.get("EIA_WG_PACK", "1") != "0":
             # decode copies of the GEMM weights in the workgroup-packed layout (ops/gemm.py
             # attach_wg_packed), before the KV cache is sized from the free memory; at most
-            # EIA_WG_PACK_BUDGET (fraction of the device, default 0.3): a 70B on one GPU keeps
+            # EIA_WG_PACK_BUDGET (fraction of the device, default 0.35): a 70B on one GPU keeps
             # the row-major weights only
             from ..ops import gemm as _g
             total = torch.cuda.get_device_properties(self.device).total_memory
-            frac = float(os.environ.get("EIA_WG_PACK_BUDGET", "0.3"))
+            frac = float(os.environ.get("EIA_WG_PACK_BUDGET", "0.35"))
             self.wg_packed_bytes = _g.attach_wg_packed(self.model, int(frac * total),
                                                        min(_g.MAX_M, cfg.scheduler.max_num_seqs))
         m = cfg.model
