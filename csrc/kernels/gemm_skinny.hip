@@ -680,7 +680,7 @@ int launch_mt(int cfg, const bf16_t* X, long ldx, const bf16_t* W, long ldw, con
       }
 #undef EIA_GL
     }
-    if (cfg & 1024) {  // workgroup-packed weights (pack_weight_wg), register-staged, 2 stages
+    if (cfg & 1024) {  // workgroup-packed weights (pack_weight_wg), register-staged, 2-4 stages
 #define EIA_CFGW(NT_, W_, S_, KC_)                                                            \
   return launch_cfg<MT, NT_, W_, S_, GROUPED, KC_, false, 2>(X, ldx, W, ldw, bias, out, ldo, M, N, \
                                                              K, sk, mode, experts, offs, row_idx,   \
@@ -689,9 +689,14 @@ int launch_mt(int cfg, const bf16_t* X, long ldx, const bf16_t* W, long ldw, con
         switch (cfg & ~1024) {
           case 1: EIA_CFGW(2, 2, 2, 256);
           case 3: EIA_CFGW(2, 4, 2, 256);
+          case 5: EIA_CFGW(2, 2, 3, 256);
+          case 7: EIA_CFGW(2, 4, 3, 256);
           case 17: EIA_CFGW(2, 2, 2, 128);
           case 19: EIA_CFGW(2, 4, 2, 128);
+          case 21: EIA_CFGW(2, 2, 3, 128);
+          case 23: EIA_CFGW(2, 4, 3, 128);
           case 512 + 17: EIA_CFGW(2, 3, 2, 128);
+          case 512 + 21: EIA_CFGW(2, 3, 3, 128);
           default: break;
         }
       }
@@ -809,11 +814,15 @@ int check_shape(int N, int K, int sk, int mode, int cfg) {
   if (sk < 1 || cfg < 0 || (cfg & ~(16 | 32 | 64 | 128 | 256 | 512 | 1024)) > 11 ||
       K % (sk * kc) != 0)
     return EIA_BAD_SHAPE;
-  // workgroup-packed: the forms built above (2 stages; the one-tile forms 0 / 2 are grouped
+  // workgroup-packed: the forms built above (2-4 stages; the one-tile forms 0 / 2 are grouped
   // only -- the MoE down projection)
-  if ((cfg & 1024) && (cfg & ~1024) > 3 && (cfg & ~1024) != 17 && (cfg & ~1024) != 19 &&
-      (cfg & ~1024) != 512 + 17)
-    return EIA_BAD_SHAPE;
+  if (cfg & 1024) {
+    switch (cfg & ~1024) {
+      case 0: case 1: case 2: case 3: case 5: case 7: case 17: case 19: case 21: case 23:
+      case 512 + 17: case 512 + 21: break;
+      default: return EIA_BAD_SHAPE;
+    }
+  }
   // 3-wave form: register-staged, plain layout, no SwiGLU pairing, 2-3 stages
   if ((cfg & 512) && ((cfg & (2 | 8 | 32 | 64 | 128 | 256)) || mode == MODE_SWIGLU))
     return EIA_BAD_SHAPE;
@@ -843,8 +852,8 @@ int check_shape(int N, int K, int sk, int mode, int cfg) {
 // bit 7 -> LDS-DMA ring kernel (with bits 1 and 4; bits 2-3 = ring depth - 2)
 // bit 8 -> 7 waves of (gate, up) pairs per workgroup (SwiGLU only; cfg 273 = + bits 0 and 4):
 //          70B's 1792 pairs are exactly 256 workgroups, where 4-wave workgroups leave 448
-// bit 10 -> workgroup-packed W (pack_weight_wg; ldw must be K) with cfg 1, 3, 17, 19 or 529
-//          (grouped: 0-3): each workgroup streams its rows as one sequential run
+// bit 10 -> workgroup-packed W (pack_weight_wg; ldw must be K) with cfg 1, 3, 5, 7, 17, 19, 21,
+//          23, 529 or 533 (grouped: 0-3): each workgroup streams its rows as one sequential run
 // bit 9 -> 3 waves per workgroup (+ bits 0, 2, 4): Llama-8B's QKV (6144 rows) as 64 x 96-row
 //          tiles x split-K 4 = 256 workgroups, where 4-wave (128-row) tiles leave 192 -- a
 //          decode GEMM streams at a per-CU rate (~20 GB/s), so idle CUs are lost bandwidth

@@ -78,6 +78,16 @@ class AsyncLLMEngine:
     async def generate(self, request_id: str, prompt: Optional[str], params: SamplingParams,
                        prompt_token_ids=None, priority: int = 0,
                        multi_modal_data=None) -> AsyncIterator[RequestOutput]:
+        async for item in self.submit(request_id, prompt, params, prompt_token_ids, priority,
+                                      multi_modal_data):
+            yield item
+
+    can_submit = True
+
+    def submit(self, request_id: str, prompt: Optional[str], params: SamplingParams,
+               prompt_token_ids=None, priority: int = 0,
+               multi_modal_data=None) -> AsyncIterator[RequestOutput]:
+        """Queue the request now and return its output iterator (MPEngineClient.submit)."""
         self.check_health()
         q: asyncio.Queue = asyncio.Queue()
         loop = asyncio.get_running_loop()
@@ -86,6 +96,9 @@ class AsyncLLMEngine:
         self._cmds.put(("add", request_id, prompt, params, prompt_token_ids, time.time(), priority,
                         multi_modal_data))
         self._wake.set()
+        return self._outputs(request_id, q)
+
+    async def _outputs(self, request_id: str, q: asyncio.Queue) -> AsyncIterator[RequestOutput]:
         try:
             while True:
                 item = await q.get()

@@ -430,6 +430,22 @@ class MPEngineClient:
             await self.start()
         if not self.ready:
             await self.wait_ready()
+        async for item in self.submit(request_id, prompt, params, prompt_token_ids, priority,
+                                      multi_modal_data):
+            yield item
+
+    @property
+    def can_submit(self) -> bool:
+        return self._writer is not None and self.ready
+
+    def submit(self, request_id: str, prompt: Optional[str], params, prompt_token_ids=None,
+               priority: int = 0, multi_modal_data=None):
+        """Hand the request to the core NOW (the "add" frame is written before this returns)
+        and return the async iterator of its outputs.  ``generate`` only sends when its
+        iterator is first advanced -- for a streaming response that is after the handler has
+        returned and the response started, so a burst of concurrent requests reached the core
+        spread over the event loop's interleaving of their handlers.  Needs ``can_submit``."""
+        self.check_health()
         if prompt_token_ids is None:
             prompt_token_ids = self.tokenizer.encode(prompt)
         q: asyncio.Queue = asyncio.Queue()
@@ -438,6 +454,9 @@ class MPEngineClient:
         self._reqs[request_id] = _ReqState(q, prompt, list(prompt_token_ids))
         self._send(("add", request_id, prompt, params, prompt_token_ids, time.time(), priority,
                     multi_modal_data))
+        return self._outputs(request_id, q)
+
+    async def _outputs(self, request_id: str, q: asyncio.Queue):
         finished = False
         try:
             while True:

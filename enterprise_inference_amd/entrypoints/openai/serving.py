@@ -10,6 +10,7 @@ from __future__ import annotations
 
 import asyncio
 import json
+import os
 import time
 from typing import AsyncIterator, Dict, List, Optional, Tuple
 
@@ -75,6 +76,18 @@ def fast_chat_chunk(head: str, index: int, content: Optional[str], finish_reason
     delta = ('{"content":' + _dumps(content) + ',"tool_calls":[]}') if content \
         else '{"tool_calls":[]}'
     return head + str(index) + ',"delta":' + delta + _chunk_tail(finish_reason, stop_reason)
+
+
+EAGER_SUBMIT = os.environ.get("EIA_EAGER_SUBMIT", "1") != "0"
+
+
+def _start(engine, request_id, prompt, params, **kw) -> AsyncIterator:
+    """The request's output iterator, with the request already handed to the engine when the
+    engine supports it (``submit``): a burst of concurrent requests then reaches the engine
+    as their handlers run instead of when each streaming response first iterates."""
+    if EAGER_SUBMIT and getattr(engine, "can_submit", False):
+        return engine.submit(request_id, prompt, params, **kw)
+    return engine.generate(request_id, prompt, params, **kw)
 
 
 async def _merge(gens: List[AsyncIterator]) -> AsyncIterator[Tuple[int, object]]:
@@ -205,8 +218,8 @@ async def create_completion(req: CompletionRequest, ctx: ServingContext):
            for p in prompts]
     params = [req.to_sampling_params(ctx.default_max_tokens(len(ids)), req.logprobs,
                                      ctx.generation_defaults) for _, ids in enc]
-    gens = [ctx.engine.generate(f"{rid}-{i}", text, params[i], prompt_token_ids=ids,
-                                priority=req.priority)
+    gens = [_start(ctx.engine, f"{rid}-{i}", text, params[i], prompt_token_ids=ids,
+                   priority=req.priority)
             for i, (text, ids) in enumerate(enc)]
     n = params[0].n
 
@@ -437,8 +450,8 @@ async def create_chat_completion(req: ChatCompletionRequest, ctx: ServingContext
         params.guided_json = fn.parameters or {}
     rid = random_id("chatcmpl")
     created = int(time.time())
-    gen = ctx.engine.generate(rid, text, params, prompt_token_ids=ids, priority=req.priority,
-                              **({"multi_modal_data": mm} if mm else {}))
+    gen = _start(ctx.engine, rid, text, params, prompt_token_ids=ids, priority=req.priority,
+                 **({"multi_modal_data": mm} if mm else {}))
     n = params.n
 
     if not req.stream:

@@ -46,7 +46,7 @@ PACKED_CFGS = tuple(64 + c for c in (1, 2, 3, 7, 17, 18, 19, 22, 23, 51, 55, 146
 # bit7: LDS-DMA ring kernel, 4 waves, KC 128: 146 | (NT-1) | (depth-2) << 2 (+64 packed)
 GLDS_CFGS = (146, 147, 150, 151, 154, 155)
 # bit10: workgroup-packed weights (pack_weight_wg) for the forms the decode tables use
-WGPACK_CFGS = tuple(1024 + c for c in (1, 3, 17, 19, 529))
+WGPACK_CFGS = tuple(1024 + c for c in (1, 3, 5, 7, 17, 19, 21, 23, 529, 533))
 GLDS_PACKED_CFGS = tuple(c + 64 for c in GLDS_CFGS)
 
 

@@ -191,3 +191,45 @@ def test_openapi_spec_in_sync():
         doc = yaml.safe_load(f)
     for p in ("/v1/chat/completions", "/v1/completions", "/v1/embeddings", "/embed", "/rerank"):
         assert p in doc["paths"], p
+
+
+def test_requests_reach_engine_before_stream_iterates(monkeypatch):
+    """Handlers hand a request to the engine while they run (engine.submit), not when the
+    streaming response first advances its iterator -- a burst of concurrent requests then
+    reaches the engine core together; engines without submit keep the lazy generate."""
+    from enterprise_inference_amd.entrypoints.openai import serving
+
+    calls = []
+
+    class Eager:
+        can_submit = True
+
+        def submit(self, rid, prompt, params, **kw):
+            calls.append(("submit", rid, kw.get("prompt_token_ids")))
+
+            async def it():
+                yield "out"
+            return it()
+
+    class Lazy:
+        def generate(self, rid, prompt, params, **kw):
+            calls.append(("generate-created", rid))
+
+            async def it():
+                calls.append(("generate-started", rid))
+                yield "out"
+            return it()
+
+    serving._start(Eager(), "r1", None, None, prompt_token_ids=[1, 2])
+    assert calls == [("submit", "r1", [1, 2])]
+    calls.clear()
+    g = serving._start(Lazy(), "r2", None, None)
+    assert calls == [("generate-created", "r2")]
+    monkeypatch.setattr(serving, "EAGER_SUBMIT", False)
+    calls.clear()
+
+    class Both(Eager, Lazy):
+        pass
+    serving._start(Both(), "r3", None, None)
+    assert calls == [("generate-created", "r3")]
+    del g
