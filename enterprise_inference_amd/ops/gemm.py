@@ -291,8 +291,11 @@ def _pack_wg_any(w: torch.Tensor, key) -> torch.Tensor:
         cfg = 1024 + (2 if waves == 4 else 0)
     else:
         cfg = 1024 + {2: 17, 3: 529, 4: 19}[waves]
-    if w.dim() == 3:               # per expert
-        return torch.stack([pack_weight_wg(w.data[e], cfg, sw) for e in range(w.shape[0])])
+    if w.dim() == 3:               # per expert, filled in place (no E-sized temporaries)
+        out = torch.empty_like(w.data)
+        for e in range(w.shape[0]):
+            out[e].copy_(pack_weight_wg(w.data[e], cfg, sw))
+        return out
     return pack_weight_wg(w.data, cfg, sw)
 
 
@@ -305,7 +308,11 @@ def refresh_wg_packed(model: torch.nn.Module) -> int:
         if not d:
             continue
         for key, wp in d.items():
-            wp.copy_(_pack_wg_any(p, key))
+            if p.dim() == 3:       # per expert: one expert-sized temporary at a time
+                for e in range(p.shape[0]):
+                    wp[e].copy_(_pack_wg_any(p[e], key))
+            else:
+                wp.copy_(_pack_wg_any(p, key))
             n += 1
     return n
 

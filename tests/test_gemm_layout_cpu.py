@@ -83,3 +83,27 @@ def test_refresh_wg_packed_follows_weight_reload():
     assert gemm.refresh_wg_packed(lin) == 1
     assert wp.data_ptr() == ptr
     assert torch.equal(wp, gemm.pack_weight_wg(lin.weight.data, cfg, False))
+
+
+def test_refresh_wg_packed_experts_in_place():
+    """Per-expert packed copies ([E, 2I, H] gate_up, [E, H, I] down one-tile form) are refreshed
+    expert by expert into the same storage."""
+    m = torch.nn.Module()
+    m.w13 = torch.nn.Parameter(torch.randn(3, 256, 256).to(torch.bfloat16), requires_grad=False)
+    m.w2 = torch.nn.Parameter(torch.randn(3, 128, 256).to(torch.bfloat16), requires_grad=False)
+    up = gemm._pack_wg_any(m.w13, (4, True))
+    dn = gemm._pack_wg_any(m.w2, (4, False, 1))
+    m.w13.__dict__["_eia_wg"] = {(4, True): up}
+    m.w2.__dict__["_eia_wg"] = {(4, False, 1): dn}
+    for e in range(3):
+        assert torch.equal(up[e], gemm.pack_weight_wg(m.w13.data[e], 1024 + 19, True))
+        assert torch.equal(dn[e], gemm.pack_weight_wg(m.w2.data[e], 1024 + 2, False))
+    with torch.no_grad():
+        m.w13.copy_(torch.randn(3, 256, 256).to(torch.bfloat16))
+        m.w2.copy_(torch.randn(3, 128, 256).to(torch.bfloat16))
+    p_up, p_dn = up.data_ptr(), dn.data_ptr()
+    assert gemm.refresh_wg_packed(m) == 2
+    assert up.data_ptr() == p_up and dn.data_ptr() == p_dn
+    for e in range(3):
+        assert torch.equal(up[e], gemm.pack_weight_wg(m.w13.data[e], 1024 + 19, True))
+        assert torch.equal(dn[e], gemm.pack_weight_wg(m.w2.data[e], 1024 + 2, False))
