@@ -61,6 +61,7 @@ _SIGNATURES = {
     "eia_moe_combine_sk": [P, I, I, P, P, I, I, I, P, L, S],
     "eia_moe_grouped_gemm": [P, L, IP, P, I, I, I, IP, I, I, P, L, S],
     "eia_gemm_skinny": [P, L, P, L, P, P, L, I, I, I, I, I, I, S],
+    "eia_gemm_prefill": [P, L, P, L, P, L, I, I, I, I, S],
     "eia_splitk_reduce": [P, I, I, I, P, P, L, S],
     "eia_mlp_fused": [P, L, P, P, P, P, IP, I, I, I, I, S],
     "eia_mlp_fused_plan": [I, I, I, I, P],

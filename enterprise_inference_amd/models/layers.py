@@ -90,6 +90,12 @@ class MergedColumnParallelLinear(ColumnParallelLinear):
         if act == "silu" and self.bias is None and len(self.out_sizes) == 2 and \
                 x.dim() == 2 and gemm.skinny_ok(x, self.weight, swiglu=True):
             return gemm.swiglu_gemm(x, self.weight)
+        if (gemm.PREFILL_SWIGLU and act == "silu" and self.bias is None
+                and len(self.out_sizes) == 2 and x.dim() == 2
+                and x.shape[0] >= gemm.PREFILL_MIN_M
+                and gemm.prefill_gemm_ok(x, self.weight, swiglu=True)):
+            # prompt-sized: the SwiGLU epilogue inside the MFMA GEMM (gemm_prefill.hip)
+            return gemm.prefill_gemm(x, self.weight, swiglu=True)
         from ..ops import activation
         return activation.act_and_mul(gemm.linear(x, self.weight, self.bias), act)
 

@@ -479,6 +479,38 @@ def linear(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = None
     return F.linear(x, w, bias)
 
 
+# --------------------------------------------------------------------------- prefill K7
+# Prompt-sized gate_up with the SwiGLU epilogue in the GEMM (csrc/kernels/gemm_prefill.hip):
+# the [T, 2I] intermediate never reaches HBM and act_and_mul disappears.  EIA_PREFILL_SWIGLU:
+# 1 on, 0 off (hipBLASLt + act_and_mul).
+PREFILL_SWIGLU = os.environ.get("EIA_PREFILL_SWIGLU", "0") == "1"
+PREFILL_MIN_M = int(os.environ.get("EIA_PREFILL_SWIGLU_MIN_M", "256"))
+
+
+def prefill_gemm_ok(x: torch.Tensor, w: torch.Tensor, swiglu: bool) -> bool:
+    if DISABLE or not use_hip(x, w) or x.dim() != 2 or x.dtype != torch.bfloat16 or \
+            w.dtype != torch.bfloat16:
+        return False
+    M, K = x.shape
+    N = w.shape[0]
+    if w.shape[1] != K or K % 64 or x.stride(1) != 1 or w.stride(1) != 1 or x.stride(0) % 8 or \
+            w.stride(0) % 8:
+        return False
+    return (N % 2 == 0 and (N // 2) % 128 == 0) if swiglu else N % 256 == 0
+
+
+def prefill_gemm(x: torch.Tensor, w: torch.Tensor, swiglu: bool = False) -> torch.Tensor:
+    """x [M, K] @ w[N, K]^T on the prompt-sized MFMA kernel; swiglu: w = [gate; up] (N = 2I)
+    -> silu(x Wg^T) * (x Wu^T) [M, I]."""
+    M, K = x.shape
+    N = w.shape[0]
+    out = torch.empty(M, N // 2 if swiglu else N, dtype=torch.bfloat16, device=x.device)
+    check(lib().eia_gemm_prefill(ptr(x), x.stride(0), ptr(w), w.stride(0), ptr(out),
+                                 out.stride(0), M, N, K, MODE_SWIGLU if swiglu else MODE_BF16,
+                                 stream(x)), "gemm_prefill")
+    return out
+
+
 # --------------------------------------------------------------------------- fused decode MLP
 # gate_up + SwiGLU and the split-K down projection in ONE launch (csrc/kernels/mlp_fused.hip):
 # 256 balanced producers (every CU streams the same gate/up bytes) hand h to the down
