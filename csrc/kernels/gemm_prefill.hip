@@ -318,7 +318,7 @@ template <bool SWIGLU>
 __global__ void __launch_bounds__(PTHREADS, 1)
 gemm_prefill_kernel_v3(const bf16_t* __restrict__ X, long ldx, const bf16_t* __restrict__ W,
                        long ldw, bf16_t* __restrict__ out, long ldo, int M, int K, int inter,
-                       int ntm, int ntn) {
+                       int ntm, int ntn, int prio) {
   extern __shared__ __align__(16) char plds[];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wr = wave >> 2, wc = wave & 3;
@@ -384,6 +384,7 @@ gemm_prefill_kernel_v3(const bf16_t* __restrict__ X, long ldx, const bf16_t* __r
     pbarrier();
     if (kt + 1 < nk) read(kt + 1, an, bn);
     const bool more = kt + QNS < nk;
+    if (prio) __builtin_amdgcn_s_setprio(1);      // the MFMA burst wins issue arbitration
 #pragma unroll
     for (int mt = 0; mt < 8; ++mt) {
       if ((mt & 1) == 0 && more) {
@@ -395,6 +396,7 @@ gemm_prefill_kernel_v3(const bf16_t* __restrict__ X, long ldx, const bf16_t* __r
       for (int nt = 0; nt < 4; ++nt)
         acc[nt][mt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ac[nt], bc[mt], acc[nt][mt], 0, 0, 0);
     }
+    if (prio) __builtin_amdgcn_s_setprio(0);
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // tile kt+1 is in registers
   };
 
@@ -461,9 +463,13 @@ int launch_prefill(const bf16_t* X, long ldx, const bf16_t* W, long ldw, bf16_t*
   }
   const int ntm = (M + PBM - 1) / PBM;
   const int ntn = SWIGLU ? (N / 2) / (PBN / 2) : N / PBN;
+  static const int prio = [] {        // EIA_PREFILL_GEMM_PRIO=1: s_setprio around MFMA bursts
+    const char* e = getenv("EIA_PREFILL_GEMM_PRIO");
+    return e != nullptr ? atoi(e) : 0;
+  }();
   if (variant == 3 && K % QBK == 0)
     hipLaunchKernelGGL(gemm_prefill_kernel_v3<SWIGLU>, dim3(ntm * ntn), dim3(PTHREADS),
-                       QNS * QSTAGE, st, X, ldx, W, ldw, out, ldo, M, K, N / 2, ntm, ntn);
+                       QNS * QSTAGE, st, X, ldx, W, ldw, out, ldo, M, K, N / 2, ntm, ntn, prio);
   else if (variant == 2 && K % QBK == 0)
     hipLaunchKernelGGL(gemm_prefill_kernel_v2<SWIGLU>, dim3(ntm * ntn), dim3(PTHREADS),
                        QNS * QSTAGE, st, X, ldx, W, ldw, out, ldo, M, K, N / 2, ntm, ntn);
