@@ -443,11 +443,129 @@ gemm_prefill_kernel_v3(const bf16_t* __restrict__ X, long ldx, const bf16_t* __r
   }
 }
 
+// Variant 4: variant 2's four 32 KiB stages with FOUR waves of 128 x 128 (2 x 2): one wave per
+// SIMD, 8 x 8 accumulator tiles (256 registers, the AGPR half of the file) -- 64 MFMAs per 16
+// fragment reads per K-step instead of 32 per 12, and no two waves sharing a SIMD's MFMA pipe.
+constexpr int VTHREADS = 256;
+
+template <bool SWIGLU>
+__global__ void __launch_bounds__(VTHREADS, 1)
+gemm_prefill_kernel_v4(const bf16_t* __restrict__ X, long ldx, const bf16_t* __restrict__ W,
+                       long ldw, bf16_t* __restrict__ out, long ldo, int M, int K, int inter,
+                       int ntm, int ntn, int prio) {
+  extern __shared__ __align__(16) char plds[];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wr = wave >> 1, wc = wave & 1;
+  const int nwg = ntm * ntn;
+  const int orig = blockIdx.x;
+  const int xcd = orig & 7, q8 = nwg >> 3, r8 = nwg & 7;
+  const int pid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (orig >> 3);
+  const int per_group = PGROUP_M * ntn;
+  const int first_m = (pid / per_group) * PGROUP_M;
+  const int gsz = min(ntm - first_m, PGROUP_M);
+  const int pm = first_m + (pid % per_group) % gsz;
+  const int pn = (pid % per_group) / gsz;
+  const int m0 = pm * PBM;
+  const int n0 = SWIGLU ? pn * (PBN / 2) : pn * PBN;
+
+  // DMA: instruction i = 4 wave + j (j < 4) of each operand covers rows 16 i + (lane >> 2)
+  const bf16_t* wsrc[4];
+  const bf16_t* xsrc[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int row = 16 * (4 * wave + j) + (lane >> 2);
+    const int c = (lane & 3) ^ ((row >> 1) & 3);
+    const int wrow = SWIGLU ? (row < 128 ? n0 + row : inter + n0 + row - 128) : n0 + row;
+    wsrc[j] = W + (long)wrow * ldw + 8 * c;
+    xsrc[j] = X + (long)min(m0 + row, M - 1) * ldx + 8 * c;
+  }
+  const unsigned lds0 = (unsigned)(uintptr_t)plds;
+  auto piece = [&](int kt, int p) {     // p < 8: W instructions 0-3, then X 0-3
+    const unsigned sb = lds0 + (kt % QNS) * QSTAGE + ((p >> 2) ? QTILE : 0);
+    const unsigned off = (unsigned)(4 * wave + (p & 3)) * 1024u;
+    const bf16_t* src = (p >> 2) ? xsrc[p & 3] : wsrc[p & 3];
+    pglds16(src + kt * QBK, sb + off);
+  };
+
+  // fragments: W tile nt (SWIGLU: nt < 4 gate rows 64 wc + 16 nt, nt >= 4 the matching up rows)
+  const int fr = lane & 15, fc = lane >> 4;
+  const unsigned abase = qswz((SWIGLU ? 64 : 128) * wc + fr, fc);
+  const unsigned bbase = QTILE + qswz(128 * wr + fr, fc);
+  auto aoff = [&](int nt) {
+    return abase + (unsigned)(SWIGLU ? (nt < 4 ? 1024 * nt : 8192 + 1024 * (nt - 4)) : 1024 * nt);
+  };
+
+  f32x4 acc[8][8];
+#pragma unroll
+  for (int nt = 0; nt < 8; ++nt)
+#pragma unroll
+    for (int mt = 0; mt < 8; ++mt) acc[nt][mt] = (f32x4){0.f, 0.f, 0.f, 0.f};
+
+  const int nk = K / QBK;
+#pragma unroll
+  for (int t = 0; t < QNS - 1; ++t)
+    if (t < nk)
+#pragma unroll
+      for (int p = 0; p < 8; ++p) piece(t, p);
+  for (int kt = 0; kt < nk; ++kt) {
+    const int ahead = min(nk - 1 - kt, QNS - 2);
+    if (ahead >= 2) pwait_vmcnt<16>(); else if (ahead == 1) pwait_vmcnt<8>(); else pwait_vmcnt<0>();
+    pbarrier();
+    const char* sb = plds + (kt % QNS) * QSTAGE;
+    bf16x8 af[8], bfr[8];
+#pragma unroll
+    for (int nt = 0; nt < 8; ++nt) af[nt] = *reinterpret_cast<const bf16x8*>(sb + aoff(nt));
+#pragma unroll
+    for (int mt = 0; mt < 8; ++mt)
+      bfr[mt] = *reinterpret_cast<const bf16x8*>(sb + bbase + 1024u * mt);
+    const bool more = kt + QNS - 1 < nk;
+    if (prio) __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int mt = 0; mt < 8; ++mt) {
+      if (more) {
+        __builtin_amdgcn_sched_barrier(0);
+        piece(kt + QNS - 1, mt);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+#pragma unroll
+      for (int nt = 0; nt < 8; ++nt)
+        acc[nt][mt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[nt], bfr[mt], acc[nt][mt], 0, 0, 0);
+    }
+    if (prio) __builtin_amdgcn_s_setprio(0);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  }
+
+#pragma unroll
+  for (int mt = 0; mt < 8; ++mt) {
+    const int tok = m0 + 128 * wr + 16 * mt + fr;
+    if (tok >= M) continue;
+    bf16_t* orow = out + (long)tok * ldo;
+    if constexpr (SWIGLU) {
+#pragma unroll
+      for (int nt = 0; nt < 4; ++nt) {
+        bf16x4 h;
+#pragma unroll
+        for (int v = 0; v < 4; ++v) h[v] = f2bf(psilu(acc[nt][mt][v]) * acc[nt + 4][mt][v]);
+        *reinterpret_cast<bf16x4*>(orow + n0 + 64 * wc + 16 * nt + 4 * fc) = h;
+      }
+    } else {
+#pragma unroll
+      for (int nt = 0; nt < 8; ++nt) {
+        bf16x4 o;
+#pragma unroll
+        for (int v = 0; v < 4; ++v) o[v] = f2bf(acc[nt][mt][v]);
+        *reinterpret_cast<bf16x4*>(orow + n0 + 128 * wc + 16 * nt + 4 * fc) = o;
+      }
+    }
+  }
+}
+
 template <bool SWIGLU>
 int launch_prefill(const bf16_t* X, long ldx, const bf16_t* W, long ldw, bf16_t* out, long ldo,
                    int M, int N, int K, hipStream_t st) {
   static const int variant = [] {    // EIA_PREFILL_GEMM_V: 1 = 2 x BK 64 stages, 2 = 4 x BK 32,
-                                     // 3 = 2 + fragment reads one step ahead
+                                     // 3 = 2 + fragment reads one step ahead,
+                                     // 4 = 2 with 4 waves of 128 x 128
     const char* e = getenv("EIA_PREFILL_GEMM_V");
     return e != nullptr ? atoi(e) : 2;
   }();
@@ -459,6 +577,8 @@ int launch_prefill(const bf16_t* X, long ldx, const bf16_t* W, long ldw, bf16_t*
                               hipFuncAttributeMaxDynamicSharedMemorySize, QNS * QSTAGE);
     (void)hipFuncSetAttribute(reinterpret_cast<const void*>(gemm_prefill_kernel_v3<SWIGLU>),
                               hipFuncAttributeMaxDynamicSharedMemorySize, QNS * QSTAGE);
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(gemm_prefill_kernel_v4<SWIGLU>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, QNS * QSTAGE);
     attr = true;
   }
   const int ntm = (M + PBM - 1) / PBM;
@@ -467,7 +587,10 @@ int launch_prefill(const bf16_t* X, long ldx, const bf16_t* W, long ldw, bf16_t*
     const char* e = getenv("EIA_PREFILL_GEMM_PRIO");
     return e != nullptr ? atoi(e) : 0;
   }();
-  if (variant == 3 && K % QBK == 0)
+  if (variant == 4 && K % QBK == 0)
+    hipLaunchKernelGGL(gemm_prefill_kernel_v4<SWIGLU>, dim3(ntm * ntn), dim3(VTHREADS),
+                       QNS * QSTAGE, st, X, ldx, W, ldw, out, ldo, M, K, N / 2, ntm, ntn, prio);
+  else if (variant == 3 && K % QBK == 0)
     hipLaunchKernelGGL(gemm_prefill_kernel_v3<SWIGLU>, dim3(ntm * ntn), dim3(PTHREADS),
                        QNS * QSTAGE, st, X, ldx, W, ldw, out, ldo, M, K, N / 2, ntm, ntn, prio);
   else if (variant == 2 && K % QBK == 0)
