@@ -481,8 +481,9 @@ def linear(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = None
 
 # --------------------------------------------------------------------------- prefill K7
 # Prompt-sized gate_up with the SwiGLU epilogue in the GEMM (csrc/kernels/gemm_prefill.hip):
-# the [T, 2I] intermediate never reaches HBM and act_and_mul disappears.  EIA_PREFILL_SWIGLU:
-# 1 on, 0 off (hipBLASLt + act_and_mul).
+# the [T, 2I] intermediate never reaches HBM and act_and_mul disappears.  Opt-in
+# (EIA_PREFILL_SWIGLU=1): at ~1.2 PFLOP/s it trails hipBLASLt's tuned 1.56 + the separate
+# act_and_mul pass in the engine's prefill step (docs/performance.md, "Prefill SwiGLU (K7)").
 PREFILL_SWIGLU = os.environ.get("EIA_PREFILL_SWIGLU", "0") == "1"
 PREFILL_MIN_M = int(os.environ.get("EIA_PREFILL_SWIGLU_MIN_M", "256"))
 
@@ -493,7 +494,7 @@ def prefill_gemm_ok(x: torch.Tensor, w: torch.Tensor, swiglu: bool) -> bool:
         return False
     M, K = x.shape
     N = w.shape[0]
-    if w.shape[1] != K or K % 64 or x.stride(1) != 1 or w.stride(1) != 1 or x.stride(0) % 8 or \
+    if w.shape[1] != K or K % 32 or x.stride(1) != 1 or w.stride(1) != 1 or x.stride(0) % 8 or \
             w.stride(0) % 8:
         return False
     return (N % 2 == 0 and (N // 2) % 128 == 0) if swiglu else N % 256 == 0

@@ -26,16 +26,12 @@ def test_tile_order_is_a_bijection(ntm, ntn):
     assert sorted(tiles) == [(m, n) for m in range(ntm) for n in range(ntn)]
 
 
-def pswz(row, c):        # 128-B rows (BK 64)
-    return row * 128 + 16 * (c ^ ((row >> 1) & 7))
-
-
 def qswz(row, c):        # 64-B rows (BK 32)
     return row * 64 + 16 * (c ^ ((row >> 1) & 3))
 
 
-@pytest.mark.parametrize("swz,row_bytes,ks_list", [(pswz, 128, (0, 1)), (qswz, 64, (0,))])
-def test_fragment_reads_conflict_free(swz, row_bytes, ks_list):
+@pytest.mark.parametrize("swz,ks_list", [(qswz, (0,))])
+def test_fragment_reads_conflict_free(swz, ks_list):
     """16x16x32 fragment read: lane l -> row base + (l & 15), chunk 4 ks + (l >> 4); every
     ds_read_b128 lane group must touch 16 distinct 16-B bank slots (256-B bank row)."""
     for base in (0, 16, 32, 128, 240):
@@ -45,36 +41,24 @@ def test_fragment_reads_conflict_free(swz, row_bytes, ks_list):
                 assert len(slots) == 16, (base, ks)
 
 
-@pytest.mark.parametrize("variant", [1, 2])
-def test_dma_sources_fill_the_swizzled_image(variant):
+def test_dma_sources_fill_the_swizzled_image():
     """Every DMA instruction writes 1 KiB lane-linearly; lane l's SOURCE is the logical chunk
     that the swizzled image expects at that LDS position.  Over all waves / instructions each
-    (row, chunk) of the 256-row operand tile is loaded exactly once, into swz(row, chunk)."""
+    (row, chunk) of the 256-row operand tile is loaded exactly once, into qswz(row, chunk)."""
     seen = {}
-    if variant == 1:     # 128-B rows: instruction i = 4 wave + j covers rows 8 i + (lane >> 3)
-        for wave in range(8):
-            for j in range(4):
-                i = 4 * wave + j
-                for lane in range(64):
-                    row = 8 * i + (lane >> 3)
-                    c = (lane & 7) ^ ((row >> 1) & 7)
-                    seen[(row, c)] = i * 1024 + 16 * lane
-        assert len(seen) == 256 * 8
-        assert all(pos == pswz(r, c) for (r, c), pos in seen.items())
-    else:                # 64-B rows: instruction i = 2 wave + j covers rows 16 i + (lane >> 2)
-        for wave in range(8):
-            for j in range(2):
-                i = 2 * wave + j
-                for lane in range(64):
-                    row = 16 * i + (lane >> 2)
-                    c = (lane & 3) ^ ((row >> 1) & 3)
-                    seen[(row, c)] = i * 1024 + 16 * lane
-        assert len(seen) == 256 * 4
-        assert all(pos == qswz(r, c) for (r, c), pos in seen.items())
+    for wave in range(8):          # instruction i = 2 wave + j covers rows 16 i + (lane >> 2)
+        for j in range(2):
+            i = 2 * wave + j
+            for lane in range(64):
+                row = 16 * i + (lane >> 2)
+                c = (lane & 3) ^ ((row >> 1) & 3)
+                seen[(row, c)] = i * 1024 + 16 * lane
+    assert len(seen) == 256 * 4
+    assert all(pos == qswz(r, c) for (r, c), pos in seen.items())
 
 
 def test_fragment_offsets_are_base_plus_constants():
-    """v3 reads tile nt / mt at one lane base plus 1024-B multiples (the swizzle term repeats
+    """Fragment tile nt / mt sits at one lane base plus 1024-B multiples (the swizzle term repeats
     every 8 rows, tiles are 16 rows apart): check against the direct formula."""
     for wc in range(4):
         for lane in range(64):
