@@ -29,8 +29,11 @@
 // 1.23 + 0.08 ms for hipBLASLt + act_and_mul, so it is opt-in (EIA_PREFILL_SWIGLU=1).  Tried and
 // slower: 2 stages of BK 64 with two barriers per step (1.10), fragment reads one step ahead
 // (1.12), four 128 x 128 waves with AGPR accumulators (1.10), the two combined (spills, 0.5),
-// s_setprio around the MFMA bursts (+0.6 %).
+// s_setprio around the MFMA bursts (+0.6 %), register staging (global_load + ds_write into
+// three stages, one barrier per step: 1.03); the half-step stagger of the two wave halves
+// (STAG, default) adds ~2 % on the SwiGLU shape.
 #include <cstdint>
+#include <cstdlib>
 
 #include "eia_common.h"
 
@@ -67,7 +70,11 @@ constexpr int QNS = 4;
 
 EIA_DEV unsigned qswz(int row, int c) { return (unsigned)(row * 64 + 16 * (c ^ ((row >> 1) & 3))); }
 
-template <bool SWIGLU>
+// STAG: the two wave halves (token rows 0-127 / 128-255; one wave of each per SIMD) run half a
+// K-step apart, with a barrier in the middle of every step: the half that just passed its
+// data barrier reads its fragments while the other half is in its second block of MFMAs, so
+// the LDS read latency after a barrier no longer stalls both waves of a SIMD together.
+template <bool SWIGLU, bool STAG>
 __global__ void __launch_bounds__(PTHREADS, 1)
 gemm_prefill_kernel(const bf16_t* __restrict__ X, long ldx, const bf16_t* __restrict__ W,
                     long ldw, bf16_t* __restrict__ out, long ldo, int M, int K, int inter, int ntm,
@@ -131,6 +138,66 @@ gemm_prefill_kernel(const bf16_t* __restrict__ X, long ldx, const bf16_t* __rest
     if (t < nk)
 #pragma unroll
       for (int p = 0; p < 4; ++p) piece(t, p);
+  auto wait_ahead = [&](int ahead) {        // this wave's newer tiles allowed in flight
+    if (ahead >= 2) pwait_vmcnt<8>(); else if (ahead == 1) pwait_vmcnt<4>(); else pwait_vmcnt<0>();
+  };
+  auto mma_half = [&](int h, const bf16x8 (&af)[4], const bf16x8 (&bfr)[8], int dma_kt) {
+#pragma unroll
+    for (int mi = 0; mi < 4; ++mi) {
+      const int mt = 4 * h + mi;
+      if (dma_kt >= 0) {
+        __builtin_amdgcn_sched_barrier(0);
+        piece(dma_kt, mi);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+#pragma unroll
+      for (int nt = 0; nt < 4; ++nt)
+        acc[nt][mt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[nt], bfr[mt], acc[nt][mt], 0, 0, 0);
+    }
+  };
+  auto read_frags = [&](int kt, bf16x8 (&af)[4], bf16x8 (&bfr)[8]) {
+    const char* sb = plds + (kt % QNS) * QSTAGE;
+#pragma unroll
+    for (int nt = 0; nt < 4; ++nt) af[nt] = *reinterpret_cast<const bf16x8*>(sb + aoff[nt]);
+#pragma unroll
+    for (int mt = 0; mt < 8; ++mt) bfr[mt] = *reinterpret_cast<const bf16x8*>(sb + boff[mt]);
+  };
+  if constexpr (STAG) {
+    // barriers X(k) (tile k readable by the first half; tile k-1's stage free for tile k+3)
+    // and Y(k) (tile k readable by the second half), in the order X0 Y0 X1 Y1 ... for all
+    if (wr == 0) {
+      for (int kt = 0; kt < nk; ++kt) {
+        wait_ahead(min(nk - 1 - kt, QNS - 2));
+        pbarrier();                                            // X(kt)
+        bf16x8 af[4], bfr[8];
+        read_frags(kt, af, bfr);
+        mma_half(0, af, bfr, kt + QNS - 1 < nk ? kt + QNS - 1 : -1);
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        pbarrier();                                            // Y(kt)
+        mma_half(1, af, bfr, -1);
+      }
+    } else {
+      wait_ahead(min(nk - 1, QNS - 2));
+      pbarrier();                                              // X(0)
+      if (QNS - 1 < nk)
+#pragma unroll
+        for (int p = 0; p < 4; ++p) piece(QNS - 1, p);
+      for (int kt = 0; kt < nk; ++kt) {
+        pbarrier();                                            // Y(kt)
+        bf16x8 af[4], bfr[8];
+        read_frags(kt, af, bfr);
+        mma_half(0, af, bfr, -1);
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        int dma_kt = -1;
+        if (kt + 1 < nk) {
+          wait_ahead(min(nk - 2 - kt, QNS - 2));              // tile kt+1 landed
+          pbarrier();                                          // X(kt+1)
+          dma_kt = kt + QNS < nk ? kt + QNS : -1;
+        }
+        mma_half(1, af, bfr, dma_kt);
+      }
+    }
+  } else
   for (int kt = 0; kt < nk; ++kt) {
     const int ahead = min(nk - 1 - kt, QNS - 2);    // newer tiles still in flight
     if (ahead >= 2) pwait_vmcnt<8>(); else if (ahead == 1) pwait_vmcnt<4>(); else pwait_vmcnt<0>();
@@ -184,16 +251,23 @@ gemm_prefill_kernel(const bf16_t* __restrict__ X, long ldx, const bf16_t* __rest
 template <bool SWIGLU>
 int launch_prefill(const bf16_t* X, long ldx, const bf16_t* W, long ldw, bf16_t* out, long ldo,
                    int M, int N, int K, hipStream_t st) {
+  static const bool stag = [] {       // EIA_PREFILL_GEMM_STAG=0: both wave halves in lockstep
+    const char* e = getenv("EIA_PREFILL_GEMM_STAG");
+    return e == nullptr || atoi(e) != 0;
+  }();
   static bool attr = false;     // > 64 KiB of dynamic LDS must be opted into
   if (!attr) {
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(gemm_prefill_kernel<SWIGLU>),
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(gemm_prefill_kernel<SWIGLU, true>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, QNS * QSTAGE);
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(gemm_prefill_kernel<SWIGLU, false>),
                               hipFuncAttributeMaxDynamicSharedMemorySize, QNS * QSTAGE);
     attr = true;
   }
   const int ntm = (M + PBM - 1) / PBM;
   const int ntn = SWIGLU ? (N / 2) / (PBN / 2) : N / PBN;
-  hipLaunchKernelGGL(gemm_prefill_kernel<SWIGLU>, dim3(ntm * ntn), dim3(PTHREADS), QNS * QSTAGE,
-                     st, X, ldx, W, ldw, out, ldo, M, K, N / 2, ntm, ntn);
+  auto kern = stag ? gemm_prefill_kernel<SWIGLU, true> : gemm_prefill_kernel<SWIGLU, false>;
+  hipLaunchKernelGGL(kern, dim3(ntm * ntn), dim3(PTHREADS), QNS * QSTAGE, st, X, ldx, W, ldw,
+                     out, ldo, M, K, N / 2, ntm, ntn);
   return (int)hipGetLastError();
 }
 
