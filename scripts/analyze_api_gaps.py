@@ -47,6 +47,12 @@ def main():
     gaps = [(ks[i][0] - ks[i - 1][1], ks[i - 1][1], ks[i][0], ks[i - 1][2], ks[i][2])
             for i in range(1, len(ks)) if ks[i][0] - ks[i - 1][1] > a.min_gap_us * 1e3]
     print(f"{len(gaps)} gaps > {a.min_gap_us} us; showing the last {a.n}")
+    # how long the host spends inside each graph launch (a launch that blocks until the GPU
+    # has nearly drained serialises the host behind every step)
+    gl = sorted((t1 - t0) / 1e3 for t0, t1, f in api if f.startswith("hipGraphLaunch"))
+    if gl:
+        print(f"hipGraphLaunch: {len(gl)} calls, host us min {gl[0]:.1f} p50 {gl[len(gl) // 2]:.1f} "
+              f"p90 {gl[int(0.9 * (len(gl) - 1))]:.1f} max {gl[-1]:.1f}")
     for g, s, e, kb, ka in gaps[-a.n:]:
         print(f"\n=== gap {g / 1e3:.1f} us: {short(kb)} -> {short(ka)}")
         for t0, t1, f in api:

@@ -43,9 +43,13 @@ def main() -> int:
                        for r in rows[ab[0] + 1:ab[1] + 1])
         pairs = sorted(zip(ends[:-1], ends[1:]), key=ktime)[-nsteps:]
     agg = collections.defaultdict(list)
+    gaps = collections.defaultdict(list)     # idle before a kernel, keyed by (previous, kernel)
     spans, busy, launches = [], [], []
     for a, b in pairs:
         ks = rows[a + 1:b + 1]
+        for prev, cur in zip(ks[:-1], ks[1:]):
+            g = (int(cur["Start_Timestamp"]) - int(prev["End_Timestamp"])) / 1e3
+            gaps[(short(prev["Kernel_Name"])[:40], short(cur["Kernel_Name"])[:40])].append(g)
         t0 = int(ks[0]["Start_Timestamp"])
         t1 = int(ks[-1]["End_Timestamp"])
         spans.append((t1 - t0) / 1e3)
@@ -64,6 +68,27 @@ def main() -> int:
     for name, v in sorted(agg.items(), key=lambda kv: -sum(kv[1])):
         per = sum(v) / n
         print(f"| {name} | {len(v) / n:.1f} | {per:.1f} | {100 * per / kern:.1f} | {sum(v) / len(v):.2f} |")
+    # one step's copies and their neighbours, relative times (us)
+    a, b = pairs[len(pairs) // 2]
+    seq = rows[a - 2:b + 3]
+    base = int(seq[0]["Start_Timestamp"])
+    print("\nA middle step around the staging copies (us from the first row):\n")
+    print("| # | kernel | start | end | gap before |")
+    print("|---:|---|---:|---:|---:|")
+    prev_end = None
+    for i, r in enumerate(seq):
+        st, en = int(r["Start_Timestamp"]), int(r["End_Timestamp"])
+        nm = short(r["Kernel_Name"])
+        near = any("copyBuffer" in short(x["Kernel_Name"]) for x in seq[max(0, i - 2):i + 3])
+        if near or i < 3 or i > len(seq) - 4:
+            gap = "" if prev_end is None else f"{(st - prev_end) / 1e3:.2f}"
+            print(f"| {i} | {nm[:48]} | {(st - base) / 1e3:.2f} | {(en - base) / 1e3:.2f} | {gap} |")
+        prev_end = en
+    print("\nIdle between consecutive kernels (by pair; us per step = count x mean gap):\n")
+    print("| previous -> next | per step | mean gap us | us/step |")
+    print("|---|---:|---:|---:|")
+    for (pa, pb), v in sorted(gaps.items(), key=lambda kv: -sum(kv[1]))[:14]:
+        print(f"| {pa} -> {pb} | {len(v) / n:.1f} | {sum(v) / len(v):.2f} | {sum(v) / n:.1f} |")
     return 0
 
 
