@@ -209,12 +209,13 @@ def attach_wg_packed(model: torch.nn.Module, budget_bytes: int, max_m: int = MAX
     """Give every decode GEMM weight whose shape has workgroup-packed table picks a packed copy
     (``w._eia_wg[(waves, swiglu)]``) -- the decode kernels then read each workgroup's rows as
     one sequential stream; prefill keeps the row-major weight for hipBLASLt.  Weight families
-    are packed whole or not at all, in priority order -- dense linears, then MoE expert
-    gate_up, then MoE expert down (``EIA_MOE_WG_PACK``: 1 both, ``up`` gate_up only, 0 none)
-    -- while the copies fit ``budget_bytes`` (a 70B on one GPU stays row-major; Mixtral at the
-    default budget packs its dense layers and expert gate_up).  Returns the bytes added."""
+    are packed whole or not at all: the dense linears one (N, K, form) family at a time,
+    smallest first, then MoE expert gate_up, then MoE expert down (``EIA_MOE_WG_PACK``: 1 both,
+    ``up`` gate_up only, 0 none); a family that does not fit the rest of ``budget_bytes`` is
+    skipped and the next one tried (a 70B on one GPU packs lm_head / o / qkv / down and keeps
+    its 75 GB gate_up row-major only).  Returns the bytes added."""
     from ..models import layers as L
-    plan = []                    # (priority, weight, key)
+    plan = []                    # (family, weight, key)
     for mod in model.modules():
         w = getattr(mod, "weight", None)
         if not isinstance(w, torch.Tensor) or w.dim() != 2 or w.dtype != torch.bfloat16 or \
@@ -229,7 +230,7 @@ def attach_wg_packed(model: torch.nn.Module, budget_bytes: int, max_m: int = MAX
             forms.append(True)
         for sw in forms:
             for waves in wg_layouts(N, K, sw, max_m):
-                plan.append((0, w, (waves, sw)))
+                plan.append(((0, N, K, sw), w, (waves, sw)))
     moe_mode = os.environ.get("EIA_MOE_WG_PACK", "1")
     if moe_mode != "0":
         # MoE expert gate_up [E, 2I, H] (the grouped skinny kernel's decode form, cfg 1 / 3)
@@ -241,27 +242,21 @@ def attach_wg_packed(model: torch.nn.Module, budget_bytes: int, max_m: int = MAX
                 E, I2, H = w13.shape
                 up, down = moe_cfgs(I2 // 2, H)
                 if up in (1, 3) and H % 128 == 0:
-                    plan.append((1, w13, (2 if up == 1 else 4, True)))
+                    plan.append(((1,), w13, (2 if up == 1 else 4, True)))
                 # expert down [E, H, I]: one 16-row tile per wave (grouped cfg 0 / 2), keyed
                 # (waves, False, 1)
                 w2 = getattr(mod, "w2", None)
                 if (moe_mode != "up" and isinstance(w2, torch.Tensor) and w2.dim() == 3
                         and w2.is_contiguous() and w2.dtype == torch.bfloat16
                         and down in (0, 2) and w2.shape[2] % 128 == 0):
-                    plan.append((2, w2, (2 if down == 0 else 4, False, 1)))
+                    plan.append(((2,), w2, (2 if down == 0 else 4, False, 1)))
     seen = set()
     size = {}
     for pri, w, key in plan:
         if (id(w), key) not in seen:
             seen.add((id(w), key))
             size[pri] = size.get(pri, 0) + w.numel() * w.element_size()
-    total = 0
-    take = set()
-    for pri in sorted(size):
-        if total + size[pri] > budget_bytes:
-            break
-        total += size[pri]
-        take.add(pri)
+    take, total = select_wg_families(size, budget_bytes)
     if total == 0:
         return 0
     for pri, w, key in plan:
@@ -281,6 +276,18 @@ def attach_wg_packed(model: torch.nn.Module, budget_bytes: int, max_m: int = MAX
         load_and_refresh._eia_wg_refresh = True
         model.load_weights = load_and_refresh
     return total
+
+
+def select_wg_families(size: dict, budget_bytes: int):
+    """Families (tuples led by their priority: 0 dense, 1 MoE gate_up, 2 MoE down) to pack:
+    in priority order, smallest first within one, each taken whole when it still fits."""
+    total = 0
+    take = set()
+    for fam in sorted(size, key=lambda f: (f[0], size[f])):
+        if total + size[fam] <= budget_bytes:
+            total += size[fam]
+            take.add(fam)
+    return take, total
 
 
 def _pack_wg_any(w: torch.Tensor, key) -> torch.Tensor:

@@ -107,3 +107,26 @@ def test_refresh_wg_packed_experts_in_place():
     for e in range(3):
         assert torch.equal(up[e], gemm.pack_weight_wg(m.w13.data[e], 1024 + 19, True))
         assert torch.equal(dn[e], gemm.pack_weight_wg(m.w2.data[e], 1024 + 2, False))
+
+
+def test_wg_family_selection_70b_tp1():
+    """Llama-3.3-70B on one GPU with the runner's budget (half of the ~147 GB the weights leave
+    free): lm_head, o, qkv and down fit, the 75 GB gate_up is skipped, not the whole dense set."""
+    from enterprise_inference_amd.ops.gemm import select_wg_families
+    L = 80
+    fam = {(0, 128256, 8192, False): 128256 * 8192 * 2,
+           (0, 8192, 8192, False): L * 8192 * 8192 * 2,
+           (0, 10240, 8192, False): L * 10240 * 8192 * 2,
+           (0, 8192, 28672, False): L * 8192 * 28672 * 2,
+           (0, 57344, 8192, True): L * 57344 * 8192 * 2}
+    take, total = select_wg_families(fam, int(0.5 * 147e9))
+    assert (0, 57344, 8192, True) not in take and len(take) == 4
+    assert total == sum(v for k, v in fam.items() if k in take)
+    # Mixtral-8x7B: dense, then expert gate_up, then expert down, all within 0.35 x 288 GB
+    mix = {(0, 6144, 4096, False): 32 * 6144 * 4096 * 2, (1,): 60_129_542_144,
+           (2,): 30_064_771_072}
+    take, total = select_wg_families(mix, int(0.35 * 288e9))
+    assert take == set(mix)
+    # a budget that cannot hold the expert gate_up still packs the down projections
+    take, _ = select_wg_families(mix, 40e9)
+    assert take == {(0, 6144, 4096, False), (2,)}
