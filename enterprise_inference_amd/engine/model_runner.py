@@ -156,15 +156,16 @@ class ModelRunner:
         if self.is_gpu and os.environ.get("EIA_WG_PACK", "1") != "0":
             # decode copies of the GEMM weights in the workgroup-packed layout (ops/gemm.py
             # attach_wg_packed), before the KV cache is sized from the free memory; at most
-            # EIA_WG_PACK_BUDGET of the device (default 0.35) and at most half of what the
-            # weights left free (the KV cache keeps the rest): a 70B on one GPU packs all but
-            # its gate_up
+            # EIA_WG_PACK_BUDGET of the device (default 0.35), and leaving EIA_WG_PACK_KV_KEEP
+            # of the device (default 0.38) free for the KV cache and the runtime: a 70B on one
+            # GPU packs its attention linears and LM head only, so its 30 x 8k-token sizing row
+            # still fits the cache (profiles/sizing_70b_tp1_r5_wgpack.md)
             from ..ops import gemm as _g
             total = torch.cuda.get_device_properties(self.device).total_memory
             free = torch.cuda.mem_get_info(self.device)[0]
             frac = float(os.environ.get("EIA_WG_PACK_BUDGET", "0.35"))
-            keep = float(os.environ.get("EIA_WG_PACK_KV_KEEP", "0.5"))
-            budget = int(min(frac * total, (1.0 - keep) * free))
+            keep = float(os.environ.get("EIA_WG_PACK_KV_KEEP", "0.38"))
+            budget = max(0, int(min(frac * total, free - keep * total)))
             self.wg_packed_bytes = _g.attach_wg_packed(self.model, budget,
                                                        min(_g.MAX_M, cfg.scheduler.max_num_seqs))
             logger.info("workgroup-packed decode weights: %.1f GiB (budget %.1f GiB, %.1f GiB "

@@ -209,13 +209,14 @@ def attach_wg_packed(model: torch.nn.Module, budget_bytes: int, max_m: int = MAX
     """Give every decode GEMM weight whose shape has workgroup-packed table picks a packed copy
     (``w._eia_wg[(waves, swiglu)]``) -- the decode kernels then read each workgroup's rows as
     one sequential stream; prefill keeps the row-major weight for hipBLASLt.  Weight families
-    are packed whole or not at all: the dense linears one (N, K, form) family at a time,
-    smallest first, then MoE expert gate_up, then MoE expert down (``EIA_MOE_WG_PACK``: 1 both,
-    ``up`` gate_up only, 0 none); a family that does not fit the rest of ``budget_bytes`` is
-    skipped and the next one tried (a 70B on one GPU packs lm_head / o / qkv / down and keeps
-    its 75 GB gate_up row-major only).  Returns the bytes added."""
+    are packed whole or not at all: the dense linears one (N, K, form, layout) family at a
+    time, smallest first, then MoE expert gate_up, then MoE expert down (``EIA_MOE_WG_PACK``: 1
+    both, ``up`` gate_up only, 0 none); a family that does not fit the rest of ``budget_bytes``
+    is skipped and the next one tried (a 70B on one GPU packs its LM head, O and one QKV layout,
+    36 GiB, and keeps the MLP row-major only).  Returns the bytes added."""
     from ..models import layers as L
     plan = []                    # (family, weight, key)
+    uses = {}                    # dense family -> batch buckets whose packed pick it serves
     for mod in model.modules():
         w = getattr(mod, "weight", None)
         if not isinstance(w, torch.Tensor) or w.dim() != 2 or w.dtype != torch.bfloat16 or \
@@ -230,7 +231,11 @@ def attach_wg_packed(model: torch.nn.Module, budget_bytes: int, max_m: int = MAX
             forms.append(True)
         for sw in forms:
             for waves in wg_layouts(N, K, sw, max_m):
-                plan.append(((0, N, K, sw), w, (waves, sw)))
+                fam = (0, N, K, sw, waves)
+                plan.append((fam, w, (waves, sw)))
+                uses[fam] = sum(1 for (mt, n, k, s_), (c, _) in _TUNED_WG.items()
+                                if (n, k, s_) == (N, K, sw) and mt <= m_bucket(max_m)
+                                and c & 1024 and cfg_waves(c) == waves)
     moe_mode = os.environ.get("EIA_MOE_WG_PACK", "1")
     if moe_mode != "0":
         # MoE expert gate_up [E, 2I, H] (the grouped skinny kernel's decode form, cfg 1 / 3)
@@ -256,7 +261,7 @@ def attach_wg_packed(model: torch.nn.Module, budget_bytes: int, max_m: int = MAX
         if (id(w), key) not in seen:
             seen.add((id(w), key))
             size[pri] = size.get(pri, 0) + w.numel() * w.element_size()
-    take, total = select_wg_families(size, budget_bytes)
+    take, total = select_wg_families(size, budget_bytes, uses)
     if total == 0:
         return 0
     for pri, w, key in plan:
@@ -278,12 +283,14 @@ def attach_wg_packed(model: torch.nn.Module, budget_bytes: int, max_m: int = MAX
     return total
 
 
-def select_wg_families(size: dict, budget_bytes: int):
+def select_wg_families(size: dict, budget_bytes: int, uses: dict = None):
     """Families (tuples led by their priority: 0 dense, 1 MoE gate_up, 2 MoE down) to pack:
-    in priority order, smallest first within one, each taken whole when it still fits."""
+    in priority order, smallest first within one (equal sizes: the layout serving more batch
+    buckets first), each taken whole when it still fits."""
+    uses = uses or {}
     total = 0
     take = set()
-    for fam in sorted(size, key=lambda f: (f[0], size[f])):
+    for fam in sorted(size, key=lambda f: (f[0], size[f], -uses.get(f, 0))):
         if total + size[fam] <= budget_bytes:
             total += size[fam]
             take.add(fam)

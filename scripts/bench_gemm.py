@@ -25,6 +25,8 @@ from enterprise_inference_amd.ops import gemm  # noqa: E402
 SHAPES = {  # name: (N, K, swiglu)
     "qkv_8b": (6144, 4096, False), "o_8b": (4096, 4096, False),
     "gate_up_8b": (28672, 4096, True), "down_8b": (4096, 14336, False),
+    # grid-fill probes: the 8B gate_up at 196 / 256 workgroups of 128 rows (224 in the model)
+    "gate_up_8b_w196": (25088, 4096, True), "gate_up_8b_w256": (32768, 4096, True),
     "lm_head_8b": (128256, 4096, False),
     "qkv_70b_tp8": (1280, 8192, False), "o_70b_tp8": (8192, 1024, False),
     "gate_up_70b_tp8": (7168, 8192, True), "down_70b_tp8": (8192, 3584, False),

@@ -110,23 +110,28 @@ def test_refresh_wg_packed_experts_in_place():
 
 
 def test_wg_family_selection_70b_tp1():
-    """Llama-3.3-70B on one GPU with the runner's budget (half of the ~147 GB the weights leave
-    free): lm_head, o, qkv and down fit, the 75 GB gate_up is skipped, not the whole dense set."""
+    """Llama-3.3-70B on one GPU with the runner's budget (155.7 GiB free after the load, 38 % of
+    the 288 GiB device kept): the LM head, O and one QKV layout fit (36.4 GiB), the second QKV
+    layout and the 70 GiB MLP families are skipped -- not the whole dense set."""
     from enterprise_inference_amd.ops.gemm import select_wg_families
-    L = 80
-    fam = {(0, 128256, 8192, False): 128256 * 8192 * 2,
-           (0, 8192, 8192, False): L * 8192 * 8192 * 2,
-           (0, 10240, 8192, False): L * 10240 * 8192 * 2,
-           (0, 8192, 28672, False): L * 8192 * 28672 * 2,
-           (0, 57344, 8192, True): L * 57344 * 8192 * 2}
-    take, total = select_wg_families(fam, int(0.5 * 147e9))
-    assert (0, 57344, 8192, True) not in take and len(take) == 4
-    assert total == sum(v for k, v in fam.items() if k in take)
+    L, GiB = 80, 2 ** 30
+    fam = {}
+    for waves in (2, 4):
+        fam[(0, 128256, 8192, False, waves)] = 128256 * 8192 * 2
+        fam[(0, 8192, 8192, False, waves)] = L * 8192 * 8192 * 2
+        fam[(0, 10240, 8192, False, waves)] = L * 10240 * 8192 * 2
+        fam[(0, 8192, 28672, False, waves)] = L * 8192 * 28672 * 2
+    fam[(0, 57344, 8192, True, 4)] = L * 57344 * 8192 * 2
+    uses = {(0, 10240, 8192, False, 2): 2, (0, 10240, 8192, False, 4): 3}
+    take, total = select_wg_families(fam, int(155.7 * GiB - 0.38 * 288 * GiB), uses)
+    assert {f[1:3] for f in take} == {(128256, 8192), (8192, 8192), (10240, 8192)}
+    assert len(take) == 5 and abs(total / GiB - 36.4) < 0.1
+    assert (0, 10240, 8192, False, 4) in take      # the QKV layout of buckets 3-5
     # Mixtral-8x7B: dense, then expert gate_up, then expert down, all within 0.35 x 288 GB
-    mix = {(0, 6144, 4096, False): 32 * 6144 * 4096 * 2, (1,): 60_129_542_144,
+    mix = {(0, 6144, 4096, False, 4): 32 * 6144 * 4096 * 2, (1,): 60_129_542_144,
            (2,): 30_064_771_072}
     take, total = select_wg_families(mix, int(0.35 * 288e9))
     assert take == set(mix)
     # a budget that cannot hold the expert gate_up still packs the down projections
     take, _ = select_wg_families(mix, 40e9)
-    assert take == {(0, 6144, 4096, False), (2,)}
+    assert take == {(0, 6144, 4096, False, 4), (2,)}
