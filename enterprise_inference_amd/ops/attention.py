@@ -119,11 +119,13 @@ def decode_partitions(batch: int, num_kv_heads: int, num_heads: int, max_len: in
     if wgs >= 4 * cus:
         return 1
     if wgs >= cus:
-        # one to two items per CU: 2 partitions fill the chip evenly only when the items do
-        # (wgs a multiple of the CU count); otherwise 4 spread the remainder thinner:
-        # B 35 (280 items) ctx 4096 120.4 us at P 4 vs 126.5 at P 2, ctx 2048 67.7 vs 69.5
-        # (profiles/attn_long_r4.log); B 32 (256 items) keeps P 2 (97 vs 102 us)
-        p = 4 if (wgs < 2 * cus and wgs % cus and max_len >= 2048) else 2
+        # one to three items per CU: 2 partitions fill the chip evenly only when the items do
+        # (wgs a multiple of the CU count); otherwise 4 spread the remainder thinner once the
+        # context is long enough to pay for the merge: B 35 (280 items) ctx 4096 120.4 us at
+        # P 4 vs 126.5 at P 2, ctx 2048 67.7 vs 69.5 (profiles/attn_long_r4.log); B 65 (520
+        # items) ctx 4096 206.5 vs 215.7, ctx 8192 389.7 vs 418.1, ctx 2048 a tie
+        # (profiles/attn_long_p_r5.log); B 32 (256 items) and B 96 (768) keep P 2
+        p = 4 if (wgs < 3 * cus and wgs % cus and max_len >= 2048 * (wgs // cus)) else 2
     else:
         p = 2
         while p < max_parts and wgs * p * 2 <= cus:

@@ -80,7 +80,10 @@ def test_decode_partition_heuristic():
     assert decode_partitions(35, 8, 32, 2048) == 4
     assert decode_partitions(35, 8, 32, 1024) == 2
     assert decode_partitions(32, 8, 32, 4096) == 2
-    assert decode_partitions(65, 8, 32, 4096) == 2
+    assert decode_partitions(65, 8, 32, 4096) == 4
+    assert decode_partitions(65, 8, 32, 8192) == 4
+    assert decode_partitions(65, 8, 32, 2048) == 2
+    assert decode_partitions(96, 8, 32, 4096) == 2
     assert decode_partitions(128, 8, 32, 4096) == 1          # >= 4 items per CU
     assert decode_partitions(16, 8, 32, 4096) == 2
     assert decode_partitions(1, 8, 32, 4096) == 8
