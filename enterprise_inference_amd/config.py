@@ -218,8 +218,11 @@ class SchedulerConfig:
     max_num_prefill_seqs: int = 64
     max_model_len: int = 8192
     enable_chunked_prefill: bool = True
-    # Decode batch-size bucket step for HIP-graph capture (VLLM_DECODE_BS_BUCKET_STEP).
-    decode_bs_bucket_step: int = 16
+    # Decode batch-size bucket step for HIP-graph capture (VLLM_DECODE_BS_BUCKET_STEP).  8, not
+    # the reference's Gaudi 32: a HIP graph captures in ~20 ms, and every padded row costs the
+    # decode GEMMs X-staging bytes (65 users in the 72 bucket instead of 80: endpoint +1.3 %,
+    # profiles/bucket_step_ab_r5.log)
+    decode_bs_bucket_step: int = 8
     # overlapped scheduling: plan step k+1 while step k runs (VLLM_DELAYED_SAMPLING)
     delayed_sampling: bool = True
 

@@ -157,7 +157,7 @@ def engine_config_from_args(args: argparse.Namespace):
         max_num_seqs=args.max_num_seqs, max_num_batched_tokens=max(mbt, args.max_num_seqs),
         max_num_prefill_seqs=args.max_num_prefill_seqs or 64, max_model_len=max_len,
         enable_chunked_prefill=bool(args.enable_chunked_prefill),
-        decode_bs_bucket_step=int(os.environ.get("VLLM_DECODE_BS_BUCKET_STEP", 16)),
+        decode_bs_bucket_step=int(os.environ.get("VLLM_DECODE_BS_BUCKET_STEP", 8)),
         delayed_sampling=_truthy(os.environ.get("VLLM_DELAYED_SAMPLING", "true")))
     kvd = (args.kv_cache_dtype or "auto").lower()
     if kvd not in ("auto", "bfloat16", "bf16", "float16", "fp16", "half", "float32"):
