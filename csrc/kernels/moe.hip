@@ -234,10 +234,13 @@ splitk_norm_route_kernel(const float* __restrict__ part, int sk_rt, int M, int H
                          bf16_t* __restrict__ residual, const bf16_t* __restrict__ w, float eps,
                          bf16_t* __restrict__ out, long ldo, const bf16_t* __restrict__ wr,
                          int E, int k, int renorm, int scoring, float* __restrict__ w_out,
-                         int* __restrict__ id_out) {
+                         int* __restrict__ id_out, const int* __restrict__ row_len) {
   __shared__ float scratch[16];
   __shared__ float red[16][EM];
   const int row = blockIdx.x;
+  // decode-graph padding rows (context length 0) route to no expert (id E, weight 0): the
+  // expert GEMMs then see only live rows
+  const bool dead = row_len != nullptr && row_len[row] == 0;
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const long total = (long)M * H;
   const int sk = SK > 0 ? SK : sk_rt;
@@ -316,6 +319,13 @@ splitk_norm_route_kernel(const float* __restrict__ part, int sk_rt, int M, int H
   if ((lane & (64 / EM - 1)) == 0 && lane / (64 / EM) < E) red[wid][lane / (64 / EM)] = lg[0];
   __syncthreads();
   if (wid != 0) return;
+  if (dead) {
+    if (lane < k) {
+      w_out[(long)row * k + lane] = 0.f;
+      id_out[(long)row * k + lane] = E;
+    }
+    return;
+  }
   float x = -INFINITY;
   if (lane < E) {
     float s = 0.f;
@@ -401,7 +411,8 @@ moe_combine_norm_kernel(const float* __restrict__ part, long slab, const float* 
 EIA_API int eia_moe_splitk_norm_route(const float* part, int sk, int M, int H, void* residual,
                                       const void* w, float eps, void* out, long ldo,
                                       const void* wr, int E, int k, int renorm, int scoring,
-                                      float* w_out, int* id_out, hipStream_t st) {
+                                      float* w_out, int* id_out, const int* row_len,
+                                      hipStream_t st) {
   if (H % 4 != 0 || H > 4 * 1024 * 2 || ldo % 4 || sk < 1 || E < 1 || E > 16 || k < 1 || k > E)
     return EIA_BAD_SHAPE;
   if (M == 0) return EIA_OK;
@@ -412,7 +423,7 @@ EIA_API int eia_moe_splitk_norm_route(const float* part, int sk, int M, int H, v
   const bf16_t* r = static_cast<const bf16_t*>(wr);
 #define EIA_SNR(V, K, EM)                                                                        \
   hipLaunchKernelGGL((splitk_norm_route_kernel<V, K, EM>), dim3(M), dim3(1024), 0, st, part, sk, \
-                     M, H, res, ww, eps, o, ldo, r, E, k, renorm, scoring, w_out, id_out)
+                     M, H, res, ww, eps, o, ldo, r, E, k, renorm, scoring, w_out, id_out, row_len)
 #define EIA_SNR_K(V, EM)                    \
   switch (sk) {                             \
     case 1: EIA_SNR(V, 1, EM); break;       \

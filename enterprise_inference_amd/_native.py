@@ -69,7 +69,7 @@ _SIGNATURES = {
     "eia_mlp_fused_error": [IP, I, P],
     "eia_splitk_add_rmsnorm": [P, I, I, I, P, P, F, P, L, S],
     "eia_ar_alloc": [P, L],
-    "eia_moe_splitk_norm_route": [P, I, I, I, P, P, F, P, L, P, I, I, I, I, P, P, S],
+    "eia_moe_splitk_norm_route": [P, I, I, I, P, P, F, P, L, P, I, I, I, I, P, P, P, S],
     "eia_moe_combine_norm": [P, I, I, P, P, I, I, I, P, P, F, P, L, S],
     "eia_ar_free": [P],
     "eia_ar_signal_bytes": [],

@@ -114,7 +114,7 @@ class LlamaDecoderLayer(nn.Module):
         h = self.self_attn(h, md, kv)
         fuse = getattr(self.mlp, "norm_and_route", None)
         if fuse is not None:            # MoE: router + top-k inside the add + RMSNorm launch
-            r = fuse(h, residual, self.post_attention_layernorm)
+            r = fuse(h, residual, self.post_attention_layernorm, md)
             if r is not None:
                 h, residual, routing = r
                 return self.mlp(h, routing=routing), residual

@@ -146,15 +146,21 @@ class MixtralMoE(nn.Module):
             self.shared_expert.down_proj.reduce_results = False   # one all-reduce for the sum
             self.shared_expert_gate = ReplicatedLinear(H, 1, dtype=dtype, device=device)
 
-    def norm_and_route(self, h, residual, norm):
+    def norm_and_route(self, h, residual, norm, md=None):
         """Decode: the O projection's split-K add + RMSNorm (``norm``) with this block's router
-        and top-k in the same launch -> (x, residual, routing), or None when not applicable."""
+        and top-k in the same launch -> (x, residual, routing), or None when not applicable.
+        A pure-decode batch on one rank (``md``) routes its bucket-padding rows (context 0) to
+        no expert."""
         ex = self.experts
         if (self.gate.bias is not None or ex.scale_input or
                 not moe_ops.splitk_norm_route_ok(h, residual, self.gate.weight, ex.k)):
             return None
+        row_len = None
+        if (md is not None and md.num_prefill_tokens == 0 and md.decode_seq_lens is not None
+                and md.num_decode == h.M and state.tp_size() == 1 and not ex.ep):
+            row_len = md.decode_seq_lens
         return moe_ops.splitk_norm_route(h, residual, norm.weight, norm.eps, self.gate.weight,
-                                         ex.k, ex.renormalize, ex.scoring)
+                                         ex.k, ex.renormalize, ex.scoring, row_len=row_len)
 
     def forward(self, x, routing=None):
         # one rank, no shared expert: the combine may be left to the next add + RMSNorm

@@ -145,9 +145,13 @@ def splitk_norm_route_ok(s, residual, router_w: torch.Tensor, k: int) -> bool:
 
 def splitk_norm_route(s, residual: torch.Tensor, weight: torch.Tensor, eps: float,
                       router_w: torch.Tensor, k: int, renormalize: bool = True,
-                      scoring: str = "softmax"):
+                      scoring: str = "softmax", row_len: Optional[torch.Tensor] = None):
     """residual += reduce(s); x = rmsnorm(residual) * weight; route(x) -- one launch.
+    ``row_len`` (int32 [T], nullable): rows whose entry is 0 -- a decode graph's batch-bucket
+    padding -- route to no expert (id = E, weight 0).
     Returns (x, residual, (topk weights fp32 [T, k], expert ids int32 [T, k]))."""
+    if row_len is not None:
+        assert row_len.dtype == torch.int32 and row_len.is_cuda and row_len.numel() >= s.M
     out = torch.empty(s.M, s.N, dtype=torch.bfloat16, device=residual.device)
     w = torch.empty(s.M, k, dtype=torch.float32, device=residual.device)
     ids = torch.empty(s.M, k, dtype=torch.int32, device=residual.device)
@@ -155,7 +159,8 @@ def splitk_norm_route(s, residual: torch.Tensor, weight: torch.Tensor, eps: floa
                                           ptr(weight), float(eps), ptr(out), out.stride(0),
                                           ptr(router_w), router_w.shape[0], k,
                                           1 if renormalize else 0, SCORING[scoring], ptr(w),
-                                          ptr(ids), stream(out)), "moe_splitk_norm_route")
+                                          ptr(ids), ptr(row_len), stream(out)),
+          "moe_splitk_norm_route")
     return out, residual, (w, ids)
 
 

@@ -283,6 +283,16 @@ def test_splitk_norm_route_matches_unfused(M, H, E, k, sk):
     hr = (part.sum(0) + res0.float()).to(BF).float()
     ref_x = hr * torch.rsqrt(hr.pow(2).mean(-1, keepdim=True) + 1e-5) * nw.float()
     assert (x2.float() - ref_x).abs().max() < 3e-2 * ref_x.abs().max()
+    # decode-graph padding rows (context length 0) route to no expert; live rows unchanged
+    row_len = torch.randint(1, 300, (M,), device=DEV, dtype=torch.int32)
+    row_len[M // 2:] = 0 if M > 1 else row_len[M // 2:]
+    r3 = res0.clone()
+    x3, _, (w3, i3) = moe.splitk_norm_route(s, r3, nw, 1e-5, rw, k, True, row_len=row_len)
+    torch.cuda.synchronize()
+    dead = row_len == 0
+    assert torch.equal(r3, r1) and torch.equal(x3, x1)
+    assert torch.equal(i3[~dead], i2[~dead]) and torch.equal(w3[~dead], w2[~dead])
+    assert bool((i3[dead] == E).all()) and bool((w3[dead] == 0).all())
 
 
 @pytest.mark.parametrize("T,E,k,H,I", [(1, 8, 2, 4096, 1024), (65, 8, 2, 4096, 2048),
