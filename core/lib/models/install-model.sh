@@ -30,10 +30,9 @@ model_extra_vars() {
          "apisix_enabled=${apisix_enabled} ingress_enabled=${ingress_enabled}" \
          "deploy_keycloak=${deploy_keycloak} deploy_genai_gateway=${deploy_genai_gateway}" \
          "vllm_metrics_enabled=${metrics} deploy_ceph=${deploy_ceph}" \
-         "huggingface_model_id=${huggingface_model_id}" \
+         "huggingface_model_id=${huggingface_model_id} runtime_image=${runtime_image:-}" \
          "huggingface_model_deployment_name=${huggingface_model_deployment_name}" \
-         "huggingface_tensor_parellel_size=${huggingface_tensor_parellel_size}" \
-         "enable_cpu_balloons=$([ "$cpu_or_gpu" = "c" ] && echo true || echo false)"
+         "huggingface_tensor_parellel_size=${huggingface_tensor_parellel_size}"
 }
 
 deploy_inference_llm_models_playbook() {

@@ -12,13 +12,16 @@ update_driver() {
   if [ -n "$drv" ] && [ "$cur" = "$drv" ]; then log "driver $cur already installed"; return 0; fi
   log "installing amdgpu-dkms (ROCm ${rocm}) over '${cur:-none}'"
   . /etc/os-release
+  # pinned to the metadata driver version when one is given (apt / dnf version globs)
   case "$ID" in
-    ubuntu) apt-get update -y && apt-get install -y "amdgpu-dkms" ;;
-    rhel|rocky|almalinux) dnf install -y amdgpu-dkms ;;
+    ubuntu) apt-get update -y && apt-get install -y --allow-downgrades "amdgpu-dkms${drv:+=1:${drv}*}" ;;
+    rhel|rocky|almalinux) dnf install -y "amdgpu-dkms${drv:+-${drv}*}" ;;
     *) log "unsupported OS $ID"; return 1 ;;
   esac
   log "reloading the amdgpu module (GPU workloads on this node must be drained)"
-  modprobe -r amdgpu && modprobe amdgpu
+  if ! (modprobe -r amdgpu && modprobe amdgpu); then
+    log "module in use: reboot required"
+  fi
 }
 update_firmware() {
   log "current firmware:"; amd-smi firmware 2>/dev/null | head -40 || true

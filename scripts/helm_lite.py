@@ -5,7 +5,8 @@ A small interpreter for the Go-template + Sprig subset the charts under core/hel
 ``if / else if / else / end``, ``with``, ``range``, ``define`` / ``include``, variables
 (``$x := ...``, ``$``), pipelines and parenthesised sub-expressions, and the functions
 and, or, not, eq, ne, default, quote, printf, print, include, nindent, indent, toYaml,
-fromYaml, splitList, last, trunc, trimSuffix, contains, int, index, sha256sum, list.
+fromYaml, splitList, last, trunc, trimSuffix, contains, int, index, sha256sum, list,
+deepCopy, set, add1.
 Anything else raises, so a template that outgrows the subset fails its test loudly instead
 of rendering wrong.  Values are merged like ``helm --values a --values b --set k=v``.
 
@@ -222,6 +223,7 @@ class Renderer:
             "contains": lambda sub, s: _str(sub) in _str(s), "int": lambda v: int(v or 0),
             "index": self._index, "sha256sum": lambda s: hashlib.sha256(_str(s).encode()).hexdigest(),
             "list": lambda *v: list(v), "include": self._include,
+            "deepCopy": copy.deepcopy, "set": _sprig_set, "add1": lambda v: int(v or 0) + 1,
         }
 
     # -- functions
@@ -454,6 +456,12 @@ def chart_values(chart_dir: str, files=(), sets: Optional[Dict[str, str]] = None
     for k, v in (sets or {}).items():
         _set(vals, k, v)
     return vals
+
+
+def _sprig_set(d: dict, key: str, value):
+    """Sprig `set`: assign in place and return the dict."""
+    d[key] = value
+    return d
 
 
 def render_chart(chart_dir: str, files=(), sets=None, release: str = "rel",
