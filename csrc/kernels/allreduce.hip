@@ -177,11 +177,15 @@ ar_twoshot_kernel(ArPeers P, const bf16_t* __restrict__ in, bf16_t* __restrict__
 //                       its own buffer -> barrier -> every rank reads each row's sum from its
 //                       owner, adds, normalises.  Every link carries 2S/W bytes.
 // 512 threads per block; each thread keeps VPT bf16x8 vectors of a row in registers.
+// Split-K input (part != nullptr): the row-parallel skinny GEMM's fp32 slabs part[sk][T][H]
+// are summed in slab order and rounded to bf16 while staging -- exactly what splitk_reduce
+// would have stored -- so the GEMM's own reduce launch and its bf16 [T, H] round trip go.
 template <int W, int VPT>
 __global__ void __launch_bounds__(512)
-ar_add_rmsnorm_kernel(ArPeers P, const bf16_t* __restrict__ in, bf16_t* __restrict__ residual,
-                      const bf16_t* __restrict__ w, bf16_t* __restrict__ out, float eps, int rank,
-                      int T, int H, long half_off, int twoshot) {
+ar_add_rmsnorm_kernel(ArPeers P, const bf16_t* __restrict__ in, const float* __restrict__ part,
+                      int sk, bf16_t* __restrict__ residual, const bf16_t* __restrict__ w,
+                      bf16_t* __restrict__ out, float eps, int rank, int T, int H, long half_off,
+                      int twoshot) {
   __shared__ float scratch[8];
   ArSignal* own = P.sig[rank];
   const long off = call_half_off(own, half_off);
@@ -198,7 +202,25 @@ ar_add_rmsnorm_kernel(ArPeers P, const bf16_t* __restrict__ in, bf16_t* __restri
 #pragma unroll
       for (int i = 0; i < VPT; ++i) {
         const int idx = threadIdx.x + i * 512;
-        if (idx < nvec) mine[row + idx] = xin[row + idx];
+        if (idx >= nvec) continue;
+        if (part != nullptr) {
+          const long e = (row + idx) * 8, slab = (long)T * H;
+          f32x4 a0 = *reinterpret_cast<const f32x4*>(part + e);
+          f32x4 a1 = *reinterpret_cast<const f32x4*>(part + e + 4);
+          for (int q = 1; q < sk; ++q) {
+            a0 += *reinterpret_cast<const f32x4*>(part + q * slab + e);
+            a1 += *reinterpret_cast<const f32x4*>(part + q * slab + e + 4);
+          }
+          bf16x8 v;
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            v[j] = f2bf(a0[j]);
+            v[j + 4] = f2bf(a1[j]);
+          }
+          mine[row + idx] = v;
+        } else {
+          mine[row + idx] = xin[row + idx];
+        }
       }
     }
   block_barrier(P, rank, W, ep, own);
@@ -316,11 +338,11 @@ EIA_API int eia_ar_run(void* const* peers_sig, void* const* peers_data, int rank
   EIA_LAUNCH_CHECK();
 }
 
-// in [T,H] (partial sums, may alias out), residual [T,H] updated in place, w [H], out [T,H].
-EIA_API int eia_ar_add_rmsnorm(void* const* peers_sig, void* const* peers_data, int rank,
-                               int world, const void* in, void* residual, const void* w,
-                               void* out, float eps, int T, int H, long max_bytes, int twoshot,
-                               int nblocks, hipStream_t st) {
+namespace {
+int ar_add_rmsnorm_impl(void* const* peers_sig, void* const* peers_data, int rank, int world,
+                        const void* in, const float* part, int sk, void* residual, const void* w,
+                        void* out, float eps, int T, int H, long max_bytes, int twoshot,
+                        int nblocks, hipStream_t st) {
   if (world < 2 || world > AR_MAXR || rank < 0 || rank >= world) return EIA_BAD_SHAPE;
   if (H % 8 != 0 || T < 0 || (long)T * H * 2 > max_bytes || nblocks < 1 || nblocks > AR_MAXB)
     return EIA_BAD_SHAPE;
@@ -335,7 +357,7 @@ EIA_API int eia_ar_add_rmsnorm(void* const* peers_sig, void* const* peers_data, 
   }
 #define ARN_LAUNCH(WW, V)                                                                    \
   hipLaunchKernelGGL((ar_add_rmsnorm_kernel<WW, V>), dim3(nblocks), dim3(512), 0, st, P,      \
-                     static_cast<const bf16_t*>(in), static_cast<bf16_t*>(residual),         \
+                     static_cast<const bf16_t*>(in), part, sk, static_cast<bf16_t*>(residual), \
                      static_cast<const bf16_t*>(w), static_cast<bf16_t*>(out), eps, rank, T, H, \
                      max_bytes, twoshot)
 #define ARN_V(WW)                                              \
@@ -356,6 +378,27 @@ EIA_API int eia_ar_add_rmsnorm(void* const* peers_sig, void* const* peers_data, 
 #undef ARN_V
 #undef ARN_LAUNCH
   EIA_LAUNCH_CHECK();
+}
+}  // namespace
+
+// in [T,H] (partial sums, may alias out), residual [T,H] updated in place, w [H], out [T,H].
+EIA_API int eia_ar_add_rmsnorm(void* const* peers_sig, void* const* peers_data, int rank,
+                               int world, const void* in, void* residual, const void* w,
+                               void* out, float eps, int T, int H, long max_bytes, int twoshot,
+                               int nblocks, hipStream_t st) {
+  return ar_add_rmsnorm_impl(peers_sig, peers_data, rank, world, in, nullptr, 0, residual, w, out,
+                             eps, T, H, max_bytes, twoshot, nblocks, st);
+}
+
+// The same with this rank's partial sums still split over K: part fp32 [sk][T][H] (the skinny
+// GEMM's MODE_F32_SPLIT slabs), summed while staging.
+EIA_API int eia_ar_add_rmsnorm_splitk(void* const* peers_sig, void* const* peers_data, int rank,
+                                      int world, const float* part, int sk, void* residual,
+                                      const void* w, void* out, float eps, int T, int H,
+                                      long max_bytes, int twoshot, int nblocks, hipStream_t st) {
+  if (part == nullptr || sk < 1) return EIA_BAD_SHAPE;
+  return ar_add_rmsnorm_impl(peers_sig, peers_data, rank, world, nullptr, part, sk, residual, w,
+                             out, eps, T, H, max_bytes, twoshot, nblocks, st);
 }
 
 EIA_API int eia_ar_read_err(const void* sig, int* err) {

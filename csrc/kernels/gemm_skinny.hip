@@ -43,8 +43,14 @@ constexpr int XPAD = 8;             // LDS row padding (elements)
 #endif
 constexpr int KLANE = EIA_GEMM_KLANE;
 constexpr int KSTEP = KLANE == 8 ? 32 : 8;
+static_assert(KLANE == 8 || KLANE == 32, "EIA_GEMM_KLANE must be 8 or 32");
 
-enum Mode : int { MODE_BF16 = 0, MODE_F32_SPLIT = 1, MODE_SWIGLU = 2 };
+// MODE_SWIGLU_SPLIT: the SwiGLU pairing over a K range split across grid.y -- fp32 gate and
+// up partials [sk][M][2I] (gate at n, up at I + n), finished by eia_splitk_swiglu.  For gate/up
+// widths too narrow to fill the chip with whole-K pair tiles (Llama-70B at TP 8: 224 tiles).
+enum Mode : int { MODE_BF16 = 0, MODE_F32_SPLIT = 1, MODE_SWIGLU = 2, MODE_SWIGLU_SPLIT = 3 };
+
+__host__ __device__ inline bool swiglu_pairing(int mode) { return mode == MODE_SWIGLU || mode == MODE_SWIGLU_SPLIT; }
 
 EIA_DEV float silu(float x) { return __fdividef(x, 1.f + __expf(-x)); }
 
@@ -64,7 +70,20 @@ EIA_DEV bf16x8 ld_w(const bf16_t* p) {
 template <int MT, int NT>
 EIA_DEV void store_tile(const f32x4 (&acc)[NT][MT], int mode, void* __restrict__ out, long ldo,
                         int M, int N, int Mc, long orow0, int nbase, int r, int g,
-                        const bf16_t* __restrict__ bias) {
+                        const bf16_t* __restrict__ bias, int inter) {
+  if (NT == 2 && mode == MODE_SWIGLU_SPLIT) {
+    float* o = reinterpret_cast<float*>(out) + (long)blockIdx.y * M * N;
+    const int n = nbase + 4 * g;
+#pragma unroll
+    for (int m = 0; m < MT; ++m) {
+      const int row = m * 16 + r;
+      if (row < Mc) {
+        *reinterpret_cast<f32x4*>(o + (orow0 + row) * N + n) = acc[0][m];
+        *reinterpret_cast<f32x4*>(o + (orow0 + row) * N + inter + n) = acc[NT - 1][m];
+      }
+    }
+    return;
+  }
   if (NT == 2 && mode == MODE_SWIGLU) {
     bf16_t* o = reinterpret_cast<bf16_t*>(out);
     const int n = nbase + 4 * g;
@@ -138,6 +157,8 @@ gemm_skinny_kernel(const bf16_t* __restrict__ X, long ldx, const bf16_t* __restr
                    const bf16_t* __restrict__ bias, void* __restrict__ out, long ldo, int M, int N,
                    int krange, int mode, int inter, const int* __restrict__ offs,
                    const int* __restrict__ row_idx, long w_estride, int rot_mul) {
+  // the packed layouts (pack_weight / pack_weight_wg) store k = 32 s + 8 g + j
+  static_assert(PK == 0 || KLANE == 8, "packed weight layouts assume EIA_GEMM_KLANE == 8");
   extern __shared__ __align__(16) bf16_t xs[];   // [2][MT*16][XLD]
   constexpr int XLD = KC + XPAD;     // LDS row stride (elements)
   constexpr int NST = KC / 32;       // 32-deep MFMA steps per chunk
@@ -179,7 +200,7 @@ gemm_skinny_kernel(const bf16_t* __restrict__ X, long ldx, const bf16_t* __restr
   // strides (elements) between a lane's fragments: MFMA step s, 128-deep super-step
   constexpr int WS_STEP = PK ? 512 : KSTEP;
   constexpr int WS_SUPER = PK == 2 ? WAVES * NT * 2048 : (PK ? 2048 : 128);
-  if (NT == 2 && mode == MODE_SWIGLU) {
+  if (NT == 2 && swiglu_pairing(mode)) {
     nbase = blockIdx.x * (WAVES * 16) + wave * 16;      // output column block
     wp[0] = W + (PK == 2 ? wgp(0) : wrow(nbase));
     wp[NT - 1] = W + (PK == 2 ? wgp(1) : wrow(inter + nbase));
@@ -360,7 +381,7 @@ gemm_skinny_kernel(const bf16_t* __restrict__ X, long ldx, const bf16_t* __restr
           phase(c + s, w[s], w[(s + S - 1) % S], xr[(s + S - 1) % S], xr[(s + 1) % S]);
     }
 
-    store_tile<MT, NT>(acc, mode, out, ldo, M, N, Mc, mbase + m0, nbase, r, g, bias);
+    store_tile<MT, NT>(acc, mode, out, ldo, M, N, Mc, mbase + m0, nbase, r, g, bias, inter);
   }
 }
 
@@ -432,7 +453,7 @@ gemm_glds_kernel(const bf16_t* __restrict__ X, long ldx, const bf16_t* __restric
   };
   constexpr int WS_STEP = PACKED ? 512 : KSTEP;
   constexpr int WS_CHUNK = PACKED ? 2048 : 128;
-  if (NT == 2 && mode == MODE_SWIGLU) {
+  if (NT == 2 && swiglu_pairing(mode)) {
     nbase = blockIdx.x * (4 * 16) + wave * 16;
     wp[0] = W + wrow(nbase);
     wp[NT - 1] = W + wrow(inter + nbase);
@@ -496,7 +517,7 @@ gemm_glds_kernel(const bf16_t* __restrict__ X, long ldx, const bf16_t* __restric
     compute(c % D);
   }
   wait_vmcnt<0>();                         // no DMA may land after the workgroup exits
-  store_tile<MT, NT>(acc, mode, out, ldo, M, N, M, 0, nbase, r, g, bias);
+  store_tile<MT, NT>(acc, mode, out, ldo, M, N, M, 0, nbase, r, g, bias, inter);
 }
 
 // Sum SK fp32 slabs [SK][M][N] (+bias) -> bf16 out[M][ldo].  One thread per 4 columns.
@@ -512,6 +533,49 @@ splitk_reduce_kernel(const float* __restrict__ part, int sk, int M, int N,
   bf16x4 v;
 #pragma unroll
   for (int i = 0; i < 4; ++i) v[i] = f2bf(s[i] + (bias ? bf2f(bias[col + i]) : 0.f));
+  *reinterpret_cast<bf16x4*>(out + (long)row * ldo + col) = v;
+}
+
+// out[M][I] = silu(sum_k gate_k) * sum_k up_k from the MODE_SWIGLU_SPLIT partials
+// part[sk][M][2I] (gate at column n, up at I + n): one 4-column group per thread, every slab
+// load in flight before the first add (SK a template parameter; 0 = runtime loop).
+template <int SK>
+__global__ void __launch_bounds__(256)
+splitk_swiglu_kernel(const float* __restrict__ part, int sk_rt, int M, int I,
+                     bf16_t* __restrict__ out, long ldo) {
+  const long idx = ((long)blockIdx.x * blockDim.x + threadIdx.x) * 4;
+  const long total = (long)M * I;
+  if (idx >= total) return;
+  const int row = idx / I, col = idx % I;
+  const long slab = (long)M * 2 * I;
+  const float* p = part + (long)row * 2 * I + col;
+  const int sk = SK > 0 ? SK : sk_rt;
+  f32x4 gs, us;
+  if constexpr (SK > 0) {
+    f32x4 gv[SK], uv[SK];
+#pragma unroll
+    for (int k = 0; k < SK; ++k) {
+      gv[k] = *reinterpret_cast<const f32x4*>(p + k * slab);
+      uv[k] = *reinterpret_cast<const f32x4*>(p + k * slab + I);
+    }
+    gs = gv[0];
+    us = uv[0];
+#pragma unroll
+    for (int k = 1; k < SK; ++k) {
+      gs += gv[k];
+      us += uv[k];
+    }
+  } else {
+    gs = *reinterpret_cast<const f32x4*>(p);
+    us = *reinterpret_cast<const f32x4*>(p + I);
+    for (int k = 1; k < sk; ++k) {
+      gs += *reinterpret_cast<const f32x4*>(p + k * slab);
+      us += *reinterpret_cast<const f32x4*>(p + k * slab + I);
+    }
+  }
+  bf16x4 v;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) v[i] = f2bf(silu(gs[i]) * us[i]);
   *reinterpret_cast<bf16x4*>(out + (long)row * ldo + col) = v;
 }
 
@@ -601,7 +665,7 @@ int launch_cfg(const bf16_t* X, long ldx, const bf16_t* W, long ldw, const bf16_
     const char* e = getenv("EIA_MOE_ROT");
     return e != nullptr ? atoi(e) : 3;
   }();
-  dim3 grid(mode == MODE_SWIGLU ? (N / 2) / (WAVES * 16) : N / (WAVES * NT * 16), sk, experts);
+  dim3 grid(swiglu_pairing(mode) ? (N / 2) / (WAVES * 16) : N / (WAVES * NT * 16), sk, experts);
   hipLaunchKernelGGL((gemm_skinny_kernel<MT, NT, WAVES, S, GROUPED, KC, LOADER, PACKED>), grid, dim3(WAVES * 64 + (LOADER ? 64 : 0)), lds, st,
                      X, ldx, W, ldw, bias, out, ldo, M, N, K / sk, mode, N / 2, offs, row_idx,
                      w_estride, GROUPED ? ((K / sk) / KC >= 8 ? moe_rot : 0) : rot_mul);
@@ -621,7 +685,7 @@ int launch_glds(const bf16_t* X, long ldx, const bf16_t* W, long ldw, const bf16
                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
       attr_set = true;
     }
-    dim3 grid(mode == MODE_SWIGLU ? (N / 2) / 64 : N / (64 * NT), sk);
+    dim3 grid(swiglu_pairing(mode) ? (N / 2) / 64 : N / (64 * NT), sk);
     hipLaunchKernelGGL((gemm_glds_kernel<MT, NT, D, PACKED>), grid, dim3(256), lds, st, X, ldx, W,
                        ldw, bias, out, ldo, M, N, K / sk, mode, N / 2, rot_mul);
     return (int)hipGetLastError();
@@ -824,16 +888,17 @@ int check_shape(int N, int K, int sk, int mode, int cfg) {
     }
   }
   // 3-wave form: register-staged, plain layout, no SwiGLU pairing, 2-3 stages
-  if ((cfg & 512) && ((cfg & (2 | 8 | 32 | 64 | 128 | 256)) || mode == MODE_SWIGLU))
+  if ((cfg & 512) && ((cfg & (2 | 8 | 32 | 64 | 128 | 256)) || swiglu_pairing(mode)))
     return EIA_BAD_SHAPE;
   // 7-wave form: SwiGLU pairs only, register-staged, plain layout
-  if ((cfg & 256) && (mode != MODE_SWIGLU || !(cfg & 1) || (cfg & (2 | 8 | 32 | 64 | 128))))
+  if ((cfg & 256) && (!swiglu_pairing(mode) || !(cfg & 1) || (cfg & (2 | 8 | 32 | 64 | 128))))
     return EIA_BAD_SHAPE;
   if ((cfg & 32) && !((cfg & 16) && (cfg & 2))) return EIA_BAD_SHAPE;   // loader: 4 waves, KC 128
   if ((cfg & 128) && ((cfg & 32) || !(cfg & 16) || !(cfg & 2) || ((cfg >> 2) & 3) == 3))
     return EIA_BAD_SHAPE;                                                // LDS-DMA ring
-  if (mode == MODE_SWIGLU) {
-    if (nt != 2 || sk != 1 || N % 2 != 0 || (N / 2) % (waves * 16) != 0) return EIA_BAD_SHAPE;
+  if (swiglu_pairing(mode)) {
+    if (nt != 2 || (mode == MODE_SWIGLU && sk != 1) || N % 2 != 0 || (N / 2) % (waves * 16) != 0)
+      return EIA_BAD_SHAPE;
   } else if (N % (waves * nt * 16) != 0) {
     return EIA_BAD_SHAPE;
   }
@@ -846,6 +911,8 @@ int check_shape(int N, int K, int sk, int mode, int cfg) {
 // mode 0: out bf16 [M][ldo] (+bias), sk must be 1
 // mode 1: out fp32 partial slabs [sk][M][N] (reduce with eia_splitk_reduce / _add_rmsnorm)
 // mode 2: SwiGLU: W = merged [gate; up] (N = 2I rows), out bf16 [M][ldo] = silu(gate) * up
+// mode 3: SwiGLU pairing, K split over sk: out fp32 [sk][M][2I] (gate n, up I + n), finished by
+//         eia_splitk_swiglu
 // cfg: bit0 -> two 16-row W tiles per wave (else one), bit1 -> 4 waves per workgroup (else 2),
 // bits 2-3 -> W pipeline stages - 2 (2..4), bit 4 -> 128-deep K chunks (else 256),
 // bit 5 -> extra X-loader wave (with bits 1 and 4), bit 6 -> tile-packed W (ldw must be K),
@@ -884,7 +951,8 @@ EIA_API int eia_gemm_skinny(const void* X, long ldx, const void* W, long ldw, co
 EIA_API int eia_moe_gemm(const void* X, long ldx, const void* W, long ldw, const void* bias,
                          void* out, long ldo, int N, int K, int experts, const int* offs,
                          const int* row_idx, int mt_hint, int mode, int cfg, hipStream_t st) {
-  if (experts < 1 || mode == MODE_F32_SPLIT || (cfg & ~(3 | 1024))) return EIA_BAD_SHAPE;
+  if (experts < 1 || mode == MODE_F32_SPLIT || mode == MODE_SWIGLU_SPLIT || (cfg & ~(3 | 1024)))
+    return EIA_BAD_SHAPE;
   if ((cfg & 1024) && ldw != K) return EIA_BAD_SHAPE;
   if (int rc = check_shape(N, K, 1, mode, cfg)) return rc;
   if ((ldx % 8) || (ldw % 8) || (ldo % 4)) return EIA_BAD_SHAPE;
@@ -916,6 +984,22 @@ EIA_API int eia_splitk_reduce(const float* part, int sk, int M, int N, const voi
   const long n4 = (long)M * N / 4;
   hipLaunchKernelGGL(splitk_reduce_kernel, dim3((n4 + 255) / 256), dim3(256), 0, st, part, sk, M, N,
                      static_cast<const bf16_t*>(bias), static_cast<bf16_t*>(out), ldo);
+  EIA_LAUNCH_CHECK();
+}
+
+EIA_API int eia_splitk_swiglu(const float* part, int sk, int M, int I, void* out, long ldo,
+                              hipStream_t st) {
+  if (I % 4 != 0 || sk < 1 || M < 1 || ldo % 4 != 0) return EIA_BAD_SHAPE;
+  const long n4 = (long)M * I / 4;
+  bf16_t* o = static_cast<bf16_t*>(out);
+  const dim3 grid((n4 + 255) / 256), block(256);
+  switch (sk) {
+    case 2: hipLaunchKernelGGL(splitk_swiglu_kernel<2>, grid, block, 0, st, part, sk, M, I, o, ldo); break;
+    case 4: hipLaunchKernelGGL(splitk_swiglu_kernel<4>, grid, block, 0, st, part, sk, M, I, o, ldo); break;
+    case 8: hipLaunchKernelGGL(splitk_swiglu_kernel<8>, grid, block, 0, st, part, sk, M, I, o, ldo); break;
+    case 16: hipLaunchKernelGGL(splitk_swiglu_kernel<16>, grid, block, 0, st, part, sk, M, I, o, ldo); break;
+    default: hipLaunchKernelGGL(splitk_swiglu_kernel<0>, grid, block, 0, st, part, sk, M, I, o, ldo); break;
+  }
   EIA_LAUNCH_CHECK();
 }
 

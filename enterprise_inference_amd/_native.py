@@ -63,10 +63,7 @@ _SIGNATURES = {
     "eia_gemm_skinny": [P, L, P, L, P, P, L, I, I, I, I, I, I, S],
     "eia_gemm_prefill": [P, L, P, L, P, L, I, I, I, I, S],
     "eia_splitk_reduce": [P, I, I, I, P, P, L, S],
-    "eia_mlp_fused": [P, L, P, P, P, P, IP, I, I, I, I, S],
-    "eia_mlp_fused_plan": [I, I, I, I, P],
-    "eia_mlp_fused_dbg": [P, L, P, P, P, P, IP, I, I, I, I, I, P, S],
-    "eia_mlp_fused_error": [IP, I, P],
+    "eia_splitk_swiglu": [P, I, I, I, P, L, S],
     "eia_splitk_add_rmsnorm": [P, I, I, I, P, P, F, P, L, S],
     "eia_ar_alloc": [P, L],
     "eia_moe_splitk_norm_route": [P, I, I, I, P, P, F, P, L, P, I, I, I, I, P, P, P, S],
@@ -78,6 +75,7 @@ _SIGNATURES = {
     "eia_ar_read_err_async": [P, P, S],
     "eia_ar_set_err": [P, I],
     "eia_ar_add_rmsnorm": [P, P, I, I, P, P, P, P, F, I, I, L, I, I, S],
+    "eia_ar_add_rmsnorm_splitk": [P, P, I, I, P, I, P, P, P, F, I, I, L, I, I, S],
 }
 
 

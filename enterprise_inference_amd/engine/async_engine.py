@@ -24,12 +24,40 @@ import os
 import queue
 import threading
 import time
-from typing import AsyncIterator, Dict, Optional
+import weakref
+from typing import AsyncIterator, Callable, Dict, Optional
 
 from .llm_engine import LLMEngine, RequestOutput
 from .sampling_params import SamplingParams
 
 logger = logging.getLogger(__name__)
+
+
+class SubmittedStream:
+    """Async iterator over one submitted request's outputs.
+
+    ``submit`` hands the request to the engine before anyone iterates, so the release of an
+    abandoned request cannot live only in the output generator's ``finally``: a generator
+    that never started (the client disconnected while the streaming response was still
+    sending its headers, or a later prompt of the same completion failed to submit) has no
+    frame and its ``finally`` never runs.  The finaliser here runs when the stream is dropped
+    and releases the request if nothing else has (``on_abandon`` must be idempotent)."""
+
+    __slots__ = ("_gen", "_fin", "__weakref__")
+
+    def __init__(self, gen, on_abandon: Callable[[], None]):
+        self._gen = gen
+        self._fin = weakref.finalize(self, on_abandon)
+
+    def __aiter__(self):
+        return self
+
+    async def __anext__(self):
+        return await self._gen.__anext__()
+
+    async def aclose(self) -> None:
+        await self._gen.aclose()
+        self._fin()
 
 
 class EngineDeadError(RuntimeError):
@@ -96,23 +124,30 @@ class AsyncLLMEngine:
         self._cmds.put(("add", request_id, prompt, params, prompt_token_ids, time.time(), priority,
                         multi_modal_data))
         self._wake.set()
-        return self._outputs(request_id, q)
+        return SubmittedStream(self._outputs(request_id, q),
+                               lambda: self._release(request_id, abort=True))
+
+    def _release(self, request_id: str, abort: bool) -> None:
+        """Drop the request's stream; abort it in the engine if it was still open."""
+        if self._streams.pop(request_id, None) is not None and abort:
+            self.abort(request_id)
+        self._loops.pop(request_id, None)
 
     async def _outputs(self, request_id: str, q: asyncio.Queue) -> AsyncIterator[RequestOutput]:
+        finished = False
         try:
             while True:
                 item = await q.get()
                 if isinstance(item, BaseException):
+                    finished = True
                     raise item
                 yield item
                 if item.finished:
+                    finished = True
                     return
-        except (asyncio.CancelledError, GeneratorExit):
-            self.abort(request_id)   # client disconnected
-            raise
         finally:
-            self._streams.pop(request_id, None)
-            self._loops.pop(request_id, None)
+            # client disconnected / generator closed early -> abort in the engine
+            self._release(request_id, abort=not finished)
 
     def abort(self, request_id: str) -> None:
         self._cmds.put(("abort", request_id))

@@ -46,7 +46,7 @@ import sys
 import time
 from typing import Dict, Optional
 
-from .async_engine import EngineDeadError
+from .async_engine import EngineDeadError, SubmittedStream
 from .llm_engine import CompletionOutput, RequestMetrics, RequestOutput
 
 logger = logging.getLogger(__name__)
@@ -454,7 +454,14 @@ class MPEngineClient:
         self._reqs[request_id] = _ReqState(q, prompt, list(prompt_token_ids))
         self._send(("add", request_id, prompt, params, prompt_token_ids, time.time(), priority,
                     multi_modal_data))
-        return self._outputs(request_id, q)
+        return SubmittedStream(self._outputs(request_id, q),
+                               lambda: self._release(request_id, abort=True))
+
+    def _release(self, request_id: str, abort: bool) -> None:
+        """Forget the request; abort it in the core if it was still open (idempotent: the
+        output generator and the stream's finaliser may both call it)."""
+        if self._reqs.pop(request_id, None) is not None and abort and self.dead is None:
+            self.abort(request_id)
 
     async def _outputs(self, request_id: str, q: asyncio.Queue):
         finished = False
@@ -469,9 +476,8 @@ class MPEngineClient:
                     finished = True
                     return
         finally:
-            self._reqs.pop(request_id, None)
-            if not finished and self.dead is None:
-                self.abort(request_id)     # client disconnected / generator closed early
+            # client disconnected / generator closed early -> abort in the core
+            self._release(request_id, abort=not finished)
 
     def abort(self, request_id: str) -> None:
         if self._writer is not None and not self._writer.is_closing():

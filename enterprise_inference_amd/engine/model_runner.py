@@ -914,6 +914,11 @@ class ModelRunner:
             return 0.0
         t0 = time.time()
         buckets = buckets or graph_buckets(self.max_num_seqs, self.cfg.scheduler.decode_bs_bucket_step)
+        if any(getattr(m, "a2a", False) for m in self.model.modules()):
+            # all-to-all EP: batches past the padded exchange's limit take the exact form,
+            # which reads the split sizes back to the host -- those run eagerly
+            from ..parallel.expert_parallel import PADDED_MAX_TOKENS
+            buckets = [b for b in buckets if b <= PADDED_MAX_TOKENS]
         self.graph_logits: Dict[int, torch.Tensor] = {}
         self.graph_pool = torch.cuda.graph_pool_handle()
         # dummy decode inputs: len 1, slot -1 (no cache write), block 0

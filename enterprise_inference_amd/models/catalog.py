@@ -55,6 +55,13 @@ PRESETS: Dict[str, dict] = {
     "meta-llama/Meta-Llama-3-70B-Instruct": _llama(8192, 28672, 80, 64, 8, rope_scaling=None,
                                                    max_position_embeddings=8192),
     "meta-llama/Llama-3.1-405B-Instruct": _llama(16384, 53248, 126, 128, 8),
+    # ONE tensor-parallel rank of Llama-3.3-70B at TP 8 (BASELINE config #3, reference
+    # core/playbooks/deploy-inference-models.yml:1884): 8 q / 1 kv heads x 128, I 3584, the
+    # vocab-parallel LM head's 16032 rows.  Served at TP 1 it runs exactly the rank's decode
+    # GEMMs, attention and norms -- everything but the all-reduces -- so the per-rank step can be
+    # profiled on one GPU (scripts/gpu_model_steps.sh).  A profiling proxy, not a real model.
+    "eia/Llama-3.3-70B-TP8-rank": _llama(8192, 3584, 80, 8, 1, head_dim=128, vocab_size=16032,
+                                         bos_token_id=1, eos_token_id=[2]),
     "meta-llama/Llama-3.2-3B-Instruct": _llama(3072, 8192, 28, 24, 8, tie_word_embeddings=True,
                                                rope_scaling={**_LLAMA31_ROPE, "factor": 32.0}),
     "deepseek-ai/DeepSeek-R1-Distill-Llama-8B": _llama(4096, 14336, 32, 32, 8,
@@ -141,6 +148,7 @@ SHORT_NAMES: Dict[str, str] = {
     "cpu-qwen3-1-7b": "Qwen/Qwen3-1.7B",
     "cpu-qwen3-4b": "Qwen/Qwen3-4B-Instruct-2507",
     "opt-125m": "facebook/opt-125m",
+    "llama-70b-tp8-rank": "eia/Llama-3.3-70B-TP8-rank",
     # BASELINE.json config names
     "Llama-3-8B": "meta-llama/Llama-3.1-8B-Instruct",
     "Llama-3-70B": "meta-llama/Llama-3.3-70B-Instruct",

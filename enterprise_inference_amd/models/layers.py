@@ -159,7 +159,10 @@ class PendingAllReduce:
         self.partial = partial
 
     def materialize(self) -> torch.Tensor:
-        return comm.all_reduce(self.partial)
+        p = self.partial
+        if hasattr(p, "materialize"):          # split-K slabs (gemm.SplitK)
+            p = p.materialize()
+        return comm.all_reduce(p)
 
 
 class RowParallelLinear(nn.Module):
@@ -192,9 +195,11 @@ class RowParallelLinear(nn.Module):
                 and x.shape[0] >= _overlap_min_tokens()):
             y = self._gemm_ar_overlapped(x)
             return y + self.bias if self.bias is not None else y
+        if defer_reduce and self.bias is None and x.dim() == 2:
+            # decode: the GEMM's split-K slabs (if it splits) go straight to the fused
+            # all-reduce + add + RMSNorm kernel, which sums them while staging
+            return PendingAllReduce(gemm.linear(x, self.weight, defer_reduce=True))
         y = gemm.linear(x, self.weight)
-        if defer_reduce and self.bias is None and y.dim() == 2:
-            return PendingAllReduce(y)
         if self.reduce_results:
             y = comm.all_reduce(y)
         if self.bias is not None:

@@ -85,13 +85,6 @@ class LlamaMLP(nn.Module):
         self.act = "silu" if act in ("silu", "swish") else act
 
     def forward(self, x: torch.Tensor):
-        from ..ops import gemm
-        from ..parallel import state
-        if (self.act == "silu" and state.tp_size() == 1 and self.gate_up_proj.bias is None
-                and self.down_proj.bias is None
-                and gemm.mlp_fused_ok(x, self.gate_up_proj.weight, self.down_proj.weight)):
-            # decode batch: gate_up + SwiGLU + down in one launch (ops/gemm.py mlp_fused)
-            return gemm.mlp_fused(x, self.gate_up_proj.weight, self.down_proj.weight)
         return self.down_proj(self.gate_up_proj.forward_act_and_mul(x, self.act), defer_reduce=True)
 
 

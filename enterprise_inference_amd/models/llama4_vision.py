@@ -160,6 +160,75 @@ def _open_stream(url: str, headers: dict, extensions: dict, timeout: float,
             r.close()
 
 
+class _ProxiedResponse:
+    """The slice of an httpx streamed response ``fetch_image_bytes`` reads, over an
+    http.client response."""
+
+    def __init__(self, resp):
+        self._r = resp
+        self.status_code = resp.status
+        self.headers = {k.lower(): v for k, v in resp.getheaders()}
+        self.is_redirect = resp.status in (301, 302, 303, 307, 308) and "location" in self.headers
+        self.extensions = {}
+
+    def raise_for_status(self) -> None:
+        if self.status_code >= 400:
+            raise ValueError(f"image fetch failed: HTTP {self.status_code}")
+
+    def iter_bytes(self, size: int = 1 << 16):
+        while True:
+            b = self._r.read(size)
+            if not b:
+                return
+            yield b
+
+
+@contextlib.contextmanager
+def _open_proxied_stream(url: str, headers: dict, extensions: dict, timeout: float, proxy: str):
+    """One GET of the PINNED target ``url`` (host = the validated address) through the egress
+    proxy, so the proxy dials exactly the address the policy check vetted -- it never
+    resolves the name itself, which would reopen the DNS-rebinding window:
+
+    * http: absolute-form request ``GET http://<ip>:<port>/path`` with Host = the name;
+    * https: ``CONNECT <ip>:<port>``, then TLS inside the tunnel with SNI and certificate
+      verification against the NAME (``sni_hostname``).  httpx's tunnel takes the TLS server
+      name from the CONNECT target, so this path is built on http.client.
+    """
+    import base64 as b64
+    import http.client
+    import ssl
+    from urllib.parse import unquote, urlparse
+
+    u, pu = urlparse(url), urlparse(proxy)
+    if pu.scheme not in ("http", ""):
+        raise ValueError(f"unsupported egress proxy scheme {pu.scheme!r}")
+    auth = {}
+    if pu.username:
+        cred = f"{unquote(pu.username)}:{unquote(pu.password or '')}".encode()
+        auth = {"Proxy-Authorization": "Basic " + b64.b64encode(cred).decode()}
+    port = u.port or (443 if u.scheme == "https" else 80)
+    path = (u.path or "/") + (f"?{u.query}" if u.query else "")
+    if u.scheme == "https":
+        name = extensions["sni_hostname"]
+        ctx = ssl.create_default_context()
+
+        class _Tunnel(http.client.HTTPSConnection):
+            def connect(self):
+                http.client.HTTPConnection.connect(self)       # TCP to the proxy + CONNECT
+                self.sock = ctx.wrap_socket(self.sock, server_hostname=name)
+
+        conn = _Tunnel(pu.hostname, pu.port or 3128, timeout=timeout, context=ctx)
+        conn.set_tunnel(u.hostname, port, headers=auth)
+        conn.request("GET", path, headers=headers)
+    else:
+        conn = http.client.HTTPConnection(pu.hostname, pu.port or 3128, timeout=timeout)
+        conn.request("GET", url, headers={**headers, **auth})
+    try:
+        yield _ProxiedResponse(conn.getresponse())
+    finally:
+        conn.close()
+
+
 def fetch_image_bytes(url: str, max_bytes: Optional[int] = None, timeout: float = 30.0) -> bytes:
     """Download an image URL with the media policy above and a byte cap (streamed: a huge or
     endless body is cut off at ``max_bytes`` instead of being buffered).  Redirects are
@@ -171,17 +240,20 @@ def fetch_image_bytes(url: str, max_bytes: Optional[int] = None, timeout: float 
     cap = MAX_IMAGE_BYTES if max_bytes is None else max_bytes
     for _ in range(5):
         ip = _check_url(url)
-        # Behind an egress proxy (enterprise clusters) the proxy dials the origin: the request
-        # carries the NAME (our own resolution above still applied the policy) and the peer
-        # is the proxy, so neither the pin nor the peer check applies.  Direct fetches dial
-        # the validated address with the environment's proxy settings ignored.
-        proxied = ip is not None and _proxy_for(url) is not None
-        if ip is None or proxied:
+        # Behind an egress proxy (enterprise clusters, HTTP(S)_PROXY not bypassed by NO_PROXY
+        # for the name) the PINNED target goes through the proxy: the proxy dials the address
+        # validated above (CONNECT <ip> / absolute-form http://<ip>), TLS still verifies the
+        # name.  The peer check cannot apply there (the peer is the proxy).  Direct fetches
+        # dial the validated address with the environment's proxy settings ignored.
+        proxy = _proxy_for(url) if ip is not None else None
+        if ip is None:
             target, headers, ext = url, {}, {}
         else:
             target, headers, ext = _pinned_request(url, ip)
-        with _open_stream(target, headers, ext, timeout, trust_env=ip is None or proxied) as r:
-            if ip is not None and not proxied:   # defence in depth: peer is the checked address
+        opener = (_open_proxied_stream(target, headers, ext, timeout, proxy) if proxy
+                  else _open_stream(target, headers, ext, timeout, trust_env=ip is None))
+        with opener as r:
+            if ip is not None and not proxy:   # defence in depth: peer is the checked address
                 stream = r.extensions.get("network_stream")
                 peer = stream.get_extra_info("server_addr") if stream is not None else None
                 if peer and ipaddress.ip_address(str(peer[0]).split("%")[0]) != ip:

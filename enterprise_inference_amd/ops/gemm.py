@@ -32,7 +32,7 @@ TUNING_FILE = resolve("gemm_tuning.json", os.path.join(_HERE, "gemm_tuning.json"
 PREFILL_TUNING_FILE = resolve("tunableop_mi355x.csv", os.path.join(_HERE, "tunableop_mi355x.csv"),
                               "EIA_PREFILL_GEMM_TUNING")
 
-MODE_BF16, MODE_SPLIT, MODE_SWIGLU = 0, 1, 2
+MODE_BF16, MODE_SPLIT, MODE_SWIGLU, MODE_SWIGLU_SPLIT = 0, 1, 2, 3
 # kernel configs: bit0 -> 2 W tiles (32 rows) per wave, bit1 -> 4 waves per workgroup
 # bit0 NT=2, bit1 WAVES=4, bits2-3 pipeline stages-2, bit4 128-deep K chunks (else 256)
 # bit5: an extra wave stages X into LDS (4 compute waves, KC 128): 50, 51, 54, 55, 58, 59
@@ -100,15 +100,15 @@ def valid(N: int, K: int, swiglu: bool, cfg: int, sk: int, M: Optional[int] = No
     if cfg & 512:   # 3-wave form: plain GEMMs only
         return not swiglu and N % cfg_rows(cfg) == 0
     if cfg & 256:   # 7-wave SwiGLU form: cfg 273 only, spill-free up to M = 64
-        return (swiglu and cfg == 273 and sk == 1 and (M is None or M <= 64)
+        return (swiglu and cfg == 273 and (M is None or M <= 64)
                 and (N // 2) % (7 * 16) == 0)
     if cfg & 128:
         if M is not None and glds_lds_bytes(cfg, M) > 160 * 1024:
             return False
     elif M is not None and (cfg & 63) in SPILL_CFGS.get(m_bucket(M), ()):
         return False
-    if swiglu:
-        return sk == 1 and (cfg & 1) == 1 and (N // 2) % (cfg_waves(cfg) * 16) == 0
+    if swiglu:   # sk > 1: fp32 gate / up partials finished by eia_splitk_swiglu
+        return (cfg & 1) == 1 and (N // 2) % (cfg_waves(cfg) * 16) == 0
     return N % cfg_rows(cfg) == 0
 
 
@@ -156,10 +156,11 @@ def unpack_weight(p: torch.Tensor) -> torch.Tensor:
 
 
 def heuristic_splitk(N: int, K: int, cfg: int, swiglu: bool = False) -> int:
-    """Smallest K split whose grid covers the chip (K/split a multiple of KC)."""
-    if swiglu:
-        return 1
+    """Smallest K split whose grid covers the chip (K/split a multiple of KC).  SwiGLU keeps
+    whole-K pair tiles (no partials) once they cover most of the chip."""
     tiles = N // cfg_rows(cfg)
+    if swiglu and tiles >= 192:
+        return 1
     nk = K // cfg_kc(cfg)
     best = 1
     for sk in range(1, nk + 1):
@@ -425,20 +426,32 @@ def linear_f32(x: torch.Tensor, w: torch.Tensor) -> Optional[torch.Tensor]:
     return out
 
 
-def swiglu_gemm(x: torch.Tensor, w_gate_up: torch.Tensor, cfg: Optional[int] = None) -> torch.Tensor:
-    """silu(x Wg^T) * (x Wu^T) with W = [gate; up] stacked on dim 0 (K7)."""
+def swiglu_gemm(x: torch.Tensor, w_gate_up: torch.Tensor, cfg: Optional[int] = None,
+                sk: Optional[int] = None) -> torch.Tensor:
+    """silu(x Wg^T) * (x Wu^T) with W = [gate; up] stacked on dim 0 (K7).  ``sk`` > 1 splits K
+    over grid.y (fp32 gate / up partials, finished by one small SwiGLU-reduce launch): for
+    gate/up widths whose whole-K pair tiles cannot fill the chip (Llama-70B at TP 8: 224)."""
     M, K = x.shape
     N = w_gate_up.shape[0]
     if cfg is None:
         pk = choose_packed(M, N, K, True, w_gate_up)
         if pk is not None:
-            cfg, _, w_gate_up = pk
+            cfg, sk, w_gate_up = pk
         else:
-            cfg = choose(M, N, K, True)[0]
+            cfg, sk = choose(M, N, K, True)
+    sk = sk or 1
     out = torch.empty(M, N // 2, dtype=torch.bfloat16, device=x.device)
+    if sk == 1:
+        check(lib().eia_gemm_skinny(ptr(x), x.stride(0), ptr(w_gate_up), w_gate_up.stride(0),
+                                    None, ptr(out), out.stride(0), M, N, K, 1, MODE_SWIGLU, cfg,
+                                    stream(x)), "gemm_skinny_swiglu")
+        return out
+    part = torch.empty(sk, M, N, dtype=torch.float32, device=x.device)
     check(lib().eia_gemm_skinny(ptr(x), x.stride(0), ptr(w_gate_up), w_gate_up.stride(0), None,
-                                ptr(out), out.stride(0), M, N, K, 1, MODE_SWIGLU, cfg, stream(x)),
-          "gemm_skinny_swiglu")
+                                ptr(part), N, M, N, K, sk, MODE_SWIGLU_SPLIT, cfg, stream(x)),
+          "gemm_skinny_swiglu_split")
+    check(lib().eia_splitk_swiglu(ptr(part), sk, M, N // 2, ptr(out), out.stride(0), stream(x)),
+          "splitk_swiglu")
     return out
 
 
@@ -524,87 +537,6 @@ def prefill_gemm(x: torch.Tensor, w: torch.Tensor, swiglu: bool = False) -> torc
                                  out.stride(0), M, N, K, MODE_SWIGLU if swiglu else MODE_BF16,
                                  stream(x)), "gemm_prefill")
     return out
-
-
-# --------------------------------------------------------------------------- fused decode MLP
-# gate_up + SwiGLU and the split-K down projection in ONE launch (csrc/kernels/mlp_fused.hip):
-# 256 balanced producers (every CU streams the same gate/up bytes) hand h to the down
-# consumers split by split through arrival counters -- no second launch, no boundary, and the
-# 32 CUs the 4-pair SwiGLU grid left idle now stream.  Opt-in (EIA_FUSED_MLP=1): measured
-# level with the two launches in isolation and slower in the engine (docs/performance.md,
-# "Round 5: the decode MLP in one launch").
-FUSED_MLP = os.environ.get("EIA_FUSED_MLP", "0") == "1"
-_MLP_SYNC: dict = {}
-_MLP_SYNC_WORDS = 64
-
-
-def mlp_sync_buffer(device: torch.device) -> Optional[torch.Tensor]:
-    """Per-device arrival / departure counters of the fused MLP (zero between launches: every
-    launch leaves them as it found them).  Created outside graph capture (the eager profiling
-    run comes first); a capture that would have to create it takes the two-launch form."""
-    key = (device.type, device.index)
-    t = _MLP_SYNC.get(key)
-    if t is None:
-        if torch.cuda.is_current_stream_capturing():
-            return None
-        t = torch.zeros(_MLP_SYNC_WORDS, dtype=torch.int32, device=device)
-        _MLP_SYNC[key] = t
-    return t
-
-
-@functools.lru_cache(maxsize=4096)
-def mlp_fused_split(M: int, H: int, I: int) -> int:
-    """Down-projection K split of the fused MLP (128-column tiles x split ~ 256 consumers), or
-    0 when the shape has no fused form (eia_mlp_fused_plan)."""
-    if H % 128:
-        return 0
-    sk = max(1, 256 // (H // 128))
-    while sk > 1 and I % sk:
-        sk //= 2
-    if 2 * sk + 1 > _MLP_SYNC_WORDS:
-        return 0
-    import ctypes
-    r = ctypes.c_int(int(os.environ.get("EIA_MLP_ROWS", "0")))
-    return sk if lib().eia_mlp_fused_plan(M, H, I, sk, ctypes.byref(r)) == 0 else 0
-
-
-def mlp_fused_ok(x: torch.Tensor, w_gate_up: torch.Tensor, w_down: torch.Tensor) -> bool:
-    if not FUSED_MLP or DISABLE or x.dim() != 2 or not use_hip(x, w_gate_up, w_down):
-        return False
-    if x.dtype != torch.bfloat16 or w_gate_up.dtype != torch.bfloat16 or \
-            w_down.dtype != torch.bfloat16:
-        return False
-    M, H = x.shape
-    I = w_down.shape[1]
-    if w_gate_up.shape != (2 * I, H) or w_down.shape != (H, I):
-        return False
-    if not (w_gate_up.is_contiguous() and w_down.is_contiguous()) or x.stride(1) != 1 or \
-            x.stride(0) % 8:
-        return False
-    return mlp_fused_split(M, H, I) > 0 and mlp_sync_buffer(x.device) is not None
-
-
-def mlp_fused(x: torch.Tensor, w_gate_up: torch.Tensor, w_down: torch.Tensor) -> SplitK:
-    """down(silu(x Wg^T) * (x Wu^T)) as fp32 split-K partials (the consumer's add + RMSNorm
-    sums them, ``splitk_add_rmsnorm``)."""
-    M, H = x.shape
-    I = w_down.shape[1]
-    sk = mlp_fused_split(M, H, I)
-    h = torch.empty(M, I, dtype=torch.bfloat16, device=x.device)
-    part = torch.empty(sk, M, H, dtype=torch.float32, device=x.device)
-    check(lib().eia_mlp_fused(ptr(x), x.stride(0), ptr(w_gate_up), ptr(w_down), ptr(h),
-                              ptr(part), ptr(mlp_sync_buffer(x.device)), M, H, I, sk,
-                              stream(x)), "mlp_fused")
-    return SplitK(part, sk, M, H)
-
-
-def mlp_fused_error(device: torch.device, sk: int) -> int:
-    """1 when a fused-MLP consumer gave up waiting (bounded spin) since the buffer was made."""
-    import ctypes
-    buf = mlp_sync_buffer(device)
-    v = ctypes.c_int(0)
-    check(lib().eia_mlp_fused_error(ptr(buf), sk, ctypes.byref(v)), "mlp_fused_error")
-    return v.value
 
 
 def splitk_add_rmsnorm(s: SplitK, residual: torch.Tensor, weight: torch.Tensor, eps: float):

@@ -166,9 +166,12 @@ def splitk_norm_route(s, residual: torch.Tensor, weight: torch.Tensor, eps: floa
 
 def fused_moe(x: torch.Tensor, w13: torch.Tensor, w2: torch.Tensor, topk_w: torch.Tensor,
               topk_ids: torch.Tensor, expert_range: Optional[Tuple[int, int]] = None,
-              act: str = "silu", defer_combine: bool = False):
+              act: str = "silu", defer_combine: bool = False, capturable: bool = False):
     """x [T, H]; w13 [E_local, 2I, H] ([gate; up] rows); w2 [E_local, H, I] -> [T, H].
-    ``defer_combine``: the decode path may return a ``MoECombine`` for the next add + norm."""
+    ``defer_combine``: the decode path may return a ``MoECombine`` for the next add + norm.
+    ``capturable`` (implied while a HIP graph is being captured): only the device-side grouped
+    forms, whatever the rows per expert -- the sorted-row and per-expert regimes read expert
+    offsets back to the host, which a graph cannot contain."""
     T, H = x.shape
     El = w13.shape[0]
     e_lo, e_hi = expert_range or (0, El)
@@ -179,11 +182,18 @@ def fused_moe(x: torch.Tensor, w13: torch.Tensor, w2: torch.Tensor, topk_w: torc
         tw = torch.where(keep, topk_w, torch.zeros_like(topk_w))
         return ref.fused_moe(x, w13, w2, tw, ids.clamp(0, El - 1).to(torch.int32), act)
     avg = T * k / max(1, El)
+    capturable = capturable or torch.cuda.is_current_stream_capturing()
     if act == "silu" and avg <= 96 and _grouped_ok(x, w13, w2):
         return _fused_moe_grouped(x, w13, w2, topk_w, topk_ids, e_lo, e_hi,
                                   defer_combine=defer_combine)
-    if act == "silu" and _mfma_ok(x, w13, w2) and avg <= MFMA_MAX_ROWS:
+    if act == "silu" and _mfma_ok(x, w13, w2) and (avg <= MFMA_MAX_ROWS or capturable):
         return _fused_moe_grouped(x, w13, w2, topk_w, topk_ids, e_lo, e_hi, mfma=True)
+    if capturable:
+        if act == "silu" and _grouped_ok(x, w13, w2):
+            return _fused_moe_grouped(x, w13, w2, topk_w, topk_ids, e_lo, e_hi)
+        raise RuntimeError(
+            f"fused_moe: no host-sync-free form for act={act} H={H} I={w13.shape[1] // 2} "
+            "(grouped kernels need SiLU, H % 128 == 0, I % 64 == 0); run this MoE eagerly")
     if _grouped_ok(x, w13, w2):
         return _fused_moe_sorted_blas(x, w13, w2, topk_w, topk_ids, e_lo, e_hi, act)
     return _fused_moe_per_expert(x, w13, w2, topk_w, topk_ids, e_lo, act)

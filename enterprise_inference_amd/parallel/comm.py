@@ -67,12 +67,16 @@ def all_reduce_add_rmsnorm(x: torch.Tensor, residual: torch.Tensor, weight: torc
     """(rmsnorm(residual + allreduce(x)) * w, residual) with residual updated in place.
 
     Decode-sized messages run the fused xGMI kernel (one launch, no HBM round trip of the
-    reduced tensor); otherwise RCCL all-reduce followed by the fused add+RMSNorm kernel."""
+    reduced tensor); otherwise RCCL all-reduce followed by the fused add+RMSNorm kernel.
+    ``x`` may be the row-parallel GEMM's split-K slabs (``gemm.SplitK``): the fused kernel sums
+    them while staging, so the GEMM's own reduce launch disappears."""
     from ..ops import norm
     ar = _CUSTOM_AR
     if state.tp_size() > 1 and ar is not None and ar.can_fuse_norm(x) and \
-            residual.is_contiguous() and residual.dtype == x.dtype:
+            residual.is_contiguous() and residual.dtype == torch.bfloat16:
         return ar.add_rmsnorm(x, residual, weight, eps), residual
+    if hasattr(x, "materialize"):          # split-K slabs the custom kernel cannot take
+        x = x.materialize()
     return norm.fused_add_rms_norm(all_reduce(x), residual, weight, eps)
 
 

@@ -187,24 +187,39 @@ class CustomAllReduce:
         _native.check(rc, "custom_allreduce")
         return out
 
-    def can_fuse_norm(self, x: torch.Tensor) -> bool:
+    def can_fuse_norm(self, x) -> bool:
+        """``x``: the [T, H] bf16 partial sums, or the row-parallel GEMM's split-K slabs
+        (``gemm.SplitK``, no bias) -- summed while the kernel stages them."""
+        if getattr(x, "part", None) is not None and hasattr(x, "sk"):
+            T, H = x.shape
+            return (x.bias is None and x.part.is_cuda and x.part.is_contiguous()
+                    and T * H * 2 <= self.use_max and H % 8 == 0 and H <= 16384)
         return (self.should_use(x) and x.dim() == 2 and x.shape[1] % 8 == 0
                 and x.shape[1] <= 16384)
 
-    def add_rmsnorm(self, x: torch.Tensor, residual: torch.Tensor, weight: torch.Tensor,
+    def add_rmsnorm(self, x, residual: torch.Tensor, weight: torch.Tensor,
                     eps: float, twoshot: Optional[bool] = None) -> torch.Tensor:
         """One kernel: all-reduce x over the TP group, residual += sum (in place), returns
-        rmsnorm(residual) * weight.  Bit-identical to all_reduce + fused_add_rms_norm."""
+        rmsnorm(residual) * weight.  Bit-identical to all_reduce + fused_add_rms_norm.  A
+        ``gemm.SplitK`` input is reduced over its K slabs in the same kernel (bit-identical to
+        materialising it first), so the row-parallel GEMM needs no reduce launch of its own."""
         T, H = x.shape
-        out = torch.empty_like(x)
+        out = torch.empty(T, H, dtype=residual.dtype, device=residual.device)
         if twoshot is None:
             twoshot = T * H * 2 > self.oneshot_max and T >= self.world
-        rc = self.lib.eia_ar_add_rmsnorm(ctypes.cast(self._sig_arr, ctypes.c_void_p),
-                                         ctypes.cast(self._data_arr, ctypes.c_void_p), self.rank,
-                                         self.world, x.data_ptr(), residual.data_ptr(),
-                                         weight.data_ptr(), out.data_ptr(), float(eps), T, H,
-                                         self.max_bytes, int(bool(twoshot)), self.nblocks,
-                                         torch.cuda.current_stream().cuda_stream)
+        st = torch.cuda.current_stream().cuda_stream
+        sig = ctypes.cast(self._sig_arr, ctypes.c_void_p)
+        data = ctypes.cast(self._data_arr, ctypes.c_void_p)
+        if getattr(x, "part", None) is not None and hasattr(x, "sk"):
+            rc = self.lib.eia_ar_add_rmsnorm_splitk(
+                sig, data, self.rank, self.world, x.part.data_ptr(), x.sk, residual.data_ptr(),
+                weight.data_ptr(), out.data_ptr(), float(eps), T, H, self.max_bytes,
+                int(bool(twoshot)), self.nblocks, st)
+        else:
+            rc = self.lib.eia_ar_add_rmsnorm(sig, data, self.rank, self.world, x.data_ptr(),
+                                             residual.data_ptr(), weight.data_ptr(),
+                                             out.data_ptr(), float(eps), T, H, self.max_bytes,
+                                             int(bool(twoshot)), self.nblocks, st)
         _native.check(rc, "custom_allreduce_add_rmsnorm")
         return out
 
@@ -308,6 +323,8 @@ def selftest_cases(max_bytes: int, oneshot_max: int, hidden: int = 4096):
     for T in (1, 65, 256):
         if T * hidden * 2 <= max_bytes:
             cases += [("norm", (T, hidden), 0), ("norm", (T, hidden), 1)]
+    if 65 * hidden * 2 <= max_bytes:   # the row-parallel GEMM's split-K slabs as the input
+        cases += [("norm_sk", (65, hidden), 0), ("norm_sk", (65, hidden), 1)]
     return cases
 
 
@@ -320,9 +337,17 @@ def selftest_inputs(case, rank: int, device, seed: int = 1234):
     x = torch.randint(-4, 5, shape, generator=g).to(torch.bfloat16)
     if op == "ar":
         return (x.to(device),)
+    if op == "norm_sk":      # two integer-valued fp32 slabs whose bf16 sum is x exactly
+        a = torch.randint(-2, 3, shape, generator=g).float()
+        x = (a + torch.randint(-2, 3, shape, generator=g).float()).to(torch.bfloat16)
+        part = torch.stack([a, x.float() - a])
     g2 = torch.Generator(device="cpu").manual_seed(seed + sum(shape))
     res = torch.randint(-8, 9, shape, generator=g2).to(torch.bfloat16)
     w = (1.0 + torch.rand(shape[1], generator=g2)).to(torch.bfloat16)
+    if op == "norm_sk":
+        from ..ops.gemm import SplitK
+        return x.to(device), res.to(device), w.to(device), \
+            SplitK(part.to(device), 2, shape[0], shape[1])
     return x.to(device), res.to(device), w.to(device)
 
 
@@ -351,11 +376,12 @@ def run_self_test(ar, reference, device, cases=None, eps: float = 1e-5) -> Optio
                 ok = torch.equal(got, want)
                 err = 0.0 if ok else float((got.float() - want.float()).abs().max())
             else:
-                x, res, w = t
+                x, res, w = t[:3]
                 r_want = res.clone()
                 want, r_want = norm_ops.fused_add_rms_norm(want, r_want, w, eps)
                 r_got = res.clone()
-                got = ar.add_rmsnorm(x.clone(), r_got, w, eps, twoshot=bool(kind))
+                src = t[3] if op == "norm_sk" else x.clone()
+                got = ar.add_rmsnorm(src, r_got, w, eps, twoshot=bool(kind))
                 ok = torch.equal(r_got, r_want) and bool(
                     torch.allclose(got.float(), want.float(), rtol=1e-2, atol=1e-2))
                 err = 0.0 if ok else max(float((r_got.float() - r_want.float()).abs().max()),

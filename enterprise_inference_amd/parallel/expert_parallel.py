@@ -80,8 +80,10 @@ def _moe_all_to_all_padded(x, topk_w, topk_ids, w13_local, w2_local, e_lo, e_per
     comm.all_to_all_single(recv_x, send_x, group=group)
     comm.all_to_all_single(recv_e, send_e, group=group)
     ones = torch.ones(W * capacity, 1, dtype=torch.float32, device=x.device)
+    # W * capacity rows over e_per experts can exceed the MFMA regime's rows per expert
+    # (Mixtral TP8: e_per 1) -- the padded form must stay on the device-side kernels
     y = moe_ops.fused_moe(recv_x, w13_local, w2_local, ones, recv_e[:, None],
-                          (e_lo, e_lo + e_per), act)
+                          (e_lo, e_lo + e_per), act, capturable=True)
     back = torch.empty_like(send_x)
     comm.all_to_all_single(back, y.contiguous(), group=group)
     pairs = back.index_select(0, dest).float() * topk_w.reshape(-1, 1).float()

@@ -194,7 +194,8 @@ def main():
             for cfg, sk in cands:
                 src = wg_pool(cfg) if cfg & 1024 else (wps if cfg & 64 else ws)
                 if swiglu:
-                    f = lambda i, cfg=cfg, src=src: gemm.swiglu_gemm(x, src[i % pool], cfg=cfg)
+                    f = lambda i, cfg=cfg, sk=sk, src=src: gemm.swiglu_gemm(
+                        x, src[i % pool], cfg=cfg, sk=sk)
                 else:
                     f = lambda i, cfg=cfg, sk=sk, src=src: gemm.skinny(x, src[i % pool], cfg=cfg,
                                                                        sk=sk)
@@ -212,7 +213,8 @@ def main():
                 pick = gemm.choose(M, N, K, swiglu)
                 tp = next((t for t, c, s_ in results if (c, s_) == tuple(pick)), None)
                 if tp is None and pick[0] >= 0:   # table pick outside the candidate list
-                    f = (lambda i: gemm.swiglu_gemm(x, ws[i % pool], cfg=pick[0])) if swiglu else \
+                    f = (lambda i: gemm.swiglu_gemm(x, ws[i % pool], cfg=pick[0], sk=pick[1])) \
+                        if swiglu else \
                         (lambda i: gemm.skinny(x, ws[i % pool], cfg=pick[0], sk=pick[1]))
                     tp = graph_time(f, a.iters)
                 if pick[0] < 0:

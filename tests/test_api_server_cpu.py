@@ -233,3 +233,50 @@ def test_requests_reach_engine_before_stream_iterates(monkeypatch):
     serving._start(Both(), "r3", None, None)
     assert calls == [("generate-created", "r3")]
     del g
+
+
+def test_submitted_request_released_when_stream_never_iterates():
+    """Eager submit registers the request before its output generator starts; a stream that
+    is dropped unstarted (client gone before the response body, a later prompt of the same
+    completion failing) must still abort the request in the core and forget it, and a stream
+    iterated to completion must not send an abort."""
+    import asyncio
+    import gc
+
+    from enterprise_inference_amd.engine.core_proc import MPEngineClient
+
+    class Out:
+        def __init__(self, finished):
+            self.finished = finished
+
+    async def scenario():
+        c = MPEngineClient.__new__(MPEngineClient)
+        c._reqs, c.dead, c.ready, c._last_msg = {}, None, False, 0.0
+        sent = []
+        c._send = sent.append
+
+        class W:
+            def is_closing(self):
+                return False
+        c._writer = W()
+        s = c.submit("a", None, None, prompt_token_ids=[1, 2])
+        assert "a" in c._reqs and sent[-1][0] == "add"
+        del s
+        gc.collect()
+        assert "a" not in c._reqs and sent[-1] == ("abort", "a")
+        s = c.submit("b", None, None, prompt_token_ids=[3])
+        c._reqs["b"].queue.put_nowait(Out(False))
+        c._reqs["b"].queue.put_nowait(Out(True))
+        got = [o.finished async for o in s]
+        assert got == [False, True] and "b" not in c._reqs
+        del s
+        gc.collect()
+        assert [f for f in sent if f[0] == "abort"] == [("abort", "a")]
+        s = c.submit("c", None, None, prompt_token_ids=[4])   # closed mid-stream
+        c._reqs["c"].queue.put_nowait(Out(False))
+        assert (await s.__anext__()).finished is False
+        await s.aclose()
+        assert "c" not in c._reqs and sent[-1] == ("abort", "c")
+        assert [f for f in sent if f == ("abort", "c")] == [("abort", "c")]
+
+    asyncio.run(scenario())

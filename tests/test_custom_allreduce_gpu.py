@@ -212,6 +212,43 @@ FUSED = textwrap.dedent('''
                     if not (torch.equal(rs[r], rs[0]) and torch.equal(outs[r], outs[0])):
                         print("RANKS DIFFER", H, T, twoshot, r, flush=True)
                         bad += 1
+                # the same partial sums handed over as the row-parallel GEMM's split-K slabs
+                # (fp32 [sk][T][H], summed while staging): bit-identical to the bf16 input path
+                for sk in (1, 3, 4):
+                    parts = []
+                    for r in range(world):
+                        p = torch.randn(sk, T, H, device="cuda", generator=g) * 0.01
+                        p[0] += base[r].float() - p.sum(0)       # slabs sum to ~base[r]
+                        parts.append(p.contiguous())
+                    xs2 = [torch.empty(T, H, device="cuda", dtype=torch.bfloat16) for _ in range(world)]
+                    for r in range(world):                     # what splitk_reduce would store
+                        acc = parts[r][0].clone()
+                        for q in range(1, sk):
+                            acc += parts[r][q]
+                        xs2[r] = acc.to(torch.bfloat16)
+                    rs2 = [res0.clone() for _ in range(world)]
+                    rs3 = [res0.clone() for _ in range(world)]
+                    o2 = [torch.empty(T, H, device="cuda", dtype=torch.bfloat16) for _ in range(world)]
+                    o3 = [torch.empty(T, H, device="cuda", dtype=torch.bfloat16) for _ in range(world)]
+                    torch.cuda.synchronize()
+                    for r in range(world):
+                        assert lib.eia_ar_add_rmsnorm_splitk(
+                            ctypes.cast(sig_arr, ctypes.c_void_p), ctypes.cast(data_arr, ctypes.c_void_p),
+                            r, world, parts[r].data_ptr(), sk, rs2[r].data_ptr(), w.data_ptr(),
+                            o2[r].data_ptr(), 1e-5, T, H, max_bytes, twoshot, nblocks,
+                            streams[r].cuda_stream) == 0
+                    torch.cuda.synchronize()
+                    for r in range(world):
+                        assert lib.eia_ar_add_rmsnorm(
+                            ctypes.cast(sig_arr, ctypes.c_void_p), ctypes.cast(data_arr, ctypes.c_void_p),
+                            r, world, xs2[r].data_ptr(), rs3[r].data_ptr(), w.data_ptr(),
+                            o3[r].data_ptr(), 1e-5, T, H, max_bytes, twoshot, nblocks,
+                            streams[r].cuda_stream) == 0
+                    torch.cuda.synchronize()
+                    for r in range(world):
+                        if not (torch.equal(rs2[r], rs3[r]) and torch.equal(o2[r], o3[r])):
+                            print("SPLITK DIFFERS", H, T, twoshot, sk, r, flush=True)
+                            bad += 1
     errs = []
     for sp in sigs:
         v = ctypes.c_int(0)
@@ -229,7 +266,8 @@ def test_allreduce_add_rmsnorm_multistream(tmp_path, world):
     and two-shot, T x H over decode/prefill-chunk rows and 4096..16384 hidden sizes, W ranks on
     W streams of one GPU (as the kernel test above).  Every rank must produce bit-identical
     residual/normed rows (fixed summation order) that match the fp32 reference of the unfused
-    all_reduce -> fused_add_rms_norm pair."""
+    all_reduce -> fused_add_rms_norm pair; the split-K input form (the row-parallel GEMM's
+    fp32 slabs summed while staging) must match the bf16 input form bit for bit."""
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     f = tmp_path / "fused.py"
     f.write_text(FUSED)

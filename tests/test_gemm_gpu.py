@@ -106,6 +106,35 @@ def test_swiglu_gemm(M, I, K):
             _check(gemm.swiglu_gemm(x, w, cfg=cfg), ref, f"swiglu M={M} I={I} cfg={cfg}")
 
 
+@pytest.mark.parametrize("M", [1, 33, 65, 72, 80])
+@pytest.mark.parametrize("I,K", [(3584, 8192), (1792, 16384 // 2), (14336, 4096)])
+@pytest.mark.parametrize("sk", [2, 4, 8, 16])
+def test_swiglu_gemm_split_k(M, I, K, sk):
+    """SwiGLU pairing with the K range split over workgroups (MODE_SWIGLU_SPLIT: fp32 gate / up
+    partials, finished by eia_splitk_swiglu) vs the fp32 oracle -- the Llama-70B TP8 rank's
+    gate_up (I 3584, K 8192), whose 224 whole-K pair tiles cannot fill 256 CUs.  Every
+    register-staged and workgroup-packed pairing form that is valid at this (M, sk) runs."""
+    from enterprise_inference_amd.ops import gemm
+    torch.manual_seed(M * 31 + I + sk)
+    x = torch.randn(M, K, device=DEV, dtype=BF)
+    w = (torch.randn(2 * I, K, device=DEV) * K ** -0.5).to(BF)
+    y = _ref(x, w)
+    ref = F.silu(y[:, :I]) * y[:, I:]
+    ran = 0
+    for cfg in (1, 3, 5, 7, 17, 19, 21, 23, 273):
+        if gemm.valid(2 * I, K, True, cfg, sk, M=M):
+            _check(gemm.swiglu_gemm(x, w, cfg=cfg, sk=sk), ref,
+                   f"swiglu split M={M} I={I} K={K} cfg={cfg} sk={sk}")
+            ran += 1
+    for cfg in (1024 + 1, 1024 + 3, 1024 + 17, 1024 + 19):
+        if gemm.valid(2 * I, K, True, cfg, sk, M=M):
+            wp = gemm.pack_weight_wg(w, cfg, swiglu=True)
+            _check(gemm.swiglu_gemm(x, wp, cfg=cfg, sk=sk), ref,
+                   f"packed swiglu split M={M} I={I} cfg={cfg} sk={sk}")
+            ran += 1
+    assert ran > 0
+
+
 
 
 @pytest.mark.parametrize("M,H,sk", [(1, 4096, 4), (65, 4096, 4), (65, 4096, 8), (128, 8192, 4),
@@ -127,81 +156,6 @@ def test_splitk_add_rmsnorm(M, H, sk):
     # slab summation order may differ from torch's: one bf16 ulp
     assert ((res.float() - new_res.float()).abs() <= 1e-2 * new_res.float().abs() + 1e-3).all()
     _check(out, ref, f"M={M} H={H} sk={sk}")
-
-
-def _mlp_ref(x, wgu, wd):
-    I = wd.shape[1]
-    g = x.float() @ wgu[:I].float().t()
-    u = x.float() @ wgu[I:].float().t()
-    h = (F.silu(g) * u).to(BF).float()       # the kernel hands h over in bf16
-    return h @ wd.float().t()
-
-
-@pytest.mark.parametrize("M", [1, 16, 33, 65, 80])
-@pytest.mark.parametrize("H,I", [(4096, 14336), (8192, 28672)])
-def test_mlp_fused(M, H, I, monkeypatch):
-    """Fused decode MLP (gate_up + SwiGLU producers -> split-K down consumers in one launch)
-    vs the fp32 reference; repeated launches (the counters re-arm themselves) and no consumer
-    may have hit its spin bound."""
-    from enterprise_inference_amd.ops import gemm
-    torch.manual_seed(M + I)
-    x = torch.randn(M, H, device=DEV, dtype=BF)
-    wgu = (torch.randn(2 * I, H, device=DEV) * H ** -0.5).to(BF)
-    wd = (torch.randn(H, I, device=DEV) * I ** -0.5).to(BF)
-    monkeypatch.setattr(gemm, "FUSED_MLP", True)
-    sk = gemm.mlp_fused_split(M, H, I)
-    assert sk > 0 and gemm.mlp_fused_ok(x, wgu, wd)
-    ref = _mlp_ref(x, wgu, wd)
-    for it in range(3):
-        out = gemm.mlp_fused(x, wgu, wd).materialize()
-        _check(out, ref, f"M={M} H={H} I={I} launch {it}")
-    torch.cuda.synchronize()
-    assert gemm.mlp_fused_split(M, H, I) == sk
-    assert gemm.mlp_fused_error(x.device, sk) == 0
-    assert int(gemm.mlp_sync_buffer(x.device)[:2 * sk].abs().sum()) == 0   # re-armed
-
-
-def test_mlp_fused_graph_replay():
-    """Captured once, replayed many times with new inputs: every replay matches."""
-    from enterprise_inference_amd.ops import gemm
-    M, H, I = 65, 4096, 14336
-    torch.manual_seed(5)
-    x = torch.randn(M, H, device=DEV, dtype=BF)
-    wgu = (torch.randn(2 * I, H, device=DEV) * H ** -0.5).to(BF)
-    wd = (torch.randn(H, I, device=DEV) * I ** -0.5).to(BF)
-    gemm.mlp_fused(x, wgu, wd)                       # eager first: creates the sync buffer
-    torch.cuda.synchronize()
-    g = torch.cuda.CUDAGraph()
-    s = torch.cuda.Stream()
-    s.wait_stream(torch.cuda.current_stream())
-    with torch.cuda.stream(s):
-        with torch.cuda.graph(g):
-            out = gemm.mlp_fused(x, wgu, wd).materialize()
-    torch.cuda.current_stream().wait_stream(s)
-    for it in range(4):
-        x.copy_(torch.randn(M, H, device=DEV, dtype=BF))
-        g.replay()
-        torch.cuda.synchronize()
-        _check(out, _mlp_ref(x, wgu, wd), f"replay {it}")
-    assert gemm.mlp_fused_error(x.device, gemm.mlp_fused_split(M, H, I)) == 0
-
-
-def test_llama_mlp_takes_fused_path(monkeypatch):
-    """The Llama MLP module routes a decode batch through the fused kernel at TP = 1 and the
-    result (split-K partials) matches the two-launch form."""
-    from enterprise_inference_amd.models.llama import LlamaMLP
-    from enterprise_inference_amd.ops import gemm
-    monkeypatch.setattr(gemm, "FUSED_MLP", True)
-    torch.manual_seed(9)
-    mlp = LlamaMLP(4096, 14336, "silu", BF, DEV)
-    mlp.gate_up_proj.weight.data.normal_(0, 4096 ** -0.5)
-    mlp.down_proj.weight.data.normal_(0, 14336 ** -0.5)
-    x = torch.randn(65, 4096, device=DEV, dtype=BF)
-    y = mlp(x)
-    assert isinstance(y, gemm.SplitK) and y.sk == gemm.mlp_fused_split(65, 4096, 14336)
-    two = mlp.down_proj(mlp.gate_up_proj.forward_act_and_mul(x), defer_reduce=True)
-    two = two.materialize() if isinstance(two, gemm.SplitK) else two
-    _check(y.materialize(), two.float(), "fused vs two launches")
 
 
 @pytest.mark.parametrize("M", [1, 33, 65, 80])

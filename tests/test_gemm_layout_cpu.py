@@ -28,7 +28,8 @@ def test_packed_cfgs_share_base_validity():
 
 def test_seven_wave_swiglu_cfg_rules():
     """cfg 273 (7 pair-waves per workgroup) is a SwiGLU-only, spill-bounded form: valid for
-    70B's 1792 pairs (256 workgroups) up to M = 64, never for plain or split-K GEMMs."""
+    70B's 1792 pairs (256 workgroups) up to M = 64, never for plain GEMMs; with the K range
+    split (MODE_SWIGLU_SPLIT) it covers the TP8 rank's 224 pairs as 32 x 8 = 256 workgroups."""
     from enterprise_inference_amd.ops import gemm
     assert gemm.cfg_waves(273) == 7 and gemm.cfg_rows(273) == 7 * 2 * 16
     assert 273 in gemm.CFGS
@@ -36,7 +37,9 @@ def test_seven_wave_swiglu_cfg_rules():
     assert gemm.valid(2 * 28672, 8192, True, 273, 1, M=64)
     assert not gemm.valid(2 * 28672, 8192, True, 273, 1, M=65)        # spills past 4 row tiles
     assert not gemm.valid(2 * 28672, 8192, False, 273, 1, M=35)       # SwiGLU only
-    assert not gemm.valid(2 * 28672, 8192, True, 273, 2, M=35)        # no split-K
+    assert gemm.valid(2 * 3584, 8192, True, 273, 8, M=64)             # 70B TP8: 32 x sk 8
+    assert not gemm.valid(2 * 3584, 8192, True, 273, 8, M=65)
+    assert not gemm.valid(2 * 3584, 8192, False, 273, 8, M=35)        # SwiGLU only
     assert not gemm.valid(2 * 11008, 4096, True, 273, 1, M=35)        # 688 pairs: not 7 | pairs
     assert not gemm.valid(2 * 28672, 8192, True, 257, 1, M=35)        # only the KC-128 form
     assert (28672 // 16) // 7 == 256

@@ -282,8 +282,9 @@ def test_remote_image_dns_rebinding_pinned(monkeypatch):
 
 def test_remote_image_through_egress_proxy(monkeypatch):
     """With HTTPS_PROXY set (enterprise egress), the policy check still resolves and vets the
-    name, but the request goes to the proxy by NAME with the environment trusted, and the
-    peer check (which would see the proxy's address) is skipped; NO_PROXY matches the name."""
+    name, and the PINNED target (the validated address, SNI / Host = the name) goes through
+    the proxy, so the proxy never resolves the name itself; the peer check (which would see
+    the proxy's address) is skipped; NO_PROXY matches the name."""
     import contextlib
     import socket
 
@@ -313,13 +314,22 @@ def test_remote_image_through_egress_proxy(monkeypatch):
     def fake_getaddrinfo(host, port, *a, **k):
         return [(socket.AF_INET, socket.SOCK_STREAM, 6, "", ("93.184.216.34", port))]
 
+    @contextlib.contextmanager
+    def fake_proxied(url, headers, extensions, timeout, proxy):
+        seen.update(url=url, headers=headers, ext=extensions, proxy=proxy, trust_env=None)
+        yield _Resp()
+
     monkeypatch.setattr(socket, "getaddrinfo", fake_getaddrinfo)
     monkeypatch.setattr(lv, "_open_stream", fake_stream)
+    monkeypatch.setattr(lv, "_open_proxied_stream", fake_proxied)
     monkeypatch.setenv("HTTPS_PROXY", "http://proxy.corp:3128")
     monkeypatch.delenv("NO_PROXY", raising=False)
     monkeypatch.delenv("no_proxy", raising=False)
     assert lv.fetch_image_bytes("https://img.example.com/a.png") == b"abc"
-    assert seen["url"] == "https://img.example.com/a.png" and seen["trust_env"] is True
+    assert seen["url"] == "https://93.184.216.34/a.png"
+    assert seen["ext"] == {"sni_hostname": "img.example.com"}
+    assert seen["headers"] == {"Host": "img.example.com"}
+    assert seen["proxy"] == "http://proxy.corp:3128"
     # the host is exempted by NO_PROXY: back to the pinned direct dial
     monkeypatch.setenv("NO_PROXY", "img.example.com")
     _Resp.extensions = {}
@@ -372,3 +382,48 @@ def test_slow_image_url_does_not_block_event_loop(monkeypatch):
         return ticks
 
     assert asyncio.run(main()) >= 10
+
+
+def test_http_image_via_local_proxy_dials_pinned_address(monkeypatch):
+    """End to end over a real socket: a forward proxy on 127.0.0.1 receives the absolute-form
+    request for the VALIDATED address (not the name, which it would resolve again) with the
+    name in Host, through _open_proxied_stream / http.client."""
+    import socket
+    import threading
+
+    from enterprise_inference_amd.models import llama4_vision as lv
+
+    srv = socket.socket()
+    srv.bind(("127.0.0.1", 0))
+    srv.listen(1)
+    got = {}
+
+    def serve():
+        c, _ = srv.accept()
+        data = b""
+        while b"\r\n\r\n" not in data:
+            data += c.recv(4096)
+        got["head"] = data.decode()
+        c.sendall(b"HTTP/1.1 200 OK\r\nContent-Length: 3\r\nConnection: close\r\n\r\nxyz")
+        c.close()
+
+    t = threading.Thread(target=serve, daemon=True)
+    t.start()
+    real = socket.getaddrinfo
+
+    def fake_getaddrinfo(host, port, *a, **k):
+        if host == "img.example.com":
+            return [(socket.AF_INET, socket.SOCK_STREAM, 6, "", ("93.184.216.34", port))]
+        return real(host, port, *a, **k)
+
+    monkeypatch.setattr(socket, "getaddrinfo", fake_getaddrinfo)
+    for k in ("NO_PROXY", "no_proxy", "ALL_PROXY", "all_proxy", "http_proxy"):
+        monkeypatch.delenv(k, raising=False)
+    monkeypatch.setenv("HTTP_PROXY", f"http://user:pw@127.0.0.1:{srv.getsockname()[1]}")
+    assert lv.fetch_image_bytes("http://img.example.com/a.png?x=1") == b"xyz"
+    t.join(5)
+    srv.close()
+    line, *hdrs = got["head"].split("\r\n")
+    assert line == "GET http://93.184.216.34/a.png?x=1 HTTP/1.1", line
+    assert "Host: img.example.com" in hdrs
+    assert any(h.startswith("Proxy-Authorization: Basic ") for h in hdrs)

@@ -224,6 +224,55 @@ def test_all_to_all_ep_captures_in_hip_graph(monkeypatch):
         assert err < 3e-2, (it, err)
 
 
+@pytest.mark.parametrize("W,T", [(8, 72), (4, 136)])
+def test_all_to_all_ep_large_bucket_captures(monkeypatch, W, T):
+    """TP-W all-to-all EP with one local expert per rank (Mixtral at TP 8) at a decode bucket
+    past 64 tokens: the padded receive block (W x capacity rows, all for the one local expert)
+    exceeds the MFMA regime's 128 rows per expert, which used to route fused_moe to the
+    sorted-row path and its host read-back inside the capture.  One rank stands in for rank
+    r of W (the identity exchange leaves this rank's own pairs in its block, the other
+    owners' pairs are skipped by the align kernel): replays must match the eager fused MoE
+    over the local expert."""
+    from enterprise_inference_amd.ops import moe
+    from enterprise_inference_amd.parallel import comm
+    from enterprise_inference_amd.parallel import expert_parallel as ep
+
+    monkeypatch.setattr(comm, "all_to_all_single",
+                        lambda out, inp, *a, **kw: out.copy_(inp))
+    E, k, H, I = W, 2, 1024, 1792
+    r = 1
+    per = -(-T // W)
+    cap = per * k
+    assert W * cap > moe.MFMA_MAX_ROWS
+    g = torch.Generator(device=DEV).manual_seed(1)
+    w13 = (torch.randn(1, 2 * I, H, device=DEV, generator=g) * H ** -0.5).to(BF)
+    w2 = (torch.randn(1, H, I, device=DEV, generator=g) * I ** -0.5).to(BF)
+    x = torch.randn(per, H, device=DEV).to(BF)
+    lg = torch.randn(per, E, device=DEV)
+
+    def layer():
+        w, ids = moe.topk_route(lg, k, True)
+        return ep._moe_all_to_all_padded(x, w, ids, w13, w2, r, 1, None, "silu", W, cap)
+    layer()
+    torch.cuda.synchronize()
+    graph = torch.cuda.CUDAGraph()
+    st = torch.cuda.Stream()
+    st.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(st):
+        with torch.cuda.graph(graph):
+            out = layer()
+    torch.cuda.current_stream().wait_stream(st)
+    for it in range(3):
+        x.copy_(torch.randn(per, H, device=DEV).to(BF))
+        lg.copy_(torch.randn(per, E, device=DEV))
+        graph.replay()
+        torch.cuda.synchronize()
+        w, ids = moe.topk_route(lg, k, True)
+        ref = moe.fused_moe(x, w13, w2, w, ids, (r, r + 1))
+        err = (out.float() - ref.float()).abs().max().item()
+        assert err < 3e-2, (it, err)
+
+
 @pytest.mark.parametrize("T,E,k,H,I", [(1, 8, 2, 512, 256), (33, 8, 2, 1024, 512),
                                        (65, 8, 2, 4096, 1792)])
 def test_fused_moe_wg_packed_gate_up(monkeypatch, T, E, k, H, I):
