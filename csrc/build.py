@@ -81,10 +81,20 @@ def build_kernels(force: bool = False, jobs: int = 8) -> str:
         futs = [ex.submit(_run, [HIPCC, *HIP_FLAGS, "-c", s, "-o", o]) for s, o in todo]
         for f in futs:
             f.result()
-    if force or todo or not _newer(KERNELS_SO, objs):
+    # the link also re-runs when the source SET changed (a kernel file deleted or added):
+    # the library must not keep symbols of sources that no longer exist
+    manifest = os.path.join(OBJ_DIR, "kernels.manifest")
+    want = "\n".join(os.path.basename(o) for o in objs)
+    try:
+        have = open(manifest).read()
+    except OSError:
+        have = None
+    if force or todo or have != want or not _newer(KERNELS_SO, objs):
         tmp = KERNELS_SO + ".tmp"
         _run([HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", tmp, *objs])
         os.replace(tmp, KERNELS_SO)
+        with open(manifest, "w") as f:
+            f.write(want)
     return KERNELS_SO
 
 

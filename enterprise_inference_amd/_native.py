@@ -61,7 +61,6 @@ _SIGNATURES = {
     "eia_moe_combine_sk": [P, I, I, P, P, I, I, I, P, L, S],
     "eia_moe_grouped_gemm": [P, L, IP, P, I, I, I, IP, I, I, P, L, S],
     "eia_gemm_skinny": [P, L, P, L, P, P, L, I, I, I, I, I, I, S],
-    "eia_gemm_prefill": [P, L, P, L, P, L, I, I, I, I, S],
     "eia_splitk_reduce": [P, I, I, I, P, P, L, S],
     "eia_splitk_swiglu": [P, I, I, I, P, L, S],
     "eia_splitk_add_rmsnorm": [P, I, I, I, P, P, F, P, L, S],

@@ -19,8 +19,11 @@ from __future__ import annotations
 import argparse
 import asyncio
 import base64
+import collections
+import concurrent.futures
 import logging
 import os
+import queue
 import struct
 import sys
 import threading
@@ -39,7 +42,13 @@ logger = logging.getLogger(__name__)
 
 
 class EmbeddingEngine:
-    """Batched encoder inference on one GPU (or the CPU path)."""
+    """Batched encoder inference on one GPU (or the CPU path).
+
+    Dynamic batching across requests (what TEI's router does): every request's sequences go
+    into one queue, and a single worker thread packs whatever is waiting -- from any number of
+    concurrent requests -- into varlen batches of up to ``max_batch_tokens`` (one forward
+    each), so many single-document calls share a forward instead of running one by one.  A
+    batch holds one kind of work (embedding with / without normalisation, or rerank)."""
 
     def __init__(self, cfg, max_batch_tokens: int = 16384, auto_truncate: bool = True):
         from ...models.loader import build_model
@@ -62,8 +71,10 @@ class EmbeddingEngine:
         self.max_batch_tokens = max_batch_tokens
         self.auto_truncate = auto_truncate
         self.is_reranker = m.architecture.endswith("SequenceClassification")
-        self.lock = threading.Lock()
-        self.stats = {"requests": 0, "tokens": 0}
+        self.stats = {"requests": 0, "tokens": 0, "batches": 0, "batch_seqs": 0}
+        self._q: "queue.Queue" = queue.Queue()
+        self._worker: Optional[threading.Thread] = None
+        self._worker_lock = threading.Lock()
 
     # ------------------------------------------------------------------ tokenise
     def _encode(self, text: str, pair: Optional[str] = None, truncate: bool = True):
@@ -94,21 +105,68 @@ class EmbeddingEngine:
         if batch:
             yield batch
 
-    @torch.no_grad()
-    def _run(self, encs, fn):
-        from ...models.bert import EncoderBatch
+    def _fn(self, key):
+        if key == "rerank":
+            return lambda b: self.model(b)
+        return lambda b: self.model(b, normalize=key == "embed_norm")
 
-        out = [None] * len(encs)
-        with self.lock:
-            for idx in self._batches(encs):
-                seqs = [encs[i][0] for i in idx]
-                tts = [encs[i][1] or [0] * len(encs[i][0]) for i in idx]
-                b = EncoderBatch(seqs, tts, self.device, self.cfg.model.position_offset)
-                res = fn(b).float().cpu()
-                for j, i in enumerate(idx):
-                    out[i] = res[j]
-                self.stats["tokens"] += sum(len(s) for s in seqs)
-            self.stats["requests"] += 1
+    def _ensure_worker(self) -> None:
+        with self._worker_lock:
+            if self._worker is None or not self._worker.is_alive():
+                self._worker = threading.Thread(target=self._loop, name="tei-batcher",
+                                                daemon=True)
+                self._worker.start()
+
+    def _loop(self) -> None:
+        carry: collections.deque = collections.deque()   # left for the next batch, in order
+        while True:
+            pending = list(carry)
+            carry.clear()
+            if not pending:
+                pending.append(self._q.get())
+            while True:                     # everything already waiting
+                try:
+                    pending.append(self._q.get_nowait())
+                except queue.Empty:
+                    break
+            key = pending[0][2]
+            batch, tok = [], 0
+            for item in pending:            # FIFO: one kind, up to the token budget
+                if item[2] == key and (not batch or tok + len(item[0]) <= self.max_batch_tokens):
+                    batch.append(item)
+                    tok += len(item[0])
+                else:
+                    carry.append(item)
+            self._forward(batch, key)
+
+    @torch.no_grad()
+    def _forward(self, batch, key) -> None:
+        from ...models.bert import EncoderBatch
+        try:
+            seqs = [it[0] for it in batch]
+            tts = [it[1] or [0] * len(it[0]) for it in batch]
+            b = EncoderBatch(seqs, tts, self.device, self.cfg.model.position_offset)
+            res = self._fn(key)(b).float().cpu()
+            self.stats["tokens"] += sum(len(x) for x in seqs)
+            self.stats["batches"] += 1
+            self.stats["batch_seqs"] += len(seqs)
+            for j, it in enumerate(batch):
+                it[3].set_result(res[j])
+        except Exception as e:   # noqa: BLE001 - delivered to every waiting request
+            for it in batch:
+                if not it[3].done():
+                    it[3].set_exception(e)
+
+    def _run(self, encs, key):
+        """Queue this request's sequences for the batcher and wait for their outputs."""
+        self._ensure_worker()
+        futs = []
+        for ids, tt in encs:
+            f: concurrent.futures.Future = concurrent.futures.Future()
+            self._q.put((ids, tt, key, f))
+            futs.append(f)
+        out = [f.result() for f in futs]
+        self.stats["requests"] += 1
         return out
 
     def embed(self, texts: List[str], normalize: bool = True, truncate: bool = True,
@@ -116,7 +174,7 @@ class EmbeddingEngine:
         if self.is_reranker:
             raise ValueError("this model is a reranker; use /rerank")
         encs = [self._encode(t, truncate=truncate) for t in texts]
-        vecs = self._run(encs, lambda b: self.model(b, normalize=normalize and not dimensions))
+        vecs = self._run(encs, "embed_norm" if normalize and not dimensions else "embed")
         if dimensions:
             vecs = [torch.nn.functional.normalize(v[:dimensions], dim=-1) if normalize else
                     v[:dimensions] for v in vecs]
@@ -127,7 +185,7 @@ class EmbeddingEngine:
         if not self.is_reranker:
             raise ValueError("this model is an embedding model; use /embed")
         encs = [self._encode(query, t, truncate=truncate) for t in texts]
-        logits = self._run(encs, lambda b: self.model(b))
+        logits = self._run(encs, "rerank")
         out = []
         for l in logits:
             s = float(l[0]) if l.numel() == 1 else float(torch.softmax(l, -1)[-1])
@@ -140,8 +198,7 @@ class EmbeddingEngine:
     def warmup(self, seq_len: int = 512) -> None:
         n = min(seq_len, self.max_len)
         encs = [([self.tokenizer.bos_token_id or 0] * n, None)]
-        self._run(encs, (lambda b: self.model(b)) if self.is_reranker else
-                  (lambda b: self.model(b, normalize=True)))
+        self._run(encs, "rerank" if self.is_reranker else "embed_norm")
 
 
 class EmbedRequest(BaseModel):

@@ -85,17 +85,13 @@ class MergedColumnParallelLinear(ColumnParallelLinear):
         """act(x Wg^T) * (x Wu^T) for a [gate; up] merged projection.
 
         Decode-sized batches run the fused SwiGLU GEMM (K7: the 2I-wide
-        intermediate never reaches HBM); larger ones hipBLASLt + the K7 kernel.
+        intermediate never reaches HBM); prompt-sized ones hipBLASLt (TunableOp picks, 1.5-1.6
+        PFLOP/s) + the act_and_mul kernel -- a hand MFMA form with the epilogue fused reached
+        1.2 PFLOP/s and lost in the prefill step, so it was removed (docs/performance.md).
         """
         if act == "silu" and self.bias is None and len(self.out_sizes) == 2 and \
                 x.dim() == 2 and gemm.skinny_ok(x, self.weight, swiglu=True):
             return gemm.swiglu_gemm(x, self.weight)
-        if (gemm.PREFILL_SWIGLU and act == "silu" and self.bias is None
-                and len(self.out_sizes) == 2 and x.dim() == 2
-                and x.shape[0] >= gemm.PREFILL_MIN_M
-                and gemm.prefill_gemm_ok(x, self.weight, swiglu=True)):
-            # prompt-sized: the SwiGLU epilogue inside the MFMA GEMM (gemm_prefill.hip)
-            return gemm.prefill_gemm(x, self.weight, swiglu=True)
         from ..ops import activation
         return activation.act_and_mul(gemm.linear(x, self.weight, self.bias), act)
 

@@ -506,39 +506,6 @@ def linear(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = None
     return F.linear(x, w, bias)
 
 
-# --------------------------------------------------------------------------- prefill K7
-# Prompt-sized gate_up with the SwiGLU epilogue in the GEMM (csrc/kernels/gemm_prefill.hip):
-# the [T, 2I] intermediate never reaches HBM and act_and_mul disappears.  Opt-in
-# (EIA_PREFILL_SWIGLU=1): at ~1.2 PFLOP/s it trails hipBLASLt's tuned 1.56 + the separate
-# act_and_mul pass in the engine's prefill step (docs/performance.md, "Prefill SwiGLU (K7)").
-PREFILL_SWIGLU = os.environ.get("EIA_PREFILL_SWIGLU", "0") == "1"
-PREFILL_MIN_M = int(os.environ.get("EIA_PREFILL_SWIGLU_MIN_M", "256"))
-
-
-def prefill_gemm_ok(x: torch.Tensor, w: torch.Tensor, swiglu: bool) -> bool:
-    if DISABLE or not use_hip(x, w) or x.dim() != 2 or x.dtype != torch.bfloat16 or \
-            w.dtype != torch.bfloat16:
-        return False
-    M, K = x.shape
-    N = w.shape[0]
-    if w.shape[1] != K or K % 32 or x.stride(1) != 1 or w.stride(1) != 1 or x.stride(0) % 8 or \
-            w.stride(0) % 8:
-        return False
-    return (N % 2 == 0 and (N // 2) % 128 == 0) if swiglu else N % 256 == 0
-
-
-def prefill_gemm(x: torch.Tensor, w: torch.Tensor, swiglu: bool = False) -> torch.Tensor:
-    """x [M, K] @ w[N, K]^T on the prompt-sized MFMA kernel; swiglu: w = [gate; up] (N = 2I)
-    -> silu(x Wg^T) * (x Wu^T) [M, I]."""
-    M, K = x.shape
-    N = w.shape[0]
-    out = torch.empty(M, N // 2 if swiglu else N, dtype=torch.bfloat16, device=x.device)
-    check(lib().eia_gemm_prefill(ptr(x), x.stride(0), ptr(w), w.stride(0), ptr(out),
-                                 out.stride(0), M, N, K, MODE_SWIGLU if swiglu else MODE_BF16,
-                                 stream(x)), "gemm_prefill")
-    return out
-
-
 def splitk_add_rmsnorm(s: SplitK, residual: torch.Tensor, weight: torch.Tensor, eps: float):
     """residual += reduce(s) (+bias); returns (rmsnorm(residual) * weight, residual)."""
     if s.bias is not None:

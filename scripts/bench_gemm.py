@@ -59,6 +59,12 @@ SHAPES = {  # name: (N, K, swiglu)
     "qkv_falcon3_7b": (5120, 3072, False), "o_falcon3_7b": (3072, 3072, False),
     "gate_up_falcon3_7b": (46080, 3072, True), "down_falcon3_7b": (3072, 23040, False),
     "lm_head_falcon3_7b": (131072, 3072, False),
+    # Llama-4-Scout-17B-16E on one GPU (reference deploy-inference-models.yml:821-891): the
+    # attention projections, the shared expert and the 202k-row LM head (routed experts run
+    # the grouped MoE kernels)
+    "qkv_scout": (7168, 5120, False), "o_scout": (5120, 5120, False),
+    "shared_gate_up_scout": (16384, 5120, True), "shared_down_scout": (5120, 8192, False),
+    "lm_head_scout": (202048, 5120, False),
     # gate_up grid-size probes (8B K): 196 / 224 (the real shape) / 256 four-pair workgroups
     "gu_probe_196": (25088, 4096, True), "gu_probe_256": (32768, 4096, True),
 }

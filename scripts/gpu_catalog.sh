@@ -1,0 +1,35 @@
+#!/bin/bash
+# Rest-of-catalog measurements on one MI355X: decode-GEMM tables for Llama-4-Scout's dense
+# shapes, endpoint chatbot rows (65 users, 128/128) for Llama-4-Scout-17B-16E and Mistral-7B,
+# TEI embedding / rerank throughput, and the TP8-rank GEMM sweep.  Steps by name; the first
+# failure ends the script (no retries).
+set -o pipefail
+R=${GRAFT_REPO_ROOT:-$(pwd)}
+cd "$R"
+mkdir -p gpurun_out
+export PYTHONUNBUFFERED=1
+STEPS=${*:-tune_scout scout mistral tei}
+run() {  # name timeout cmd...
+  local name=$1 t=$2; shift 2
+  echo "== $name: $*"
+  timeout -k 10 "$t" "$@" > "gpurun_out/$name.log" 2>&1
+  local rc=$?
+  tail -3 "gpurun_out/$name.log" | cut -c1-400
+  if [[ $rc != 0 ]]; then echo "$name rc=$rc"; exit $rc; fi
+}
+for s in $STEPS; do
+  case $s in
+    tune_scout) run tune_scout 900 python scripts/bench_gemm.py --tune --m ${SCOUT_M:-33 40 48 65 72 80} \
+                  --shapes qkv_scout o_scout shared_gate_up_scout shared_down_scout lm_head_scout \
+                  --out gpurun_out/gemm_tuning.json ;;
+    scout) run endpoint_scout 1100 python bench.py --model llama-4-scout-17b --steps 2 --warmup 1 \
+             --extras off --verbose ;;
+    mistral) run endpoint_mistral 600 python bench.py --model mistral-7b --steps 3 --warmup 1 \
+               --verbose ;;
+    tei) run tei 900 python scripts/bench_tei.py --window ${TEI_WINDOW:-10} --out gpurun_out/tei.md ;;
+    sweep_tp8) run sweep_tp8 900 python scripts/bench_gemm.py --sweep --all --m ${GEMM_M:-65} \
+                 --shapes qkv_70b_tp8 o_70b_tp8 gate_up_70b_tp8 down_70b_tp8 ;;
+    *) echo "unknown step $s"; exit 2 ;;
+  esac
+done
+exit 0

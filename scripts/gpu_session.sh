@@ -51,6 +51,7 @@ for s in $STEPS; do
     sizing70) run sizing_70b 1100 python scripts/sizing_sweep.py --model 70b --timeout 600 \
             --cases ${SIZING70_CASES:-chatbot describe translate} --out gpurun_out/sizing_70b_tp1.md ;;
     probe) run probe 300 python scripts/probe_overlap.py ;;
+    tei) run tei 900 python scripts/bench_tei.py --window ${TEI_WINDOW:-10} --out gpurun_out/tei.md ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac
 done

@@ -59,6 +59,8 @@ class _GlooAR:
 
     def add_rmsnorm(self, x, residual, weight, eps, twoshot=None):
         from enterprise_inference_amd.ops import norm
+        if hasattr(x, "materialize"):   # split-K slabs: the real kernel sums them while staging
+            x = x.materialize()
         s = self.all_reduce(x)
         out, _ = norm.fused_add_rms_norm(s, residual, weight, eps)
         return out
@@ -134,7 +136,13 @@ def test_self_test_agreed_fallback(world, bad):
 def test_self_test_cases_are_exact_and_cover_both_forms():
     cases = cam.selftest_cases(16 << 20, 512 << 10)
     kinds = {(op, kind) for op, _, kind in cases}
-    assert kinds == {("ar", 0), ("ar", 1), ("norm", 0), ("norm", 1)}
+    assert kinds == {("ar", 0), ("ar", 1), ("norm", 0), ("norm", 1), ("norm_sk", 0),
+                     ("norm_sk", 1)}
+    # the split-K input: two integer fp32 slabs whose sum is the bf16 x exactly
+    case = next(c for c in cases if c[0] == "norm_sk")
+    x, _, _, sk = cam.selftest_inputs(case, 3, "cpu")
+    assert sk.sk == 2 and torch.equal(sk.part.sum(0).to(torch.bfloat16), x)
+    assert torch.equal(sk.materialize(), x)
     assert len({shape for op, shape, _ in cases if op == "ar"}) == 3
     # integer inputs: the sum over 8 ranks is exact in bf16
     for case in cases[:2]:

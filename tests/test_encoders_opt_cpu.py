@@ -103,3 +103,52 @@ def test_opt_matches_transformers():
         ids = torch.tensor([prompt])
         ref = hf.generate(ids, max_new_tokens=8, do_sample=False)[0, len(prompt):].tolist()
     assert out[0].outputs[0].token_ids == ref
+
+
+def test_tei_dynamic_batching_across_requests():
+    """Concurrent single-document requests share forwards (TEI-style dynamic batching): the
+    batcher packs what is waiting into one varlen batch up to max_batch_tokens, kinds never
+    mix, and every request gets exactly its own rows back."""
+    import threading
+
+    import torch
+
+    from enterprise_inference_amd.config import EngineConfig, ModelConfig
+    from enterprise_inference_amd.entrypoints.tei.server import EmbeddingEngine
+    from enterprise_inference_amd.models import catalog
+
+    d = catalog.get_preset("BAAI/bge-base-en-v1.5")
+    d.update(num_hidden_layers=2, hidden_size=64, intermediate_size=128, num_attention_heads=4)
+    cfg = EngineConfig(model=ModelConfig.from_hf_dict(d, name="m"), device="cpu",
+                       dtype=torch.float32, served_model_name="m", load_format="dummy")
+    eng = EmbeddingEngine(cfg, max_batch_tokens=256)
+    texts = [f"document number {i} " * (1 + i % 5) for i in range(24)]
+    solo = [eng.embed([t])[0] for t in texts]             # one request at a time
+    b0 = eng.stats["batches"]
+    gate = threading.Event()
+    res = [None] * len(texts)
+    orig = eng._forward
+
+    def slow_forward(batch, key):                           # first forward holds the worker
+        gate.wait(5)
+        orig(batch, key)
+    eng._forward = slow_forward
+
+    def one(i):
+        res[i] = eng.embed([texts[i]], normalize=(i % 3 != 0))[0]
+    th = [threading.Thread(target=one, args=(i,)) for i in range(len(texts))]
+    for t in th:
+        t.start()
+    import time
+    time.sleep(0.3)
+    gate.set()
+    for t in th:
+        t.join(30)
+    nb = eng.stats["batches"] - b0
+    assert nb < len(texts) // 2, nb                         # requests shared forwards
+    for i, t in enumerate(texts):
+        want = torch.tensor(solo[i])
+        got = torch.tensor(res[i])
+        if i % 3 == 0:                                      # the unnormalised kind
+            got = torch.nn.functional.normalize(got, dim=-1)
+        assert torch.allclose(got, want, atol=1e-4), i

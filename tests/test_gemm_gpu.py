@@ -187,50 +187,3 @@ def test_skinny_wg_packed(M, N, K, swiglu):
             _check(out, ref, f"M={M} N={N} K={K} cfg={cfg} sk={sk}")
             n += 1
     assert n > 0
-
-
-@pytest.mark.parametrize("M", [256, 300, 2048, 8192])
-@pytest.mark.parametrize("K,I", [(4096, 1024), (512, 128)])
-def test_prefill_swiglu_gemm_vs_fp32(M, K, I):
-    """K7 at prompt sizes (gemm_prefill.hip): silu(x Wg^T) * (x Wu^T) from the MFMA kernel with
-    the epilogue in registers vs the fp32 oracle, incl. a token count off the 256-row tile."""
-    from enterprise_inference_amd.ops import gemm
-    torch.manual_seed(M + K)
-    x = torch.randn(M, K, device=DEV, dtype=BF)
-    w = (torch.randn(2 * I, K, device=DEV) * K ** -0.5).to(BF)
-    out = gemm.prefill_gemm(x, w, swiglu=True)
-    xf, wf = x.float(), w.float()
-    ref = F.silu(xf @ wf[:I].t()) * (xf @ wf[I:].t())
-    _check(out, ref, f"prefill swiglu M={M} K={K} I={I}")
-
-
-@pytest.mark.parametrize("M,N,K", [(256, 256, 64), (1000, 1024, 4096), (2048, 4096, 4096)])
-def test_prefill_plain_gemm_vs_fp32(M, N, K):
-    from enterprise_inference_amd.ops import gemm
-    torch.manual_seed(N + K)
-    x = torch.randn(M, K, device=DEV, dtype=BF)
-    w = (torch.randn(N, K, device=DEV) * K ** -0.5).to(BF)
-    out = gemm.prefill_gemm(x, w)
-    _check(out, x.float() @ w.float().t(), f"prefill M={M} N={N} K={K}")
-
-
-def test_prefill_swiglu_mlp_path(monkeypatch):
-    """The merged gate_up layer routes prompt-sized batches to the fused kernel when enabled
-    and matches the hipBLASLt + act_and_mul path."""
-    from enterprise_inference_amd.models import layers as L
-    from enterprise_inference_amd.ops import gemm
-    torch.manual_seed(5)
-    lin = L.MergedColumnParallelLinear(1024, [512, 512], dtype=BF, device=DEV)
-    with torch.no_grad():
-        lin.weight.copy_(torch.randn_like(lin.weight) * 0.03)
-    x = torch.randn(512, 1024, device=DEV, dtype=BF)
-    monkeypatch.setattr(gemm, "PREFILL_SWIGLU", False)
-    ref = lin.forward_act_and_mul(x)
-    monkeypatch.setattr(gemm, "PREFILL_SWIGLU", True)
-    calls = []
-    orig = gemm.prefill_gemm
-    monkeypatch.setattr(gemm, "prefill_gemm", lambda *a, **k: calls.append(1) or orig(*a, **k))
-    out = lin.forward_act_and_mul(x)
-    assert calls, "prefill SwiGLU kernel not used"
-    d = (out.float() - ref.float()).abs().max().item()
-    assert d <= 2e-2 * ref.float().abs().max().item() + 1e-2, d
