@@ -522,7 +522,11 @@ def init_custom_allreduce(max_bytes: int, factory=None, reference=None, agree=No
         ar.oneshot_max, ar.use_max = info["oneshot_max"], info["use_max"]
         logger.info("custom all-reduce tuned: one-shot <= %d B, custom <= %d B (RCCL above)",
                     ar.oneshot_max, ar.use_max)
+    # decode_epilogue: how a TP decode layer's row-parallel output reaches the next norm --
+    # the skinny GEMM's split-K slabs (or its bf16 tile) go straight into ONE kernel that
+    # stages them (summing the slabs), all-reduces over xGMI, adds the residual and normalises
     STATUS = {"active": True, "reason": "ok", "oneshot_max": ar.oneshot_max,
-              "use_max": ar.use_max, **({"tuning": info} if info else {})}
+              "use_max": ar.use_max, "decode_epilogue": "splitk+allreduce+add+rmsnorm, 1 launch",
+              **({"tuning": info} if info else {})}
     comm.set_custom_allreduce(ar)
     return ar

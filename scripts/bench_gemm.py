@@ -6,6 +6,11 @@ the number) with weights rotating through a pool larger than the 256 MiB Infinit
 Cache, so each call streams its weights from HBM.  Variants are timed in
 interleaved rounds in one process (guide §5.4 rule 24).
 
+  Projections are timed together with what consumes them in the decode step (consumer_of):
+  an o/down GEMM with its add + RMSNorm (which sums split-K slabs itself), a QKV GEMM without
+  a reduce (attention sums its slabs) -- a separate reduce launch would bias the table against
+  split-K.  --no-consumer times the bare op with its reduce.
+
   --tune  sweeps (cfg, split-K) per (M-tile bucket, N, K) and writes the winners to
           enterprise_inference_amd/ops/gemm_tuning.json (read by ops/gemm.py).  Several --m
           values in one 16-row bucket are scored together: the bucket's pick is the variant with
@@ -68,6 +73,22 @@ SHAPES = {  # name: (N, K, swiglu)
     # gate_up grid-size probes (8B K): 196 / 224 (the real shape) / 256 four-pair workgroups
     "gu_probe_196": (25088, 4096, True), "gu_probe_256": (32768, 4096, True),
 }
+
+
+def consumer_of(name: str) -> str:
+    """What consumes this projection's output in the decode step, so the tuner times the pair
+    the engine runs instead of charging split-K variants a reduce launch the engine never makes:
+      "norm"   o / down projections: the split-K slabs (or the bf16 tile) go straight into the
+               residual add + RMSNorm kernel (splitk_add_rmsnorm / fused_add_rms_norm; at TP > 1
+               the fused all-reduce kernel, which stages them the same way);
+      "defer"  QKV: the slabs are summed in the decode attention's fused prologue (its cost per
+               slab is small and paid by attention, not timed here);
+      "plain"  everything else (LM head, SwiGLU): the op as the engine calls it."""
+    if name.startswith(("o_", "down_", "shared_down")):
+        return "norm"
+    if name.startswith("qkv_"):
+        return "defer"
+    return "plain"
 
 
 def graph_time(fn, iters, rounds=3):
@@ -137,6 +158,9 @@ def main():
     ap.add_argument("--shapes", nargs="+", default=list(SHAPES))
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--tune", action="store_true")
+    ap.add_argument("--consumer", action=argparse.BooleanOptionalAction, default=True,
+                    help="time each projection with its decode-step consumer (consumer_of): "
+                         "o/down + add+RMSNorm, QKV with the slabs left to attention")
     ap.add_argument("--sweep", action="store_true", help="time every candidate (no table write)")
     ap.add_argument("--check", action="store_true",
                     help="sweep, and report the tuning table's pick against the best (regret) at "
@@ -175,6 +199,25 @@ def main():
                 base = lambda i: (lambda y: F.silu(y[:, :I]) * y[:, I:])(F.linear(x, ws[i % pool]))
             else:
                 base = lambda i: F.linear(x, ws[i % pool])
+            cons = consumer_of(name) if a.consumer else "plain"
+            if cons == "norm":
+                from enterprise_inference_amd.ops import norm as norm_ops
+                res = torch.randn(M, N, device="cuda", dtype=torch.bfloat16) * 0.1
+                wn = torch.ones(N, device="cuda", dtype=torch.bfloat16)
+                base = lambda i: norm_ops.fused_add_rms_norm(F.linear(x, ws[i % pool]), res, wn,
+                                                             1e-5)
+
+                def skinny_call(i, cfg, sk, src):
+                    y = gemm.skinny(x, src[i % pool], cfg=cfg, sk=sk, defer_reduce=True)
+                    if isinstance(y, gemm.SplitK):
+                        return gemm.splitk_add_rmsnorm(y, res, wn, 1e-5)
+                    return norm_ops.fused_add_rms_norm(y, res, wn, 1e-5)
+            elif cons == "defer":
+                def skinny_call(i, cfg, sk, src):
+                    return gemm.skinny(x, src[i % pool], cfg=cfg, sk=sk, defer_reduce=True)
+            else:
+                def skinny_call(i, cfg, sk, src):
+                    return gemm.skinny(x, src[i % pool], cfg=cfg, sk=sk)
             tb = graph_time(base, a.iters)
             cands = candidates(M, N, K, swiglu) if (a.tune or a.sweep or a.check) else \
                 [c for c in [gemm.choose(M, N, K, swiglu)] if c[0] >= 0]
@@ -203,8 +246,7 @@ def main():
                     f = lambda i, cfg=cfg, sk=sk, src=src: gemm.swiglu_gemm(
                         x, src[i % pool], cfg=cfg, sk=sk)
                 else:
-                    f = lambda i, cfg=cfg, sk=sk, src=src: gemm.skinny(x, src[i % pool], cfg=cfg,
-                                                                       sk=sk)
+                    f = lambda i, cfg=cfg, sk=sk, src=src: skinny_call(i, cfg, sk, src)
                 results.append((graph_time(f, a.iters), cfg, sk))
             results.sort(key=lambda r_: r_[0])
             to, cfg, sk = results[0]
@@ -221,7 +263,7 @@ def main():
                 if tp is None and pick[0] >= 0:   # table pick outside the candidate list
                     f = (lambda i: gemm.swiglu_gemm(x, ws[i % pool], cfg=pick[0], sk=pick[1])) \
                         if swiglu else \
-                        (lambda i: gemm.skinny(x, ws[i % pool], cfg=pick[0], sk=pick[1]))
+                        (lambda i: skinny_call(i, pick[0], pick[1], ws))
                     tp = graph_time(f, a.iters)
                 if pick[0] < 0:
                     tp = tb

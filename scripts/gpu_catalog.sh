@@ -27,6 +27,27 @@ for s in $STEPS; do
     mistral) run endpoint_mistral 600 python bench.py --model mistral-7b --steps 3 --warmup 1 \
                --verbose ;;
     tei) run tei 900 python scripts/bench_tei.py --window ${TEI_WINDOW:-10} --out gpurun_out/tei.md ;;
+    tune_tp8) run tune_tp8 900 python scripts/bench_gemm.py --tune --m ${TP8_M:-33 40 48 65 72 80} \
+                --shapes qkv_70b_tp8 o_70b_tp8 gate_up_70b_tp8 down_70b_tp8 \
+                --out gpurun_out/gemm_tuning.json ;;
+    tune_tp8_wg) run tune_tp8_wg 900 python scripts/bench_gemm.py --tune --wgpack \
+                   --m ${TP8_M:-33 40 48 65 72 80} \
+                   --shapes qkv_70b_tp8 o_70b_tp8 gate_up_70b_tp8 down_70b_tp8 \
+                   --out gpurun_out/gemm_tuning.json ;;
+    retune) cp enterprise_inference_amd/ops/gemm_tuning.json gpurun_out/table_before.json
+            run retune 900 python scripts/bench_gemm.py --tune --m ${RT_M:-33 40 48 65 72 80} \
+              --shapes ${RT_SHAPES:-qkv_8b o_8b down_8b qkv_70b_tp8 o_70b_tp8 down_70b_tp8} \
+              --out gpurun_out/gemm_tuning.json
+            run retune_wg 900 python scripts/bench_gemm.py --tune --wgpack --m ${RT_M:-33 40 48 65 72 80} \
+              --shapes ${RT_SHAPES:-qkv_8b o_8b down_8b qkv_70b_tp8 o_70b_tp8 down_70b_tp8} \
+              --out gpurun_out/gemm_tuning.json
+            cp enterprise_inference_amd/ops/gemm_tuning.json gpurun_out/table_after.json ;;
+    abtable)   # engine loop, headline config, table before / after the re-tune, alternating
+      for t in before after before after; do
+        EIA_GEMM_TUNING=$R/gpurun_out/table_$t.json timeout -k 10 600 python bench.py --mode engine \
+          --steps 3 --warmup 1 > gpurun_out/abtable_$t.log 2>&1 || { tail -20 gpurun_out/abtable_$t.log; exit 1; }
+        echo "table=$t $(grep -o '"value": [0-9.]*\|"tpot_p50_ms": [0-9.]*' gpurun_out/abtable_$t.log | tr '\n' ' ')"
+      done ;;
     sweep_tp8) run sweep_tp8 900 python scripts/bench_gemm.py --sweep --all --m ${GEMM_M:-65} \
                  --shapes qkv_70b_tp8 o_70b_tp8 gate_up_70b_tp8 down_70b_tp8 ;;
     *) echo "unknown step $s"; exit 2 ;;

@@ -24,6 +24,8 @@ for s in $STEPS; do
     steps65) MODEL=llama-70b-tp8-rank TAG=tp8rank_65 LIMIT=600 bash scripts/gpu_model_steps.sh || exit 1 ;;
     steps35) MODEL=llama-70b-tp8-rank TAG=tp8rank_35 LIMIT=600 BENCH_ARGS="--users 35" \
                bash scripts/gpu_model_steps.sh || exit 1 ;;
+    p2|p4) EIA_DECODE_P=${s#p} MODEL=llama-70b-tp8-rank TAG=tp8rank_65_$s LIMIT=600 \
+             bash scripts/gpu_model_steps.sh || exit 1 ;;
     sweep) run sweep_tp8 900 python scripts/bench_gemm.py --sweep --all --m ${GEMM_M:-65} \
              --shapes ${GEMM_SHAPES:-qkv_70b_tp8 o_70b_tp8 gate_up_70b_tp8 down_70b_tp8 lm_head_70b_tp8} ;;
     *) echo "unknown step $s"; exit 2 ;;

@@ -130,6 +130,53 @@ MULTISTREAM = textwrap.dedent('''
                 if err > 0.06 * world:
                     print("MISMATCH", it, n, r, err, flush=True)
                     bad += 1
+    # the split-K form under HIP-graph replay (how the TP decode step runs it): every rank's
+    # launch captured once on its own stream, replayed with fresh slabs, vs the bf16 form
+    T, H, sk = 65, 8192, 4
+    g = torch.Generator(device="cuda").manual_seed(77)
+    parts = [torch.zeros(sk, T, H, device="cuda") for _ in range(world)]
+    rs = [torch.zeros(T, H, device="cuda", dtype=torch.bfloat16) for _ in range(world)]
+    os_ = [torch.empty(T, H, device="cuda", dtype=torch.bfloat16) for _ in range(world)]
+    w = (1.0 + 0.1 * torch.randn(H, device="cuda", generator=g)).to(torch.bfloat16)
+    graphs = []
+    torch.cuda.synchronize()
+    for r in range(world):
+        gr = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(gr, stream=streams[r]):
+            assert lib.eia_ar_add_rmsnorm_splitk(
+                ctypes.cast(sig_arr, ctypes.c_void_p), ctypes.cast(data_arr, ctypes.c_void_p),
+                r, world, parts[r].data_ptr(), sk, rs[r].data_ptr(), w.data_ptr(),
+                os_[r].data_ptr(), 1e-5, T, H, max_bytes, 0, nblocks,
+                streams[r].cuda_stream) == 0
+        graphs.append(gr)
+    for it in range(6):
+        res0 = torch.randn(T, H, device="cuda", generator=g).to(torch.bfloat16)
+        for r in range(world):
+            parts[r].copy_(torch.randn(sk, T, H, device="cuda", generator=g) * 0.3)
+            rs[r].copy_(res0)
+        torch.cuda.synchronize()
+        for r in range(world):
+            with torch.cuda.stream(streams[r]):
+                graphs[r].replay()
+        torch.cuda.synchronize()
+        xs2 = []
+        for r in range(world):
+            acc = parts[r][0].clone()
+            for q in range(1, sk):
+                acc += parts[r][q]
+            xs2.append(acc.to(torch.bfloat16))
+        rs3 = [res0.clone() for _ in range(world)]
+        o3 = [torch.empty(T, H, device="cuda", dtype=torch.bfloat16) for _ in range(world)]
+        for r in range(world):
+            assert lib.eia_ar_add_rmsnorm(
+                ctypes.cast(sig_arr, ctypes.c_void_p), ctypes.cast(data_arr, ctypes.c_void_p),
+                r, world, xs2[r].data_ptr(), rs3[r].data_ptr(), w.data_ptr(),
+                o3[r].data_ptr(), 1e-5, T, H, max_bytes, 0, nblocks, streams[r].cuda_stream) == 0
+        torch.cuda.synchronize()
+        for r in range(world):
+            if not (torch.equal(rs[r], rs3[r]) and torch.equal(os_[r], o3[r])):
+                print("GRAPH SPLITK DIFFERS", it, r, flush=True)
+                bad += 1
     errs = []
     for sp in sigs:
         v = ctypes.c_int(0)
@@ -249,6 +296,53 @@ FUSED = textwrap.dedent('''
                         if not (torch.equal(rs2[r], rs3[r]) and torch.equal(o2[r], o3[r])):
                             print("SPLITK DIFFERS", H, T, twoshot, sk, r, flush=True)
                             bad += 1
+    # the split-K form under HIP-graph replay (how the TP decode step runs it): every rank's
+    # launch captured once on its own stream, replayed with fresh slabs, vs the bf16 form
+    T, H, sk = 65, 8192, 4
+    g = torch.Generator(device="cuda").manual_seed(77)
+    parts = [torch.zeros(sk, T, H, device="cuda") for _ in range(world)]
+    rs = [torch.zeros(T, H, device="cuda", dtype=torch.bfloat16) for _ in range(world)]
+    os_ = [torch.empty(T, H, device="cuda", dtype=torch.bfloat16) for _ in range(world)]
+    w = (1.0 + 0.1 * torch.randn(H, device="cuda", generator=g)).to(torch.bfloat16)
+    graphs = []
+    torch.cuda.synchronize()
+    for r in range(world):
+        gr = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(gr, stream=streams[r]):
+            assert lib.eia_ar_add_rmsnorm_splitk(
+                ctypes.cast(sig_arr, ctypes.c_void_p), ctypes.cast(data_arr, ctypes.c_void_p),
+                r, world, parts[r].data_ptr(), sk, rs[r].data_ptr(), w.data_ptr(),
+                os_[r].data_ptr(), 1e-5, T, H, max_bytes, 0, nblocks,
+                streams[r].cuda_stream) == 0
+        graphs.append(gr)
+    for it in range(6):
+        res0 = torch.randn(T, H, device="cuda", generator=g).to(torch.bfloat16)
+        for r in range(world):
+            parts[r].copy_(torch.randn(sk, T, H, device="cuda", generator=g) * 0.3)
+            rs[r].copy_(res0)
+        torch.cuda.synchronize()
+        for r in range(world):
+            with torch.cuda.stream(streams[r]):
+                graphs[r].replay()
+        torch.cuda.synchronize()
+        xs2 = []
+        for r in range(world):
+            acc = parts[r][0].clone()
+            for q in range(1, sk):
+                acc += parts[r][q]
+            xs2.append(acc.to(torch.bfloat16))
+        rs3 = [res0.clone() for _ in range(world)]
+        o3 = [torch.empty(T, H, device="cuda", dtype=torch.bfloat16) for _ in range(world)]
+        for r in range(world):
+            assert lib.eia_ar_add_rmsnorm(
+                ctypes.cast(sig_arr, ctypes.c_void_p), ctypes.cast(data_arr, ctypes.c_void_p),
+                r, world, xs2[r].data_ptr(), rs3[r].data_ptr(), w.data_ptr(),
+                o3[r].data_ptr(), 1e-5, T, H, max_bytes, 0, nblocks, streams[r].cuda_stream) == 0
+        torch.cuda.synchronize()
+        for r in range(world):
+            if not (torch.equal(rs[r], rs3[r]) and torch.equal(os_[r], o3[r])):
+                print("GRAPH SPLITK DIFFERS", it, r, flush=True)
+                bad += 1
     errs = []
     for sp in sigs:
         v = ctypes.c_int(0)
