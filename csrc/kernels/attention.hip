@@ -527,35 +527,45 @@ paged_decode_kernel(const bf16_t* __restrict__ q, long q_stride,
   // until the unit loop ends -- where the RoPE lanes sum them in slab order.  One lane per
   // 16-element row slice loading all sk slabs itself held 64 VGPRs of slab data and spilled
   // at the 3-workgroups-per-CU budget.  Shapes whose slabs exceed the staging capacity sum
-  // them per lane, one round trip per slab.
+  // them per lane, one round trip per slab.  Slab sets larger than one JS x 256 pass (a TP8
+  // rank of a 70B: 8 q heads + k + v per KV head, split-K 4 = 1280 float4) are staged in
+  // passes of 1024 float4 -- one more round trip per pass, not one per slab.
   constexpr int JS = 4;
   const int nh = nq + 2;
   const int n4 = SPLIT ? rope.src.sk * nh * (D / 4) : 0;
-  const bool staged = SPLIT && n4 <= JS * 256 && n4 * 4 <= NW * D * 17;
+  const bool staged = SPLIT && n4 * 4 <= NW * D * 17;
   f32x4 sv[JS];
   float* stage = &so[0][0][0];
   RopeLane<D, true, QK_NORM, HAS_BIAS, SPLIT ? ROPE_SRC_CALLER : ROPE_SRC_BF16> rl;
   int slot = -1;
   const int ntot = Hq + 2 * Hkv;
   auto head_of = [&](int r) { return r < nq ? hq0 + r : (r == nq ? Hq + kvh : Hq + Hkv + kvh); };
-  auto pro_issue = [&]() {
-    if (staged) {
-      // float4 f = row (f / (D/4)) of the [sk][nh] row list, column f % (D/4); the row's
-      // (slab, head) split uses a float reciprocal (exact for these small integers) instead
-      // of a ~40-instruction integer division per float4
-      const float inv_nh = 1.f / (float)nh;
+  const float inv_nh = 1.f / (float)nh;
+  // float4 f = row (f / (D/4)) of the [sk][nh] row list, column f % (D/4); the row's (slab,
+  // head) split uses a float reciprocal (exact for these small integers) instead of a
+  // ~40-instruction integer division per float4
+  auto slab_src = [&](int f) {
+    const int rr = f / (D / 4);
+    const int k = (int)(((float)rr + 0.5f) * inv_nh);
+    return rope.src.part + (long)k * rope.src.slab + (long)b * ntot * D +
+           (long)head_of(rr - k * nh) * D + 4 * (f % (D / 4));
+  };
+  auto load_pass = [&](int base) {
 #pragma unroll
-      for (int j = 0; j < JS; ++j) {
-        const int f = threadIdx.x + 256 * j;
-        if (f < n4) {
-          const int rr = f / (D / 4);
-          const int k = (int)(((float)rr + 0.5f) * inv_nh);
-          const float* src = rope.src.part + (long)k * rope.src.slab + (long)b * ntot * D +
-                             (long)head_of(rr - k * nh) * D + 4 * (f % (D / 4));
-          sv[j] = *reinterpret_cast<const f32x4*>(src);
-        }
-      }
+    for (int j = 0; j < JS; ++j) {
+      const int f = base + threadIdx.x + 256 * j;
+      if (f < n4) sv[j] = *reinterpret_cast<const f32x4*>(slab_src(f));
     }
+  };
+  auto store_pass = [&](int base) {
+#pragma unroll
+    for (int j = 0; j < JS; ++j) {
+      const int f = base + threadIdx.x + 256 * j;
+      if (f < n4) *reinterpret_cast<f32x4*>(stage + 4 * f) = sv[j];
+    }
+  };
+  auto pro_issue = [&]() {
+    if (staged) load_pass(0);
     rl.issue(rope.src, b, act ? h : 0, act, sub, Hq, Hkv, rope.cos_sin, pos_b);
     if (act && hs >= nq && writer) slot = slot_b;
   };
@@ -571,10 +581,10 @@ paged_decode_kernel(const bf16_t* __restrict__ q, long q_stride,
       int e0, e1;
       rope_lane_offsets<D, true>(sub, e0, e1);
       if (staged) {
-#pragma unroll
-        for (int j = 0; j < JS; ++j) {
-          const int f = threadIdx.x + 256 * j;
-          if (f < n4) *reinterpret_cast<f32x4*>(stage + 4 * f) = sv[j];
+        store_pass(0);
+        for (int base = JS * 256; base < n4; base += JS * 256) {   // further passes
+          load_pass(base);
+          store_pass(base);
         }
         __syncthreads();
         if (act) {

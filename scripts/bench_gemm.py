@@ -91,6 +91,19 @@ def consumer_of(name: str) -> str:
     return "plain"
 
 
+# q heads per KV head of each QKV shape: the decode attention stages the QKV split-K slabs of a
+# (sequence, KV head) in LDS while sk * (G + 2) <= 68 (csrc/kernels/attention.hip); past that
+# it sums them one round trip per slab, which costs attention more than the split saves
+QKV_GROUP = {"qkv_8b": 4, "qkv_70b_tp8": 8, "qkv_70b": 8, "qkv_70b_tp4": 8, "qkv_405b_tp8": 16,
+             "qkv_qwen32b": 5, "qkv_qwen32b_tp2": 5, "qkv_codellama34b": 8,
+             "qkv_falcon3_7b": 3, "qkv_scout": 5}
+
+
+def qkv_max_sk(name: str) -> int:
+    g = QKV_GROUP.get(name)
+    return 68 // (g + 2) if g else 1 << 30
+
+
 def graph_time(fn, iters, rounds=3):
     torch.cuda.synchronize()
     fn(0)
@@ -221,6 +234,8 @@ def main():
             tb = graph_time(base, a.iters)
             cands = candidates(M, N, K, swiglu) if (a.tune or a.sweep or a.check) else \
                 [c for c in [gemm.choose(M, N, K, swiglu)] if c[0] >= 0]
+            if cons == "defer":
+                cands = [c for c in cands if c[1] <= qkv_max_sk(name)]
             if a.packed:
                 cands = [(c, sk) for c in gemm.PACKED_CFGS for sk in {s for _, s in cands}
                          if gemm.valid(N, K, swiglu, c, sk, M=M)
@@ -232,6 +247,7 @@ def main():
                 cands = ([(pc, ps)] if pc >= 0 else []) + [
                     (c, sk) for c in gemm.WGPACK_CFGS for sk in (1, 2, 3, 4, 6, 8, 12, 16)
                     if gemm.valid(N, K, swiglu, c, sk, M=M)
+                    and (cons != "defer" or sk <= qkv_max_sk(name))
                     and K % (sk * gemm.cfg_kc(c)) == 0 and (N // gemm.cfg_rows(c)) * sk <= 4096
                     and (N // gemm.cfg_rows(c)) * sk >= 64]
             if not cands:

@@ -433,12 +433,15 @@ def test_fill_ids():
 
 
 @pytest.mark.parametrize("Hq,Hkv,D,bs,bias,qkn,split", [
-    (32, 8, 128, 128, False, False, True),      # Llama-3-8B decode (split-K QKV)
-    (32, 8, 128, 128, False, False, False),
-    (28, 4, 128, 64, True, False, True),        # Qwen2 (bias)
-    (16, 8, 128, 32, False, True, True),        # Qwen3 (qk-norm)
-    (12, 12, 64, 32, True, True, False),
-    (64, 8, 128, 128, False, False, True)])     # 70B-like G = 8
+    (32, 8, 128, 128, False, False, 4),         # Llama-3-8B decode (split-K 4 QKV)
+    (32, 8, 128, 128, False, False, 0),
+    (28, 4, 128, 64, True, False, 4),           # Qwen2 (bias)
+    (16, 8, 128, 32, False, True, 4),           # Qwen3 (qk-norm)
+    (12, 12, 64, 32, True, True, 0),
+    (64, 8, 128, 128, False, False, 4),         # 70B-like G = 8: slabs staged in 2 passes
+    (8, 1, 128, 128, False, False, 4),          # a 70B TP8 rank: 8 q heads on 1 KV head
+    (8, 1, 128, 128, False, False, 8),          # past the LDS staging capacity: per-lane sum
+    (8, 1, 128, 128, False, False, 3)])         # one staging pass
 @pytest.mark.parametrize("P,dyn", [(1, None), (4, None), (8, 3)])
 def test_decode_rope_fused_matches_two_kernels(Hq, Hkv, D, bs, bias, qkn, split, P, dyn):
     """eia_paged_decode_rope == rope_qkv_cache + paged_decode, bit for bit (q, out, K/V cache)."""
@@ -458,7 +461,7 @@ def test_decode_rope_fused_matches_two_kernels(Hq, Hkv, D, bs, bias, qkn, split,
                           for i, l in enumerate(lens)], dtype=torch.int32, device=DEV)
     N = (Hq + 2 * Hkv) * D
     if split:
-        qkv = SplitK(torch.randn(4, B, N, device=DEV) * 0.5, 4, B, N, None)
+        qkv = SplitK(torch.randn(split, B, N, device=DEV) * 0.5, split, B, N, None)
     else:
         qkv = torch.randn(B, N, device=DEV, dtype=BF)
     b = torch.randn(N, device=DEV, dtype=BF) if bias else None
