@@ -26,6 +26,12 @@ for s in $STEPS; do
              --extras off --verbose ;;
     mistral) run endpoint_mistral 600 python bench.py --model mistral-7b --steps 3 --warmup 1 \
                --verbose ;;
+    codellama) run endpoint_codellama 900 python bench.py --model codellama-34b --steps 2 \
+                 --warmup 1 --verbose ;;
+    dsqwen) run endpoint_dsqwen 900 python bench.py --model deepseek-r1-distill-qwen-32b --steps 2 \
+              --warmup 1 --verbose ;;
+    dsllama) run endpoint_dsllama 600 python bench.py --model deepseek-r1-distill-llama8b --steps 3 \
+               --warmup 1 --verbose ;;
     tei) run tei 900 python scripts/bench_tei.py --window ${TEI_WINDOW:-10} --out gpurun_out/tei.md ;;
     tune_tp8) run tune_tp8 900 python scripts/bench_gemm.py --tune --m ${TP8_M:-33 40 48 65 72 80} \
                 --shapes qkv_70b_tp8 o_70b_tp8 gate_up_70b_tp8 down_70b_tp8 \
