@@ -135,3 +135,63 @@ def test_tp2_sync_mode_sharded_sampling(tmp_path):
     ref = _run(path, d, 1, temperature=0.8, delayed=False, **FILTERS)
     assert _run(path, d, 2, temperature=0.8, delayed=False, **FILTERS) == ref
     assert _run(path, d, 2, temperature=0.8, delayed=False) == _run(path, d, 1, temperature=0.8)
+
+
+def _splitk_epilogue_worker(rank, world, port, q):
+    import os
+    try:
+        os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
+                          WORLD_SIZE=str(world))
+        from enterprise_inference_amd.models.layers import PendingAllReduce, RMSNorm
+        from enterprise_inference_amd.ops.gemm import SplitK
+        from enterprise_inference_amd.parallel import state
+        state.init_distributed(tp_size=world, backend="gloo")
+        g = torch.Generator().manual_seed(100 + rank)
+        T, H, sk = 5, 64, 3
+        part = torch.randn(sk, T, H, generator=g)
+        res0 = torch.randn(T, H, generator=torch.Generator().manual_seed(7)).to(torch.bfloat16)
+        norm = RMSNorm(H, 1e-5, dtype=torch.bfloat16, device="cpu")
+        with torch.no_grad():
+            norm.weight.fill_(1.25)
+        # the decode epilogue as RowParallelLinear hands it over at TP > 1 (split-K slabs)
+        r1 = res0.clone()
+        out1, r1 = norm(PendingAllReduce(SplitK(part.clone(), sk, T, H)), r1)
+        # the same partial sums as one bf16 tensor
+        r2 = res0.clone()
+        out2, r2 = norm(PendingAllReduce(SplitK(part.clone(), sk, T, H).materialize()), r2)
+        m = PendingAllReduce(SplitK(part.clone(), sk, T, H)).materialize()
+        full = [torch.empty_like(part) for _ in range(world)]
+        import torch.distributed as dist
+        dist.all_gather(full, part)
+        want = sum(p.sum(0).to(torch.bfloat16).float() for p in full)
+        ok = (torch.equal(out1, out2) and torch.equal(r1, r2)
+              and torch.allclose(m.float(), want, atol=0.05, rtol=0.02))
+        state.destroy_distributed()
+        q.put((rank, ok))
+    except Exception as e:   # noqa: BLE001
+        q.put((rank, repr(e)))
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_splitk_slabs_through_deferred_allreduce_norm(world):
+    """TP > 1 decode epilogue with the row-parallel GEMM's split-K slabs deferred
+    (PendingAllReduce(SplitK)): the residual add + RMSNorm consumer gives exactly what the
+    materialised bf16 partial sums give, over gloo (the custom xGMI kernel sums the slabs
+    while staging; tests/test_custom_allreduce_gpu.py checks that form bit for bit)."""
+    import socket
+
+    import torch.multiprocessing as mp
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    ps = [ctx.Process(target=_splitk_epilogue_worker, args=(r, world, port, q))
+          for r in range(world)]
+    for p in ps:
+        p.start()
+    res = dict(q.get(timeout=180) for _ in range(world))
+    for p in ps:
+        p.join(30)
+    assert all(v is True for v in res.values()), res
