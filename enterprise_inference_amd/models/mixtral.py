@@ -105,8 +105,9 @@ class FusedMoE(nn.Module):
         else:
             w, ids = moe_ops.topk_route(router_logits, self.k, self.renormalize, self.scoring)
         if self.scale_input:
-            # Llama-4 applies the routing score to the expert input (k = 1)
-            x = (x.float() * w[:, :1]).to(x.dtype)
+            # Llama-4 applies the routing score to the expert input (k = 1), as the reference
+            # model does: bf16 score x bf16 activation (one elementwise launch)
+            x = x * w[:, :1].to(x.dtype)
             w = torch.ones_like(w)
         if self.a2a:
             from ..parallel.expert_parallel import moe_all_to_all_replicated
@@ -264,7 +265,8 @@ class Llama4Attention(LlamaAttention):
         from ..ops import gemm
 
         T = h.shape[0]
-        qkv = gemm.linear(h, self.qkv_proj.weight)
+        # split-K QKV slabs are summed inside the RoPE / KV-write kernel (no reduce launch)
+        qkv = gemm.linear(h, self.qkv_proj.weight, defer_reduce=True)
         q = rope_qkv_cache(qkv, md.positions, self.rotary, md.slot_mapping, kv[0], kv[1],
                            self.num_heads, self.num_kv_heads, self.head_dim,
                            bias=self.qkv_proj.bias,
@@ -272,9 +274,17 @@ class Llama4Attention(LlamaAttention):
                            k_norm_w=self.ones if self.qk_l2 else None,
                            norm_eps=self.cfg.rms_norm_eps)
         if self.temp_tuning:
-            pos = md.positions.float()
-            sc = torch.log1p(torch.floor((pos + 1.0) / self.floor_scale)) * self.attn_scale + 1.0
-            q = (q.float() * sc[:, None, None]).to(q.dtype)
+            # the per-position temperature is the same for every NoPE layer of the step:
+            # computed once per step (cached on the step's metadata), applied in fp32
+            key = (self.floor_scale, self.attn_scale)
+            cached = getattr(md, "_l4_attn_temp", None)
+            if cached is None or cached[0] != key:
+                pos = md.positions.float()
+                sc = torch.log1p(torch.floor((pos + 1.0) / self.floor_scale)) * self.attn_scale \
+                    + 1.0
+                cached = (key, sc[:, None, None])
+                md._l4_attn_temp = cached
+            q = (q * cached[1]).to(q.dtype)
         o = attention(q, kv[0], kv[1], md, self.scale, None, self.chunk_size)
         return self.o_proj(o.view(T, self.num_heads * self.head_dim), defer_reduce=True)
 
@@ -291,7 +301,11 @@ class Llama4MoE(nn.Module):
         self.shared_expert.down_proj.reduce_results = False   # one all-reduce for the sum
 
     def forward(self, x):
-        routed = self.experts(x, self.router(x), reduce=False)
+        if self.router.bias is None and x.dim() == 2:
+            # router GEMM + sigmoid top-1 in one kernel (moe.hip route_kernel)
+            routed = self.experts(x, None, reduce=False, router_w=self.router.weight)
+        else:
+            routed = self.experts(x, self.router(x), reduce=False)
         s = self.shared_expert.down_proj(self.shared_expert.gate_up_proj.forward_act_and_mul(x))
         return _deferred_reduce(routed + s)
 
