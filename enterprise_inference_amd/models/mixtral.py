@@ -108,7 +108,7 @@ class FusedMoE(nn.Module):
             # Llama-4 applies the routing score to the expert input (k = 1), as the reference
             # model does: bf16 score x bf16 activation (one elementwise launch)
             x = x * w[:, :1].to(x.dtype)
-            w = torch.ones_like(w)
+            w = self._unit_weights(w)
         if self.a2a:
             from ..parallel.expert_parallel import moe_all_to_all_replicated
             return moe_all_to_all_replicated(x, w, ids, self.w13, self.w2, self.e_lo,
@@ -120,6 +120,18 @@ class FusedMoE(nn.Module):
         if reduce and state.tp_size() > 1:
             out = comm.all_reduce(out)
         return out
+
+    def _unit_weights(self, w: torch.Tensor) -> torch.Tensor:
+        """All-ones routing weights shaped like ``w``: a slice of a cached buffer (no fill
+        launch per layer and step), grown outside graph capture only."""
+        buf = getattr(self, "_ones", None)
+        if (buf is None or buf.device != w.device or buf.shape[0] < w.shape[0]
+                or buf.shape[1] != w.shape[1]):
+            if torch.cuda.is_available() and torch.cuda.is_current_stream_capturing():
+                return torch.ones_like(w)
+            buf = torch.ones(max(256, w.shape[0]), w.shape[1], dtype=w.dtype, device=w.device)
+            self._ones = buf
+        return buf[:w.shape[0]]
 
     @property
     def a2a(self) -> bool:
