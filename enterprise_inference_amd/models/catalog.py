@@ -62,6 +62,11 @@ PRESETS: Dict[str, dict] = {
     # profiled on one GPU (scripts/gpu_model_steps.sh).  A profiling proxy, not a real model.
     "eia/Llama-3.3-70B-TP8-rank": _llama(8192, 3584, 80, 8, 1, head_dim=128, vocab_size=16032,
                                          bos_token_id=1, eos_token_id=[2]),
+    # ONE rank of Llama-3.1-405B at TP 8 (the reference's 405B deployment,
+    # core/playbooks/deploy-inference-models.yml:1884; sizing-guide.md:82-89): 16 q / 1 kv heads
+    # x 128, I 6656, 126 layers, LM head 16032 rows -- ~101 GB, the same per-rank profiling proxy.
+    "eia/Llama-3.1-405B-TP8-rank": _llama(16384, 6656, 126, 16, 1, head_dim=128, vocab_size=16032,
+                                          bos_token_id=1, eos_token_id=[2]),
     "meta-llama/Llama-3.2-3B-Instruct": _llama(3072, 8192, 28, 24, 8, tie_word_embeddings=True,
                                                rope_scaling={**_LLAMA31_ROPE, "factor": 32.0}),
     "deepseek-ai/DeepSeek-R1-Distill-Llama-8B": _llama(4096, 14336, 32, 32, 8,
@@ -149,6 +154,7 @@ SHORT_NAMES: Dict[str, str] = {
     "cpu-qwen3-4b": "Qwen/Qwen3-4B-Instruct-2507",
     "opt-125m": "facebook/opt-125m",
     "llama-70b-tp8-rank": "eia/Llama-3.3-70B-TP8-rank",
+    "llama-405b-tp8-rank": "eia/Llama-3.1-405B-TP8-rank",
     # BASELINE.json config names
     "Llama-3-8B": "meta-llama/Llama-3.1-8B-Instruct",
     "Llama-3-70B": "meta-llama/Llama-3.3-70B-Instruct",

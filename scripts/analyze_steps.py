@@ -43,6 +43,7 @@ def main() -> int:
                        for r in rows[ab[0] + 1:ab[1] + 1])
         pairs = sorted(zip(ends[:-1], ends[1:]), key=ktime)[-nsteps:]
     agg = collections.defaultdict(list)
+    by_grid = collections.defaultdict(list)  # (kernel, grid) -> durations: tells one GEMM shape from another
     gaps = collections.defaultdict(list)     # idle before a kernel, keyed by (previous, kernel)
     spans, busy, launches = [], [], []
     for a, b in pairs:
@@ -57,7 +58,10 @@ def main() -> int:
         busy.append(k)
         launches.append(len(ks))
         for r in ks:
-            agg[short(r["Kernel_Name"])].append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3)
+            d = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3
+            agg[short(r["Kernel_Name"])].append(d)
+            grid = "x".join(r.get(k, "?") for k in ("Grid_Size_X", "Grid_Size_Y", "Grid_Size_Z"))
+            by_grid[(short(r["Kernel_Name"])[:60], grid)].append(d)
     n = len(pairs)
     span, kern = sum(spans) / n, sum(busy) / n
     print(f"### {title}\n")
@@ -68,6 +72,11 @@ def main() -> int:
     for name, v in sorted(agg.items(), key=lambda kv: -sum(kv[1])):
         per = sum(v) / n
         print(f"| {name} | {len(v) / n:.1f} | {per:.1f} | {100 * per / kern:.1f} | {sum(v) / len(v):.2f} |")
+    print("\nBy kernel and grid (threads x, y, z): one row per GEMM shape / launch form:\n")
+    print("| kernel | grid | launches/step | avg us | us/step |")
+    print("|---|---|---:|---:|---:|")
+    for (name, grid), v in sorted(by_grid.items(), key=lambda kv: -sum(kv[1]))[:24]:
+        print(f"| {name} | {grid} | {len(v) / n:.1f} | {sum(v) / len(v):.2f} | {sum(v) / n:.1f} |")
     # one step's copies and their neighbours, relative times (us)
     a, b = pairs[len(pairs) // 2]
     seq = rows[a - 2:b + 3]

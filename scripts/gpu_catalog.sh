@@ -54,6 +54,20 @@ for s in $STEPS; do
           --steps 3 --warmup 1 > gpurun_out/abtable_$t.log 2>&1 || { tail -20 gpurun_out/abtable_$t.log; exit 1; }
         echo "table=$t $(grep -o '"value": [0-9.]*\|"tpot_p50_ms": [0-9.]*' gpurun_out/abtable_$t.log | tr '\n' ' ')"
       done ;;
+    tune_405) run tune_405 900 python scripts/bench_gemm.py --tune --m ${T405_M:-33 40 48 65 72} \
+                --shapes qkv_405b_tp8 o_405b_tp8 gate_up_405b_tp8 down_405b_tp8 lm_head_405b_tp8 \
+                --out gpurun_out/gemm_tuning.json
+              run tune_405_wg 900 env EIA_GEMM_TUNING=gpurun_out/gemm_tuning.json \
+                python scripts/bench_gemm.py --tune --wgpack --m ${T405_M:-33 40 48 65 72} \
+                --shapes qkv_405b_tp8 o_405b_tp8 gate_up_405b_tp8 down_405b_tp8 lm_head_405b_tp8 \
+                --out gpurun_out/gemm_tuning.json ;;
+    # the 405B TP8 rank proxy (~101 GB) at the reference's 405B chatbot row (35 users, 128/128)
+    rank405) run engine_405_rank 900 env EIA_GEMM_TUNING=${T405_TABLE:-enterprise_inference_amd/ops/gemm_tuning.json} \
+               python bench.py --mode engine --model llama-405b-tp8-rank --users 35 --steps 2 \
+               --warmup 1 --verbose ;;
+    steps405) EIA_GEMM_TUNING=${T405_TABLE:-enterprise_inference_amd/ops/gemm_tuning.json} \
+                MODEL=llama-405b-tp8-rank TAG=405b_rank BENCH_ARGS="--users 35" LIMIT=900 \
+                bash scripts/gpu_model_steps.sh > gpurun_out/steps405.log 2>&1 || exit 1 ;;
     sweep_tp8) run sweep_tp8 900 python scripts/bench_gemm.py --sweep --all --m ${GEMM_M:-65} \
                  --shapes qkv_70b_tp8 o_70b_tp8 gate_up_70b_tp8 down_70b_tp8 ;;
     *) echo "unknown step $s"; exit 2 ;;
