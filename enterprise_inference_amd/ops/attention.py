@@ -255,6 +255,9 @@ def paged_prefill(q: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tensor,
 
 
 _FUSED_ENV = os.environ.get("EIA_DECODE_FUSED_ROPE", "1") != "0"
+# rows of D fp32 the fused decode prologue stages split-K QKV slabs in (the kernel's merge
+# buffer, NW * 17 = 68 rows; csrc/kernels/attention.hip `staged`): sk * (q heads per group + 2)
+DECODE_STAGE_ROWS = 68
 
 
 def decode_rope_attention(qkv, md: AttentionMetadata, k_cache: torch.Tensor,
@@ -278,6 +281,12 @@ def decode_rope_attention(qkv, md: AttentionMetadata, k_cache: torch.Tensor,
     if k_cache.shape[2] % 32 != 0 or md.positions is None:
         return None
     split = isinstance(qkv, SplitK)
+    if split and qkv.sk * (min(16, num_heads // num_kv_heads) + 2) > DECODE_STAGE_ROWS:
+        # more slabs than the prologue stages in LDS (it would sum them one round trip per
+        # slab): one reduce launch first -- a tall split-K (e.g. the 405B TP8 rank's QKV,
+        # K 16384) still beats the library GEMM with it (scripts/bench_gemm.py "defer" rows)
+        qkv = qkv.materialize()
+        split = False
     src = qkv.part if split else qkv
     if not (use_hip(src, k_cache) and k_cache.dtype == torch.bfloat16):
         return None

@@ -82,7 +82,8 @@ def consumer_of(name: str) -> str:
                residual add + RMSNorm kernel (splitk_add_rmsnorm / fused_add_rms_norm; at TP > 1
                the fused all-reduce kernel, which stages them the same way);
       "defer"  QKV: the slabs are summed in the decode attention's fused prologue (its cost per
-               slab is small and paid by attention, not timed here);
+               slab is small and paid by attention, not timed here) while they fit its LDS
+               staging; a larger split is timed with the reduce launch the engine then runs;
       "plain"  everything else (LM head, SwiGLU): the op as the engine calls it."""
     if name.startswith(("o_", "down_", "shared_down")):
         return "norm"
@@ -93,7 +94,7 @@ def consumer_of(name: str) -> str:
 
 # q heads per KV head of each QKV shape: the decode attention stages the QKV split-K slabs of a
 # (sequence, KV head) in LDS while sk * (G + 2) <= 68 (csrc/kernels/attention.hip); past that
-# it sums them one round trip per slab, which costs attention more than the split saves
+# the engine reduces them in a launch of their own first (ops/attention.py), timed with the GEMM
 QKV_GROUP = {"qkv_8b": 4, "qkv_70b_tp8": 8, "qkv_70b": 8, "qkv_70b_tp4": 8, "qkv_405b_tp8": 16,
              "qkv_qwen32b": 5, "qkv_qwen32b_tp2": 5, "qkv_codellama34b": 8,
              "qkv_falcon3_7b": 3, "qkv_scout": 5}
@@ -226,16 +227,19 @@ def main():
                         return gemm.splitk_add_rmsnorm(y, res, wn, 1e-5)
                     return norm_ops.fused_add_rms_norm(y, res, wn, 1e-5)
             elif cons == "defer":
+                cap = qkv_max_sk(name)
+
                 def skinny_call(i, cfg, sk, src):
-                    return gemm.skinny(x, src[i % pool], cfg=cfg, sk=sk, defer_reduce=True)
+                    # past the attention's staging capacity the engine reduces the slabs first
+                    # (ops/attention.py decode_rope_attention): time that launch too
+                    return gemm.skinny(x, src[i % pool], cfg=cfg, sk=sk,
+                                       defer_reduce=sk <= cap)
             else:
                 def skinny_call(i, cfg, sk, src):
                     return gemm.skinny(x, src[i % pool], cfg=cfg, sk=sk)
             tb = graph_time(base, a.iters)
             cands = candidates(M, N, K, swiglu) if (a.tune or a.sweep or a.check) else \
                 [c for c in [gemm.choose(M, N, K, swiglu)] if c[0] >= 0]
-            if cons == "defer":
-                cands = [c for c in cands if c[1] <= qkv_max_sk(name)]
             if a.packed:
                 cands = [(c, sk) for c in gemm.PACKED_CFGS for sk in {s for _, s in cands}
                          if gemm.valid(N, K, swiglu, c, sk, M=M)
@@ -247,7 +251,6 @@ def main():
                 cands = ([(pc, ps)] if pc >= 0 else []) + [
                     (c, sk) for c in gemm.WGPACK_CFGS for sk in (1, 2, 3, 4, 6, 8, 12, 16)
                     if gemm.valid(N, K, swiglu, c, sk, M=M)
-                    and (cons != "defer" or sk <= qkv_max_sk(name))
                     and K % (sk * gemm.cfg_kc(c)) == 0 and (N // gemm.cfg_rows(c)) * sk <= 4096
                     and (N // gemm.cfg_rows(c)) * sk >= 64]
             if not cands:

@@ -440,8 +440,10 @@ def test_fill_ids():
     (12, 12, 64, 32, True, True, 0),
     (64, 8, 128, 128, False, False, 4),         # 70B-like G = 8: slabs staged in 2 passes
     (8, 1, 128, 128, False, False, 4),          # a 70B TP8 rank: 8 q heads on 1 KV head
-    (8, 1, 128, 128, False, False, 8),          # past the LDS staging capacity: per-lane sum
-    (8, 1, 128, 128, False, False, 3)])         # one staging pass
+    (8, 1, 128, 128, False, False, 8),          # past the LDS staging capacity: reduced first
+    (8, 1, 128, 128, False, False, 3),          # one staging pass
+    (16, 1, 128, 128, False, False, 3),         # a 405B TP8 rank (G 16): two staging passes
+    (16, 1, 128, 128, False, False, 8)])        # its tall split-K QKV: reduced first
 @pytest.mark.parametrize("P,dyn", [(1, None), (4, None), (8, 3)])
 def test_decode_rope_fused_matches_two_kernels(Hq, Hkv, D, bs, bias, qkn, split, P, dyn):
     """eia_paged_decode_rope == rope_qkv_cache + paged_decode, bit for bit (q, out, K/V cache)."""
