@@ -83,9 +83,12 @@ def _load_tuning(section: str = "entries") -> dict:
     for k, v in raw.get(section, {}).items():
         mt, n, kk, sw = (int(x) for x in k.split(","))
         out[(mt, n, kk, bool(sw))] = (int(v[0]), int(v[1]))
+        if len(v) > 2:      # wg_entries: the measured gain over the plain pick, % of its time
+            _WG_GAIN[(mt, n, kk, bool(sw))] = float(v[2])
     return out
 
 
+_WG_GAIN: dict = {}
 _TUNED = _load_tuning()
 _TUNED_WG = _load_tuning("wg_entries")
 
@@ -218,6 +221,7 @@ def attach_wg_packed(model: torch.nn.Module, budget_bytes: int, max_m: int = MAX
     from ..models import layers as L
     plan = []                    # (family, weight, key)
     uses = {}                    # dense family -> batch buckets whose packed pick it serves
+    gains = {}                   # dense family -> mean measured gain of its picks (%)
     for mod in model.modules():
         w = getattr(mod, "weight", None)
         if not isinstance(w, torch.Tensor) or w.dim() != 2 or w.dtype != torch.bfloat16 or \
@@ -234,9 +238,13 @@ def attach_wg_packed(model: torch.nn.Module, budget_bytes: int, max_m: int = MAX
             for waves in wg_layouts(N, K, sw, max_m):
                 fam = (0, N, K, sw, waves)
                 plan.append((fam, w, (waves, sw)))
-                uses[fam] = sum(1 for (mt, n, k, s_), (c, _) in _TUNED_WG.items()
-                                if (n, k, s_) == (N, K, sw) and mt <= m_bucket(max_m)
-                                and c & 1024 and cfg_waves(c) == waves)
+                keys = [key for key, (c, _) in _TUNED_WG.items()
+                        if key[1:] == (N, K, sw) and key[0] <= m_bucket(max_m)
+                        and c & 1024 and cfg_waves(c) == waves]
+                uses[fam] = len(keys)
+                g = [_WG_GAIN[k_] for k_ in keys if k_ in _WG_GAIN]
+                if g:
+                    gains[fam] = sum(g) / len(g)
     moe_mode = os.environ.get("EIA_MOE_WG_PACK", "1")
     if moe_mode != "0":
         # MoE expert gate_up [E, 2I, H] (the grouped skinny kernel's decode form, cfg 1 / 3)
@@ -262,7 +270,7 @@ def attach_wg_packed(model: torch.nn.Module, budget_bytes: int, max_m: int = MAX
         if (id(w), key) not in seen:
             seen.add((id(w), key))
             size[pri] = size.get(pri, 0) + w.numel() * w.element_size()
-    take, total = select_wg_families(size, budget_bytes, uses)
+    take, total = select_wg_families(size, budget_bytes, uses, gains)
     if total == 0:
         return 0
     for pri, w, key in plan:
@@ -284,14 +292,18 @@ def attach_wg_packed(model: torch.nn.Module, budget_bytes: int, max_m: int = MAX
     return total
 
 
-def select_wg_families(size: dict, budget_bytes: int, uses: dict = None):
+def select_wg_families(size: dict, budget_bytes: int, uses: dict = None, gains: dict = None):
     """Families (tuples led by their priority: 0 dense, 1 MoE gate_up, 2 MoE down) to pack:
-    in priority order, smallest first within one (equal sizes: the layout serving more batch
-    buckets first), each taken whole when it still fits."""
+    in priority order; within one, the largest measured gain first (``gains``: the tuner's
+    packed-vs-plain saving in % of the GEMM's time -- for weight-streaming GEMMs the time saved
+    per byte of copy, so the greedy fill approximates the best set), then smallest first (equal
+    sizes: the layout serving more batch buckets first); each taken whole when it still fits.
+    Families without a recorded gain rank after those with one."""
     uses = uses or {}
+    gains = gains or {}
     total = 0
     take = set()
-    for fam in sorted(size, key=lambda f: (f[0], size[f], -uses.get(f, 0))):
+    for fam in sorted(size, key=lambda f: (f[0], -gains.get(f, -1.0), size[f], -uses.get(f, 0))):
         if total + size[fam] <= budget_bytes:
             total += size[fam]
             take.add(fam)

@@ -309,7 +309,9 @@ def main():
                 packed = [(t, c) for t, c in full if c[0] & 1024]
                 ref_t = plain[0][0] if plain else b["hip"]
                 if packed and packed[0][0] < 0.99 * ref_t:
-                    tuned_wg[key] = list(packed[0][1])
+                    # third element: the gain in % of the plain time, which ranks the packed
+                    # copies when the memory budget cannot hold them all (attach_wg_packed)
+                    tuned_wg[key] = list(packed[0][1]) + [round(100.0 * (1 - packed[0][0] / ref_t), 1)]
                 else:
                     tuned_wg.pop(key, None)
                 print(json.dumps({"shape": name, "bucket": mt, "rows": b["rows"],

@@ -138,3 +138,35 @@ def test_wg_family_selection_70b_tp1():
     # a budget that cannot hold the expert gate_up still packs the down projections
     take, _ = select_wg_families(mix, 40e9)
     assert take == {(0, 6144, 4096, False, 4), (2,)}
+
+
+def test_wg_family_selection_by_gain_405b_tp8_rank():
+    """The 405B TP8 rank (101 GB) with the runner's default budget (187 GB free after the load,
+    38 % of the 288 GiB device kept: ~70 GB): ranked by the tuner's measured gain, the QKV and gate_up copies (15-16 %, 12-16 %)
+    go in before down (6-8 %), which no longer fits -- smallest-first would have packed down and
+    O and left gate_up, the largest saving, row-major."""
+    from enterprise_inference_amd.ops.gemm import select_wg_families
+    L = 126
+    fam = {(0, 2304, 16384, False, 3): L * 2304 * 16384 * 2,
+           (0, 16384, 2048, False, 2): L * 16384 * 2048 * 2,
+           (0, 13312, 16384, True, 3): L * 13312 * 16384 * 2,
+           (0, 16384, 6656, False, 3): L * 16384 * 6656 * 2,
+           (0, 16032, 16384, False, 3): 16032 * 16384 * 2}
+    gains = {(0, 2304, 16384, False, 3): 15.8, (0, 16384, 2048, False, 2): 4.7,
+             (0, 13312, 16384, True, 3): 14.2, (0, 16384, 6656, False, 3): 7.0,
+             (0, 16032, 16384, False, 3): 3.9}
+    budget = int(187e9 - 0.38 * 288 * 2 ** 30)
+    take, total = select_wg_families(fam, budget, None, gains)
+    assert (0, 13312, 16384, True, 3) in take and (0, 2304, 16384, False, 3) in take
+    assert (0, 16384, 6656, False, 3) not in take
+    assert total <= budget
+    # without gains: the old smallest-first order
+    take0, _ = select_wg_families(fam, budget)
+    assert (0, 13312, 16384, True, 3) not in take0 and (0, 16384, 6656, False, 3) in take0
+
+
+def test_wg_gain_loaded_from_table():
+    """A wg_entries value may carry a third element, the packed pick's measured gain (%)."""
+    from enterprise_inference_amd.ops import gemm
+    assert gemm._TUNED_WG[(3, 13312, 16384, True)] == (1043, 2)
+    assert gemm._WG_GAIN[(3, 13312, 16384, True)] > 5.0
