@@ -53,3 +53,22 @@ def test_wg_packed_selection(monkeypatch):
     assert (cfg, sk) == (1024 + 17, 4) and wp is packed
     assert gemm.choose_packed(20, N, K, False, w) is None            # layout 4 not attached
     assert gemm.choose_packed(5, N, K, False, w) is None             # bucket 1: no packed pick
+
+
+def test_every_catalog_decode_shape_has_all_batch_buckets():
+    """Every decode GEMM shape the tuner knows (the catalog's models, TP ranks included) has a
+    table entry at each 16-row bucket up to 128 rows: a missing bucket would silently fall back
+    to hipBLASLt at that batch size (1-3 TB/s there, profiles/gemm_tune_tp8_all_buckets_r6.log)."""
+    import json
+    bg = _mod()
+    with open(os.path.join(ROOT, "enterprise_inference_amd", "ops", "gemm_tuning.json")) as f:
+        table = json.load(f)["entries"]
+    gaps = {}
+    for name, (N, K, sw) in bg.SHAPES.items():
+        if "probe" in name or name.startswith("gate_up_8b_w"):
+            continue
+        have = {int(k.split(",")[0]) for k in table if k.split(",", 1)[1] == f"{N},{K},{int(sw)}"}
+        miss = [m for m in range(1, 9) if m not in have]
+        if miss:
+            gaps[name] = miss
+    assert not gaps, gaps
