@@ -70,6 +70,16 @@ SHAPES = {  # name: (N, K, swiglu)
     "qkv_scout": (7168, 5120, False), "o_scout": (5120, 5120, False),
     "shared_gate_up_scout": (16384, 5120, True), "shared_down_scout": (5120, 8192, False),
     "lm_head_scout": (202048, 5120, False),
+    # Llama-3.2-3B (attention projections = the Falcon3-7B shapes), Qwen3-4B-Instruct-2507 and
+    # Qwen3-1.7B (the reference serves these on Xeon, deploy-inference-models.yml; here on GPU)
+    "gate_up_llama3b": (16384, 3072, True), "down_llama3b": (3072, 8192, False),
+    "lm_head_llama3b": (128256, 3072, False),
+    "qkv_qwen3_4b": (6144, 2560, False), "o_qwen3_4b": (2560, 4096, False),
+    "gate_up_qwen3_4b": (19456, 2560, True), "down_qwen3_4b": (2560, 9728, False),
+    "lm_head_qwen3_4b": (151936, 2560, False),
+    "qkv_qwen3_1_7b": (4096, 2048, False), "o_qwen3_1_7b": (2048, 2048, False),
+    "gate_up_qwen3_1_7b": (12288, 2048, True), "down_qwen3_1_7b": (2048, 6144, False),
+    "lm_head_qwen3_1_7b": (151936, 2048, False),
     # gate_up grid-size probes (8B K): 196 / 224 (the real shape) / 256 four-pair workgroups
     "gu_probe_196": (25088, 4096, True), "gu_probe_256": (32768, 4096, True),
 }
@@ -97,7 +107,7 @@ def consumer_of(name: str) -> str:
 # the engine reduces them in a launch of their own first (ops/attention.py), timed with the GEMM
 QKV_GROUP = {"qkv_8b": 4, "qkv_70b_tp8": 8, "qkv_70b": 8, "qkv_70b_tp4": 8, "qkv_405b_tp8": 16,
              "qkv_qwen32b": 5, "qkv_qwen32b_tp2": 5, "qkv_codellama34b": 8,
-             "qkv_falcon3_7b": 3, "qkv_scout": 5}
+             "qkv_falcon3_7b": 3, "qkv_scout": 5, "qkv_qwen3_4b": 4, "qkv_qwen3_1_7b": 2}
 
 
 def qkv_max_sk(name: str) -> int:
