@@ -181,6 +181,11 @@ gemm_skinny_kernel(const bf16_t* __restrict__ X, long ldx, const bf16_t* __restr
     if (Mtot <= 0) return;                                // uniform over the workgroup
     W += (long)e * w_estride;
     if (bias != nullptr) bias += (long)e * N;
+  } else {
+    // batches of more than 16*MT rows: grid.z = row blocks of 16*MT, run side by side -- the
+    // blocks of one weight tile stream it concurrently, the later reads hitting L2 / MALL
+    mbase = blockIdx.z * (MT * 16);
+    Mtot = min(MT * 16, M - mbase);
   }
 
   // rows of W owned by this wave's tiles
@@ -927,9 +932,11 @@ int check_shape(int N, int K, int sk, int mode, int cfg) {
 EIA_API int eia_gemm_skinny(const void* X, long ldx, const void* W, long ldw, const void* bias,
                             void* out, long ldo, int M, int N, int K, int sk, int mode, int cfg,
                             hipStream_t st) {
-  if (M < 1 || M > 128) return EIA_BAD_SHAPE;
+  // M <= 128: one row block; up to 256: row blocks of 128 on grid.z (main kernel only)
+  if (M < 1 || M > 256 || (M > 128 && (cfg & 128))) return EIA_BAD_SHAPE;
+  const int mt = M > 128 ? 8 : (M + 15) / 16;
   if (int rc = check_shape(N, K, sk, mode, cfg)) return rc;
-  if (!(cfg & 896) && ((kSpillCfg[(M + 15) / 16] >> (cfg & 63)) & 1ull)) return EIA_BAD_SHAPE;
+  if (!(cfg & 896) && ((kSpillCfg[mt] >> (cfg & 63)) & 1ull)) return EIA_BAD_SHAPE;
   if ((cfg & 1024) && ldw != K) return EIA_BAD_SHAPE;           // packed over the full K
   // 7-wave form: cfg 273 only (KC 128, 2 stages), spill-free up to 4 row tiles (M <= 64); at
   // 7 waves two share a SIMD, so the register budget is 256
@@ -938,9 +945,9 @@ EIA_API int eia_gemm_skinny(const void* X, long ldx, const void* W, long ldw, co
                          160 * 1024)
     return EIA_BAD_SHAPE;
   if ((ldx % 8) || (ldw % 8) || (ldo % 4) || ((cfg & 64) && ldw != K)) return EIA_BAD_SHAPE;
-  return dispatch_mt<false>((M + 15) / 16, cfg, static_cast<const bf16_t*>(X), ldx,
+  return dispatch_mt<false>(mt, cfg, static_cast<const bf16_t*>(X), ldx,
                             static_cast<const bf16_t*>(W), ldw, static_cast<const bf16_t*>(bias),
-                            out, ldo, M, N, K, sk, mode, 1, nullptr, nullptr, 0, st);
+                            out, ldo, M, N, K, sk, mode, (M + 127) / 128, nullptr, nullptr, 0, st);
 }
 
 // K9 grouped GEMM for MoE: W = [E][N][K]; expert e multiplies the rows

@@ -21,7 +21,8 @@ import torch.nn.functional as F
 from ..utils.cache_dir import resolve
 from ._dispatch import check, lib, ptr, stream, use_hip
 
-MAX_M = 128
+MAX_M = 256          # skinny kernel: one 128-row block, or two side by side on grid.z (129-256)
+ROW_BLOCK = 128
 KC = 256
 TARGET_WGS = int(os.environ.get("EIA_SKINNY_TARGET_WGS", "512"))
 DISABLE = os.environ.get("EIA_DISABLE_SKINNY_GEMM", "0") == "1"
@@ -106,9 +107,9 @@ def valid(N: int, K: int, swiglu: bool, cfg: int, sk: int, M: Optional[int] = No
         return (swiglu and cfg == 273 and (M is None or M <= 64)
                 and (N // 2) % (7 * 16) == 0)
     if cfg & 128:
-        if M is not None and glds_lds_bytes(cfg, M) > 160 * 1024:
+        if M is not None and (M > ROW_BLOCK or glds_lds_bytes(cfg, M) > 160 * 1024):
             return False
-    elif M is not None and (cfg & 63) in SPILL_CFGS.get(m_bucket(M), ()):
+    elif M is not None and (cfg & 63) in SPILL_CFGS.get(min(8, m_bucket(M)), ()):
         return False
     if swiglu:   # sk > 1: fp32 gate / up partials finished by eia_splitk_swiglu
         return (cfg & 1) == 1 and (N // 2) % (cfg_waves(cfg) * 16) == 0
@@ -181,6 +182,8 @@ def choose(M: int, N: int, K: int, swiglu: bool = False):
     key = (m_bucket(M), N, K, swiglu)
     if key in _TUNED and (_TUNED[key][0] < 0 or valid(N, K, swiglu, *_TUNED[key], M=M)):
         return _TUNED[key]
+    if M > ROW_BLOCK:       # two row blocks: only where the tuner measured them to win
+        return -1, 1
     cfg = 3 if m_bucket(M) >= 3 else 1
     if not valid(N, K, swiglu, cfg, 1, M=M):
         cfg = 2 if valid(N, K, swiglu, 2, 1, M=M) else 1

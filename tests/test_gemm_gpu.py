@@ -187,3 +187,57 @@ def test_skinny_wg_packed(M, N, K, swiglu):
             _check(out, ref, f"M={M} N={N} K={K} cfg={cfg} sk={sk}")
             n += 1
     assert n > 0
+
+
+@pytest.mark.parametrize("M", [129, 136, 200, 256])
+def test_skinny_two_row_blocks(M):
+    """Batches of 129-256 rows: two 128-row blocks side by side on grid.z, every output mode --
+    bf16 (+bias), fp32 split-K slabs, SwiGLU whole-K and split-K, workgroup-packed weights --
+    vs the fp32 oracle, and the consumers of the slabs (add + RMSNorm) at those rows."""
+    from enterprise_inference_amd.ops import gemm
+    torch.manual_seed(M)
+    K, N, I = 4096, 6144, 3584
+    x = torch.randn(M, K, device=DEV, dtype=BF)
+    w = (torch.randn(N, K, device=DEV) * K ** -0.5).to(BF)
+    b = torch.randn(N, device=DEV, dtype=BF)
+    ref = _ref(x, w, b)
+    ran = 0
+    for cfg in gemm.CFGS:
+        for sk in (1, 4):
+            if not gemm.valid(N, K, False, cfg, sk, M=M):
+                continue
+            _check(gemm.skinny(x, w, b, cfg=cfg, sk=sk), ref, f"M={M} cfg={cfg} sk={sk}")
+            ran += 1
+    assert ran > 0
+    for cfg in (1024 + 1, 1024 + 3, 1024 + 17, 1024 + 19):
+        if gemm.valid(N, K, False, cfg, 4, M=M):
+            wp = gemm.pack_weight_wg(w, cfg)
+            _check(gemm.skinny(x, wp, b, cfg=cfg, sk=4), ref, f"packed M={M} cfg={cfg}")
+    wg = (torch.randn(2 * I, K, device=DEV) * K ** -0.5).to(BF)
+    y = _ref(x, wg)
+    sref = F.silu(y[:, :I]) * y[:, I:]
+    for cfg in (1, 3, 17, 19):
+        for sk in (1, 4):
+            if gemm.valid(2 * I, K, True, cfg, sk, M=M):
+                _check(gemm.swiglu_gemm(x, wg, cfg=cfg, sk=sk), sref,
+                       f"swiglu M={M} cfg={cfg} sk={sk}")
+    # the down projection's slabs through the fused add + RMSNorm at these rows
+    H = 4096
+    wd = (torch.randn(H, 14336, device=DEV) * 14336 ** -0.5).to(BF)
+    xd = torch.randn(M, 14336, device=DEV, dtype=BF)
+    res = torch.randn(M, H, device=DEV, dtype=BF)
+    nw = (torch.rand(H, device=DEV) + 0.5).to(BF)
+    cfg = next(c for c in gemm.CFGS if gemm.valid(H, 14336, False, c, 8, M=M))
+    s = gemm.skinny(xd, wd, cfg=cfg, sk=8, defer_reduce=True)
+    assert isinstance(s, gemm.SplitK)
+    r0 = res.float() + _ref(xd, wd).to(BF).float()
+    out, r1 = gemm.splitk_add_rmsnorm(s, res.clone(), nw, 1e-5)
+    want = r0 * torch.rsqrt(r0.pow(2).mean(-1, keepdim=True) + 1e-5) * nw.float()
+    _check(out, want, f"add+rmsnorm M={M}")
+
+
+def test_linear_routes_past_128_rows_by_table_only():
+    """Past 128 rows the skinny kernel runs only where the table has a measured pick; an
+    untuned bucket stays on hipBLASLt."""
+    from enterprise_inference_amd.ops import gemm
+    assert gemm.choose(200, 384, 768) == (-1, 1)
